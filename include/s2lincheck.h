@@ -1,0 +1,234 @@
+/*
+ * s2lincheck.h — C ABI of libs2lincheck, the MI355X (gfx950) linearizability
+ * checker for the S2 stream model.
+ *
+ * This is the drop-in boundary for the hot path of s2-streamstore/s2-verification:
+ *
+ *   reference                                                 replaced by
+ *   ---------------------------------------------------------------------------------
+ *   eventsFromReader(r io.Reader) ([]porcupine.Event, error)  s2lc_load_jsonl
+ *       golang/s2-porcupine/main.go:529-563 (+ UnmarshalJSON variants main.go:32-188)
+ *   porcupine.Event{Kind, Value: StreamInput|StreamOutput,     s2lc_event / s2lc_history_from_events
+ *       Id, ClientId}  main.go:206-225, main.go:545-558
+ *   s2Model.ToModel()  main.go:253-361, 605                    (built in: S2 model on device)
+ *   porcupine.CheckEventsVerbose(model, events, 0)             s2lc_check / s2lc_check_batch
+ *       main.go:606 (porcupine v1.0.3 checkSingle, upstream)
+ *   s2Model.Step  main.go:264-335                              s2lc_step_cpu
+ *   chainHash / foldRecordHashes  main.go:227-244              s2lc_chain_hash / s2lc_fold_record_hashes
+ *
+ * Conventions
+ *   - Every entry point returns 0 (S2LC_SUCCESS) or a negative s2lc_status.
+ *     A human-readable message is available from s2lc_last_error(ctx) (ctx
+ *     calls) or written into the caller's err buffer (ctx-free calls).
+ *   - No C++ exception crosses this ABI and the library never calls exit().
+ *   - Objects returned through out-pointers are owned by the library and are
+ *     released with the matching *_free function.
+ *   - A context is single-threaded; distinct contexts may be used
+ *     concurrently from different threads. All calls block.
+ *   - The checker itself runs only on the GPU. With no usable HIP device,
+ *     s2lc_create fails with S2LC_ENODEV: there is no CPU fallback.
+ */
+#ifndef S2LINCHECK_H
+#define S2LINCHECK_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define S2LC_ABI_VERSION 1
+
+/* CheckResult (porcupine: Ok / Illegal / Unknown). Unknown only when a
+ * timeout or configuration budget was set and hit (the reference CLI passes
+ * timeout 0, main.go:606, so it never sees Unknown). */
+enum s2lc_verdict { S2LC_OK = 0, S2LC_ILLEGAL = 1, S2LC_UNKNOWN = 2 };
+
+enum s2lc_status {
+  S2LC_SUCCESS = 0,
+  S2LC_EINVAL = -1,       /* bad argument / malformed event array */
+  S2LC_EDECODE = -2,      /* JSONL decode error (eventsFromReader error, main.go:539,560) */
+  S2LC_EIO = -3,          /* cannot open / read the file (main.go:591-595) */
+  S2LC_ENODEV = -4,       /* no usable HIP device */
+  S2LC_EHIP = -5,         /* HIP runtime error */
+  S2LC_EUNSUPPORTED = -6, /* history outside the supported envelope */
+  S2LC_ENOMEM = -7
+};
+
+/* StreamInput.InputType, main.go:207-208 */
+enum s2lc_input_type { S2LC_INPUT_APPEND = 0, S2LC_INPUT_READ = 1, S2LC_INPUT_CHECK_TAIL = 2 };
+/* porcupine.EventKind */
+enum s2lc_event_kind { S2LC_CALL_EVENT = 0, S2LC_RETURN_EVENT = 1 };
+
+/* One porcupine.Event. For a CALL the input fields mirror StreamInput
+ * (main.go:206-215); for a RETURN the output fields mirror StreamOutput
+ * (main.go:217-225). Pointer-typed Go fields become has_* flags or NULL. */
+typedef struct s2lc_event {
+  int32_t kind;                  /* S2LC_CALL_EVENT / S2LC_RETURN_EVENT */
+  int64_t op_id;                 /* Event.Id */
+  int64_t client_id;             /* Event.ClientId (visualization only) */
+  /* --- call: StreamInput --- */
+  uint8_t input_type;            /* s2lc_input_type */
+  uint8_t has_num_records;       /* NumRecords != nil (required for appends) */
+  uint8_t has_match_seq_num;     /* MatchSeqNum != nil */
+  uint8_t _pad0;
+  uint64_t num_records;
+  uint64_t match_seq_num;
+  const char* set_fencing_token; /* SetFencingToken, NULL = nil */
+  const char* fencing_token;     /* BatchFencingToken, NULL = nil */
+  const uint64_t* record_hashes; /* RecordHashes */
+  uint64_t n_record_hashes;      /* independent of num_records (main_test.go:322) */
+  /* --- return: StreamOutput --- */
+  uint8_t failure;               /* Failure */
+  uint8_t definite_failure;      /* DefiniteFailure */
+  uint8_t has_tail;              /* Tail != nil */
+  uint8_t has_stream_hash;       /* StreamHash != nil */
+  uint32_t _pad1;
+  uint64_t tail;
+  uint64_t stream_hash;
+} s2lc_event;
+
+/* Model state. token is an id interned per history: 0 = nil; equal token
+ * strings get equal ids, so id equality is stringPtrEqual (main.go:246-251). */
+typedef struct s2lc_state {
+  uint64_t tail;
+  uint64_t stream_hash;
+  uint32_t token;
+  uint32_t _pad;
+} s2lc_state;
+
+typedef struct s2lc_history s2lc_history;
+typedef struct s2lc_ctx s2lc_ctx;
+typedef struct s2lc_batch s2lc_batch;
+
+/* Context options. Zero-initialise, set struct_size = sizeof(s2lc_opts). */
+#define S2LC_F_NO_WITNESS 0x1u   /* do not record the witness trace */
+typedef struct s2lc_opts {
+  uint32_t struct_size;
+  int32_t device;          /* HIP device ordinal; -1 = current device */
+  uint32_t flags;          /* S2LC_F_* */
+  uint32_t _pad;
+  uint64_t max_configs;    /* per-history budget of unique configurations; 0 = unlimited
+                              (the search always terminates: it is bounded by n rounds) */
+  void* stream;            /* hipStream_t to launch on; NULL = context-owned stream */
+} s2lc_opts;
+
+/* Result of one history check. */
+typedef struct s2lc_result {
+  int32_t verdict;            /* s2lc_verdict */
+  int32_t reason;             /* 0; or S2LC_R_* explaining Illegal/Unknown */
+  uint64_t configs_explored;  /* unique (linearized set, state) configurations inserted */
+  uint32_t rounds;            /* search rounds run (one non-identity op per round) */
+  uint32_t n_ops;             /* operations in the history */
+  uint32_t witness_len;       /* ops in *witness (n_ops when verdict == OK and witness on) */
+  uint32_t _pad;
+  int64_t* witness;           /* Event.Id of each op in linearization order; library-owned */
+  double device_ms;           /* device time of the search launch(es) */
+} s2lc_result;
+
+#define S2LC_R_NONE 0
+#define S2LC_R_UNMATCHED 1       /* a call without a later return, or a return without an
+                                    earlier call: checkSingle can never empty its list */
+#define S2LC_R_SEARCH_EXHAUSTED 2 /* no configuration survived */
+#define S2LC_R_BUDGET 3          /* max_configs exceeded (Unknown) */
+#define S2LC_R_FRONTIER 4        /* frontier exceeded device capacity (Unknown) */
+
+/* ----- context ----------------------------------------------------------- */
+s2lc_ctx* s2lc_create(const s2lc_opts* opts, int* status);
+void s2lc_destroy(s2lc_ctx* ctx);
+const char* s2lc_last_error(const s2lc_ctx* ctx);
+const char* s2lc_version(void);
+
+/* ----- histories (loader; main.go:529-563) --------------------------------- */
+/* Decode a JSONL history: from path (or "-" = stdin) when buf == NULL, else
+ * from buf[0..len). Accepts and rejects exactly what eventsFromReader does
+ * (SURVEY.md A1). On error returns S2LC_EDECODE / S2LC_EIO and writes a
+ * message into err. */
+int s2lc_load_jsonl(const char* path_or_dash, const uint8_t* buf, size_t len,
+                    s2lc_history** out, char* err, size_t errlen);
+/* Build a history from porcupine-style events; all buffers are copied. */
+int s2lc_history_from_events(const s2lc_event* events, size_t n_events,
+                             s2lc_history** out, char* err, size_t errlen);
+void s2lc_history_free(s2lc_history* h);
+size_t s2lc_history_event_count(const s2lc_history* h);
+/* Export event i (pointers stay valid while h lives). */
+int s2lc_history_get_event(const s2lc_history* h, size_t i, s2lc_event* out);
+
+typedef struct s2lc_history_info {
+  uint32_t n_events;
+  uint32_t n_ops;
+  uint32_t n_chains;        /* K: greedy interval-colouring chain count */
+  uint32_t n_tokens;
+  uint64_t n_record_hashes;
+  int32_t structural;       /* 0 = well formed, S2LC_R_UNMATCHED */
+  uint32_t n_identity_ops;  /* reads, check-tails, definite failures */
+} s2lc_history_info;
+int s2lc_history_info_get(const s2lc_history* h, s2lc_history_info* out);
+
+/* ----- checker (porcupine.CheckEventsVerbose, main.go:606) ------------------ */
+int s2lc_check(s2lc_ctx* ctx, const s2lc_history* h, s2lc_result* out);
+int s2lc_check_batch(s2lc_ctx* ctx, const s2lc_history* const* hs, size_t n, s2lc_result* out);
+void s2lc_result_free(s2lc_result* r); /* frees r->witness; r itself is caller storage */
+
+/* Device-resident batches: upload once, check many times (bench / DST loops). */
+int s2lc_batch_create(s2lc_ctx* ctx, const s2lc_history* const* hs, size_t n, s2lc_batch** out);
+int s2lc_batch_check(s2lc_ctx* ctx, s2lc_batch* b, s2lc_result* out /* [n] */);
+void s2lc_batch_free(s2lc_batch* b);
+
+typedef struct s2lc_batch_stats {
+  double kernel_ms;          /* main search launch, HIP events on the ctx stream */
+  double total_ms;           /* whole s2lc_batch_check including overflow reruns */
+  uint64_t configs_explored; /* sum over histories */
+  uint64_t children_generated;
+  uint64_t rounds;           /* sum over histories */
+  uint64_t algo_bytes;       /* algorithmic bytes of the main launch */
+  uint32_t n_overflow;       /* histories re-run on the wide path */
+  uint32_t launches;
+} s2lc_batch_stats;
+int s2lc_batch_stats_get(const s2lc_batch* b, s2lc_batch_stats* out);
+
+/* ----- model (s2Model, main.go:253-340) ------------------------------------ */
+/* Step op op_index (dense id, first-appearance order) of history h from
+ * state *s; writes 0, 1 or 2 successor states, returns the count. */
+int s2lc_step_cpu(const s2lc_history* h, const s2lc_state* s, uint32_t op_index, s2lc_state out[2]);
+uint64_t s2lc_chain_hash(uint64_t stream_hash, uint64_t record_hash);
+uint64_t s2lc_fold_record_hashes(uint64_t stream_hash, const uint64_t* record_hashes, size_t n);
+/* Replay a linearization (op indices) through the CPU model; 0 if every op
+ * is accepted in order and every op appears exactly once, else -1. */
+int s2lc_replay(const s2lc_history* h, const uint32_t* order, size_t n);
+
+/* ----- deterministic S2 simulator (collector workload, history.rs) ---------- */
+enum s2lc_workflow { S2LC_WF_REGULAR = 0, S2LC_WF_MATCH_SEQ_NUM = 1, S2LC_WF_FENCING = 2 };
+enum s2lc_violation {
+  S2LC_VIOL_NONE = 0,
+  S2LC_VIOL_READ_HASH = 1,     /* perturb one ReadSuccess stream_hash (cf. main_test.go:349-374) */
+  S2LC_VIOL_DEFINITE_APPLIED = 2, /* a definite failure that was applied (cf. :192-232) */
+  S2LC_VIOL_TAIL = 3,          /* one success tail off by one */
+  S2LC_VIOL_STALE_MSN = 4      /* msn append applied despite a stale msn (cf. :315-343) */
+};
+typedef struct s2lc_sim_params {
+  uint32_t struct_size;
+  uint32_t workflow;           /* s2lc_workflow */
+  uint32_t num_clients;        /* --num-concurrent-clients (collect-history.rs) */
+  uint32_t ops_per_client;     /* --num-ops-per-client */
+  uint64_t seed;
+  double p_indefinite;         /* append -> AppendIndefiniteFailure */
+  double p_definite;           /* append -> AppendDefiniteFailure (transient) */
+  double p_read_failure;
+  double p_check_tail_failure;
+  uint64_t initial_records;    /* > 0: pre-existing stream, rectifying append (history.rs:641-670) */
+  uint32_t violation;          /* s2lc_violation */
+  uint32_t max_client_ids;     /* 0 = 20 (history.rs:33) */
+} s2lc_sim_params;
+void s2lc_sim_params_default(s2lc_sim_params* p);
+/* Emit a collector-format JSONL history (library-owned buffer, s2lc_free). */
+int s2lc_simulate_jsonl(const s2lc_sim_params* p, uint8_t** out, size_t* len);
+/* Same history, directly as an s2lc_history (no JSON round trip). */
+int s2lc_simulate_history(const s2lc_sim_params* p, s2lc_history** out);
+void s2lc_free(void* p);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* S2LINCHECK_H */

@@ -1,0 +1,229 @@
+"""TEST INFRASTRUCTURE ONLY — Python face of the CPU oracle (oracle.c).
+
+Only tests/, __graft_entry__.smoke() and bench.py's cpu_baseline leg import
+this module; the product (s2_verification_amd) never does.
+
+Events are plain dicts in the porcupine.Event shape (golang/s2-porcupine/
+main.go:206-225, 545-558):
+
+    {"kind": "call"|"return", "op_id": int, "client_id": int,
+     # call (StreamInput)
+     "input_type": 0|1|2, "num_records": int|None, "match_seq_num": int|None,
+     "set_fencing_token": str|None, "fencing_token": str|None, "record_hashes": [int],
+     # return (StreamOutput)
+     "failure": bool, "definite_failure": bool, "tail": int|None, "stream_hash": int|None}
+
+``load_jsonl`` restates eventsFromReader (main.go:529-563) for well-formed
+collector output using Python's json module; the product loader's edge cases
+are pinned separately in tests/test_loader.py.
+"""
+from __future__ import annotations
+
+import ctypes
+import json
+import os
+import subprocess
+
+import numpy as np
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+_LIB_PATH = os.path.join(_HERE, "build", "liboracle.so")
+
+OK, ILLEGAL, UNKNOWN, PANIC = 0, 1, 2, -2
+_NAMES = {OK: "Ok", ILLEGAL: "Illegal", UNKNOWN: "Unknown", PANIC: "Panic", -1: "EInval"}
+
+EVENT_DTYPE = np.dtype([
+    ("kind", "<i4"), ("_pad0", "<i4"), ("op_id", "<i8"), ("client_id", "<i8"),
+    ("input_type", "u1"), ("has_num_records", "u1"), ("has_msn", "u1"), ("_pad1", "u1"),
+    ("set_tok", "<i4"), ("batch_tok", "<i4"), ("_pad2", "<i4"),
+    ("num_records", "<u8"), ("msn", "<u8"), ("hashes", "<u8"), ("n_hashes", "<u8"),
+    ("failure", "u1"), ("definite", "u1"), ("has_tail", "u1"), ("has_hash", "u1"), ("_pad3", "<u4"),
+    ("tail", "<u8"), ("stream_hash", "<u8"),
+])
+assert EVENT_DTYPE.itemsize == 96
+
+
+class _Stats(ctypes.Structure):
+    _fields_ = [("cache_inserts", ctypes.c_uint64), ("steps", ctypes.c_uint64),
+                ("backtracks", ctypes.c_uint64), ("max_state_set", ctypes.c_uint64),
+                ("seconds", ctypes.c_double)]
+
+
+_lib = None
+
+
+def build():
+    subprocess.run(["make", "-s", "-C", _HERE], check=True)
+
+
+def lib():
+    global _lib
+    if _lib is None:
+        if not os.path.exists(_LIB_PATH):
+            build()
+        L = ctypes.CDLL(_LIB_PATH)
+        L.or_chain_hash.restype = ctypes.c_uint64
+        L.or_chain_hash.argtypes = [ctypes.c_uint64, ctypes.c_uint64]
+        L.or_fold.restype = ctypes.c_uint64
+        L.or_fold.argtypes = [ctypes.c_uint64, ctypes.c_void_p, ctypes.c_uint64]
+        L.or_check_wgl.restype = ctypes.c_int
+        L.or_check_wgl.argtypes = [ctypes.c_void_p, ctypes.c_size_t, ctypes.c_int, ctypes.c_double,
+                                   ctypes.c_uint64, ctypes.POINTER(_Stats)]
+        L.or_check_brute.restype = ctypes.c_int
+        L.or_check_brute.argtypes = [ctypes.c_void_p, ctypes.c_size_t, ctypes.POINTER(_Stats)]
+        _lib = L
+    return _lib
+
+
+def chain_hash(h: int, r: int) -> int:
+    return lib().or_chain_hash(h, r)
+
+
+def fold(h: int, rs) -> int:
+    a = np.ascontiguousarray(np.asarray(rs, dtype=np.uint64))
+    return lib().or_fold(h, a.ctypes.data, len(a))
+
+
+class EventArray:
+    """Events packed into the or_event layout (keeps the hash pool alive)."""
+
+    def __init__(self, events):
+        toks = {}
+
+        def tok(s):
+            if s is None:
+                return 0
+            return toks.setdefault(s, len(toks) + 1)
+
+        n = len(events)
+        arr = np.zeros(n, dtype=EVENT_DTYPE)
+        pool = []
+        offs = np.zeros(n, dtype=np.uint64)
+        for i, e in enumerate(events):
+            r = arr[i]
+            call = e["kind"] == "call"
+            r["kind"] = 0 if call else 1
+            r["op_id"] = e["op_id"]
+            r["client_id"] = e.get("client_id", 0)
+            if call:
+                r["input_type"] = e["input_type"]
+                nr = e.get("num_records")
+                r["has_num_records"] = nr is not None
+                r["num_records"] = nr or 0
+                msn = e.get("match_seq_num")
+                r["has_msn"] = msn is not None
+                r["msn"] = msn or 0
+                r["set_tok"] = tok(e.get("set_fencing_token"))
+                r["batch_tok"] = tok(e.get("fencing_token"))
+                hs = e.get("record_hashes") or []
+                offs[i] = len(pool)
+                r["n_hashes"] = len(hs)
+                pool.extend(hs)
+            else:
+                r["failure"] = bool(e.get("failure"))
+                r["definite"] = bool(e.get("definite_failure"))
+                t = e.get("tail")
+                r["has_tail"] = t is not None
+                r["tail"] = t or 0
+                sh = e.get("stream_hash")
+                r["has_hash"] = sh is not None
+                r["stream_hash"] = sh or 0
+        self.pool = np.array(pool, dtype=np.uint64) if pool else np.zeros(1, dtype=np.uint64)
+        base = self.pool.ctypes.data
+        arr["hashes"] = base + offs * 8
+        self.arr = arr
+
+    @property
+    def ptr(self):
+        return self.arr.ctypes.data
+
+    def __len__(self):
+        return len(self.arr)
+
+
+def _as_array(events):
+    return events if isinstance(events, EventArray) else EventArray(events)
+
+
+def check_wgl(events, compute_partial=True, timeout=0.0, max_entries=0):
+    """porcupine.CheckEventsVerbose(s2Model.ToModel(), events, timeout) restated."""
+    ea = _as_array(events)
+    st = _Stats()
+    r = lib().or_check_wgl(ea.ptr, len(ea), int(compute_partial), float(timeout), int(max_entries),
+                           ctypes.byref(st))
+    return _NAMES[r], {"cache_inserts": st.cache_inserts, "steps": st.steps,
+                       "backtracks": st.backtracks, "max_state_set": st.max_state_set,
+                       "seconds": st.seconds}
+
+
+def check_brute(events):
+    ea = _as_array(events)
+    st = _Stats()
+    r = lib().or_check_brute(ea.ptr, len(ea), ctypes.byref(st))
+    return _NAMES[r], {"steps": st.steps}
+
+
+# ------------------------------------------------------------------ loader --
+def _finish_to_output(fe):
+    """outputFromFinish, main.go:466-523."""
+    if isinstance(fe, str):
+        if fe == "AppendDefiniteFailure":
+            return dict(failure=True, definite_failure=True, tail=None, stream_hash=None)
+        if fe == "AppendIndefiniteFailure":
+            return dict(failure=True, definite_failure=False, tail=None, stream_hash=None)
+        if fe in ("ReadFailure", "CheckTailFailure"):
+            return dict(failure=True, definite_failure=True, tail=None, stream_hash=None)
+        raise ValueError(f"unknown string finish event: {fe}")
+    if not isinstance(fe, dict):
+        raise ValueError("unknown finish event format")
+    for k in ("AppendSuccess", "ReadSuccess", "CheckTailSuccess"):
+        if k in fe:
+            v = fe[k] or {}
+            return dict(failure=False, definite_failure=False, tail=int(v.get("tail", 0)),
+                        stream_hash=int(v.get("stream_hash", 0)) if k == "ReadSuccess" else None)
+    raise ValueError("unknown finish event format")
+
+
+def _start_to_input(se):
+    """StartEvent.UnmarshalJSON + inputFromStart, main.go:32-70, 428-464."""
+    if isinstance(se, str):
+        if se == "Read":
+            return dict(input_type=1)
+        if se == "CheckTail":
+            return dict(input_type=2)
+        raise ValueError(f"unknown string start event: {se}")
+    if isinstance(se, dict) and "Append" in se:
+        a = se["Append"] or {}
+        hs = [int(x) for x in (a.get("record_hashes") or [])]
+        nr = int(a.get("num_records", 0))
+        if len(hs) != nr:
+            raise ValueError(f"append has {len(hs)} record_hashes but {nr} records")
+        msn = a.get("match_seq_num")
+        return dict(input_type=0, num_records=nr, record_hashes=hs,
+                    set_fencing_token=a.get("set_fencing_token"),
+                    fencing_token=a.get("fencing_token"),
+                    match_seq_num=None if msn is None else int(msn))
+    raise ValueError("unknown start event format")
+
+
+def load_jsonl(text):
+    """eventsFromReader restated for well-formed input (one JSON value per line)."""
+    if isinstance(text, (bytes, bytearray)):
+        text = text.decode()
+    dec = json.JSONDecoder()
+    events, i, n = [], 0, len(text)
+    while True:
+        while i < n and text[i] in " \t\r\n":
+            i += 1
+        if i >= n:
+            return events
+        rec, i = dec.raw_decode(text, i)
+        ev = rec.get("event") or {}
+        has_s, has_f = "Start" in ev, "Finish" in ev
+        if has_s == has_f:
+            raise ValueError("expected exactly one of Start/Finish")
+        base = {"op_id": int(rec.get("op_id", 0)), "client_id": int(rec.get("client_id", 0))}
+        if has_s:
+            events.append({"kind": "call", **base, **_start_to_input(ev["Start"])})
+        else:
+            events.append({"kind": "return", **base, **_finish_to_output(ev["Finish"])})
