@@ -133,6 +133,7 @@ typedef struct s2lc_result {
 #define S2LC_R_SEARCH_EXHAUSTED 2 /* no configuration survived */
 #define S2LC_R_BUDGET 3          /* max_configs exceeded (Unknown) */
 #define S2LC_R_FRONTIER 4        /* frontier exceeded device capacity (Unknown) */
+#define S2LC_R_WITNESS_INVALID 5 /* Ok, but the witness failed CPU replay (a bug; never expected) */
 
 /* ----- context ----------------------------------------------------------- */
 s2lc_ctx* s2lc_create(const s2lc_opts* opts, int* status);
@@ -173,7 +174,13 @@ void s2lc_result_free(s2lc_result* r); /* frees r->witness; r itself is caller s
 
 /* Device-resident batches: upload once, check many times (bench / DST loops). */
 int s2lc_batch_create(s2lc_ctx* ctx, const s2lc_history* const* hs, size_t n, s2lc_batch** out);
+/* s2lc_batch_run + s2lc_batch_results(..., with_witness = 1). */
 int s2lc_batch_check(s2lc_ctx* ctx, s2lc_batch* b, s2lc_result* out /* [n] */);
+/* Device work only: search every history, copy verdicts back. */
+int s2lc_batch_run(s2lc_ctx* ctx, s2lc_batch* b);
+/* Results of the last run; with_witness expands and replay-verifies witnesses
+ * on the host (CPU model, powerset semantics). */
+int s2lc_batch_results(s2lc_ctx* ctx, s2lc_batch* b, s2lc_result* out /* [n] */, int with_witness);
 void s2lc_batch_free(s2lc_batch* b);
 
 typedef struct s2lc_batch_stats {

@@ -1,0 +1,478 @@
+"""s2_verification_amd — MI355X linearizability checker for the S2 stream model.
+
+Python face of libs2lincheck (include/s2lincheck.h), mirroring the reference's
+Go surface so callers and tests read like golang/s2-porcupine/main_test.go:
+
+    reference (Go)                                  here
+    ----------------------------------------------  ------------------------------------
+    StreamInput / StreamOutput   main.go:206-225     StreamInput / StreamOutput
+    porcupine.Event{Kind,Value,Id,ClientId}          Event(kind, value, id, client_id)
+    porcupine.CallEvent / ReturnEvent                CallEvent / ReturnEvent
+    eventsFromReader(r)          main.go:529-563     events_from_reader(data) -> History
+    chainHash / foldRecordHashes main.go:227-244     chain_hash / fold_record_hashes
+    porcupine.CheckEventsVerbose main.go:606         check_events_verbose(model, events, timeout)
+    porcupine.Ok / Illegal / Unknown                 Ok / Illegal / Unknown
+
+The check itself only runs on the GPU (HIP, gfx950). Without a device
+``Checker()`` raises; there is no CPU fallback.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+from dataclasses import dataclass, field
+from typing import List, Optional, Sequence, Tuple
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "libs2lincheck.so")
+CLI_PATH = os.path.join(_HERE, "s2-porcupine")
+
+# ------------------------------------------------------------------ C ABI ---
+S2LC_OK, S2LC_ILLEGAL, S2LC_UNKNOWN = 0, 1, 2
+CallEvent, ReturnEvent = 0, 1
+Ok, Illegal, Unknown = "Ok", "Illegal", "Unknown"
+_VERDICT = {S2LC_OK: Ok, S2LC_ILLEGAL: Illegal, S2LC_UNKNOWN: Unknown}
+STATUS = {0: "SUCCESS", -1: "EINVAL", -2: "EDECODE", -3: "EIO", -4: "ENODEV", -5: "EHIP",
+          -6: "EUNSUPPORTED", -7: "ENOMEM"}
+REASONS = {0: "none", 1: "unmatched", 2: "search_exhausted", 3: "budget", 4: "frontier", 5: "witness_invalid"}
+WF_REGULAR, WF_MATCH_SEQ_NUM, WF_FENCING = 0, 1, 2
+VIOL_NONE, VIOL_READ_HASH, VIOL_DEFINITE_APPLIED, VIOL_TAIL, VIOL_STALE_MSN = 0, 1, 2, 3, 4
+
+
+class S2LCError(RuntimeError):
+    def __init__(self, status, msg=""):
+        super().__init__(f"{STATUS.get(status, status)}: {msg}")
+        self.status = status
+
+
+class c_event(ctypes.Structure):
+    _fields_ = [
+        ("kind", ctypes.c_int32), ("op_id", ctypes.c_int64), ("client_id", ctypes.c_int64),
+        ("input_type", ctypes.c_uint8), ("has_num_records", ctypes.c_uint8),
+        ("has_match_seq_num", ctypes.c_uint8), ("_pad0", ctypes.c_uint8),
+        ("num_records", ctypes.c_uint64), ("match_seq_num", ctypes.c_uint64),
+        ("set_fencing_token", ctypes.c_char_p), ("fencing_token", ctypes.c_char_p),
+        ("record_hashes", ctypes.POINTER(ctypes.c_uint64)), ("n_record_hashes", ctypes.c_uint64),
+        ("failure", ctypes.c_uint8), ("definite_failure", ctypes.c_uint8), ("has_tail", ctypes.c_uint8),
+        ("has_stream_hash", ctypes.c_uint8), ("_pad1", ctypes.c_uint32),
+        ("tail", ctypes.c_uint64), ("stream_hash", ctypes.c_uint64),
+    ]
+
+
+class c_state(ctypes.Structure):
+    _fields_ = [("tail", ctypes.c_uint64), ("stream_hash", ctypes.c_uint64), ("token", ctypes.c_uint32),
+                ("_pad", ctypes.c_uint32)]
+
+
+class c_opts(ctypes.Structure):
+    _fields_ = [("struct_size", ctypes.c_uint32), ("device", ctypes.c_int32), ("flags", ctypes.c_uint32),
+                ("_pad", ctypes.c_uint32), ("max_configs", ctypes.c_uint64), ("stream", ctypes.c_void_p)]
+
+
+class c_result(ctypes.Structure):
+    _fields_ = [("verdict", ctypes.c_int32), ("reason", ctypes.c_int32), ("configs_explored", ctypes.c_uint64),
+                ("rounds", ctypes.c_uint32), ("n_ops", ctypes.c_uint32), ("witness_len", ctypes.c_uint32),
+                ("_pad", ctypes.c_uint32), ("witness", ctypes.POINTER(ctypes.c_int64)),
+                ("device_ms", ctypes.c_double)]
+
+
+class c_history_info(ctypes.Structure):
+    _fields_ = [("n_events", ctypes.c_uint32), ("n_ops", ctypes.c_uint32), ("n_chains", ctypes.c_uint32),
+                ("n_tokens", ctypes.c_uint32), ("n_record_hashes", ctypes.c_uint64),
+                ("structural", ctypes.c_int32), ("n_identity_ops", ctypes.c_uint32)]
+
+
+class c_batch_stats(ctypes.Structure):
+    _fields_ = [("kernel_ms", ctypes.c_double), ("total_ms", ctypes.c_double),
+                ("configs_explored", ctypes.c_uint64), ("children_generated", ctypes.c_uint64),
+                ("rounds", ctypes.c_uint64), ("algo_bytes", ctypes.c_uint64),
+                ("n_overflow", ctypes.c_uint32), ("launches", ctypes.c_uint32)]
+
+
+class c_sim_params(ctypes.Structure):
+    _fields_ = [("struct_size", ctypes.c_uint32), ("workflow", ctypes.c_uint32),
+                ("num_clients", ctypes.c_uint32), ("ops_per_client", ctypes.c_uint32),
+                ("seed", ctypes.c_uint64), ("p_indefinite", ctypes.c_double), ("p_definite", ctypes.c_double),
+                ("p_read_failure", ctypes.c_double), ("p_check_tail_failure", ctypes.c_double),
+                ("initial_records", ctypes.c_uint64), ("violation", ctypes.c_uint32),
+                ("max_client_ids", ctypes.c_uint32)]
+
+
+# Every symbol include/s2lincheck.h declares: (name, restype, argtypes)
+_P = ctypes.c_void_p
+SIGNATURES = [
+    ("s2lc_create", _P, [ctypes.POINTER(c_opts), ctypes.POINTER(ctypes.c_int)]),
+    ("s2lc_destroy", None, [_P]),
+    ("s2lc_last_error", ctypes.c_char_p, [_P]),
+    ("s2lc_version", ctypes.c_char_p, []),
+    ("s2lc_load_jsonl", ctypes.c_int, [ctypes.c_char_p, ctypes.c_char_p, ctypes.c_size_t, ctypes.POINTER(_P),
+                                       ctypes.c_char_p, ctypes.c_size_t]),
+    ("s2lc_history_from_events", ctypes.c_int, [ctypes.POINTER(c_event), ctypes.c_size_t, ctypes.POINTER(_P),
+                                                ctypes.c_char_p, ctypes.c_size_t]),
+    ("s2lc_history_free", None, [_P]),
+    ("s2lc_history_event_count", ctypes.c_size_t, [_P]),
+    ("s2lc_history_get_event", ctypes.c_int, [_P, ctypes.c_size_t, ctypes.POINTER(c_event)]),
+    ("s2lc_history_info_get", ctypes.c_int, [_P, ctypes.POINTER(c_history_info)]),
+    ("s2lc_check", ctypes.c_int, [_P, _P, ctypes.POINTER(c_result)]),
+    ("s2lc_check_batch", ctypes.c_int, [_P, ctypes.POINTER(_P), ctypes.c_size_t, ctypes.POINTER(c_result)]),
+    ("s2lc_result_free", None, [ctypes.POINTER(c_result)]),
+    ("s2lc_batch_create", ctypes.c_int, [_P, ctypes.POINTER(_P), ctypes.c_size_t, ctypes.POINTER(_P)]),
+    ("s2lc_batch_check", ctypes.c_int, [_P, _P, ctypes.POINTER(c_result)]),
+    ("s2lc_batch_run", ctypes.c_int, [_P, _P]),
+    ("s2lc_batch_results", ctypes.c_int, [_P, _P, ctypes.POINTER(c_result), ctypes.c_int]),
+    ("s2lc_batch_free", None, [_P]),
+    ("s2lc_batch_stats_get", ctypes.c_int, [_P, ctypes.POINTER(c_batch_stats)]),
+    ("s2lc_step_cpu", ctypes.c_int, [_P, ctypes.POINTER(c_state), ctypes.c_uint32, ctypes.POINTER(c_state)]),
+    ("s2lc_chain_hash", ctypes.c_uint64, [ctypes.c_uint64, ctypes.c_uint64]),
+    ("s2lc_fold_record_hashes", ctypes.c_uint64, [ctypes.c_uint64, ctypes.POINTER(ctypes.c_uint64), ctypes.c_size_t]),
+    ("s2lc_replay", ctypes.c_int, [_P, ctypes.POINTER(ctypes.c_uint32), ctypes.c_size_t]),
+    ("s2lc_sim_params_default", None, [ctypes.POINTER(c_sim_params)]),
+    ("s2lc_simulate_jsonl", ctypes.c_int, [ctypes.POINTER(c_sim_params), ctypes.POINTER(ctypes.POINTER(ctypes.c_uint8)),
+                                           ctypes.POINTER(ctypes.c_size_t)]),
+    ("s2lc_simulate_history", ctypes.c_int, [ctypes.POINTER(c_sim_params), ctypes.POINTER(_P)]),
+    ("s2lc_free", None, [_P]),
+]
+
+_lib = None
+
+
+def lib():
+    """Load libs2lincheck.so (built in-tree by `make -C s2_verification_amd`)."""
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB_PATH):
+            raise ImportError(f"{LIB_PATH} is not built: run `make -C s2_verification_amd` "
+                              "(or __graft_entry__.build()); there is no fallback")
+        L = ctypes.CDLL(LIB_PATH)
+        for name, res, args in SIGNATURES:
+            fn = getattr(L, name)
+            fn.restype = res
+            fn.argtypes = args
+        _lib = L
+    return _lib
+
+
+# -------------------------------------------------------------- the model ---
+def chain_hash(stream_hash: int, record_hash: int) -> int:
+    """chainHash, main.go:232-236."""
+    return lib().s2lc_chain_hash(stream_hash, record_hash)
+
+
+def fold_record_hashes(stream_hash: int, record_hashes: Sequence[int]) -> int:
+    """foldRecordHashes, main.go:238-244."""
+    arr = (ctypes.c_uint64 * len(record_hashes))(*record_hashes)
+    return lib().s2lc_fold_record_hashes(stream_hash, arr, len(record_hashes))
+
+
+def Ptr(v):  # main.go:525 — pointers are plain Optional values here
+    return v
+
+
+@dataclass
+class StreamInput:
+    """main.go:206-215. 0 append, 1 read, 2 check-tail."""
+    InputType: int = 0
+    SetFencingToken: Optional[str] = None
+    BatchFencingToken: Optional[str] = None
+    MatchSeqNum: Optional[int] = None
+    NumRecords: Optional[int] = None
+    RecordHashes: List[int] = field(default_factory=list)
+
+
+@dataclass
+class StreamOutput:
+    """main.go:217-225."""
+    Failure: bool = False
+    DefiniteFailure: bool = False
+    Tail: Optional[int] = None
+    StreamHash: Optional[int] = None
+
+
+@dataclass
+class Event:
+    """porcupine.Event."""
+    Kind: int
+    Value: object
+    Id: int
+    ClientId: int = 0
+
+
+def _to_c_events(events: Sequence[Event]):
+    arr = (c_event * len(events))()
+    keep = []
+    for i, e in enumerate(events):
+        c = arr[i]
+        c.kind = e.Kind
+        c.op_id = e.Id
+        c.client_id = e.ClientId
+        v = e.Value
+        if e.Kind == CallEvent:
+            c.input_type = v.InputType
+            c.has_num_records = v.NumRecords is not None
+            c.num_records = v.NumRecords or 0
+            c.has_match_seq_num = v.MatchSeqNum is not None
+            c.match_seq_num = v.MatchSeqNum or 0
+            if v.SetFencingToken is not None:
+                b = v.SetFencingToken.encode()
+                keep.append(b)
+                c.set_fencing_token = b
+            if v.BatchFencingToken is not None:
+                b = v.BatchFencingToken.encode()
+                keep.append(b)
+                c.fencing_token = b
+            hs = list(v.RecordHashes or [])
+            if hs:
+                h = (ctypes.c_uint64 * len(hs))(*hs)
+                keep.append(h)
+                c.record_hashes = h
+            c.n_record_hashes = len(hs)
+        else:
+            c.failure = bool(v.Failure)
+            c.definite_failure = bool(v.DefiniteFailure)
+            c.has_tail = v.Tail is not None
+            c.tail = v.Tail or 0
+            c.has_stream_hash = v.StreamHash is not None
+            c.stream_hash = v.StreamHash or 0
+    return arr, keep
+
+
+class History:
+    """An s2lc_history: decoded events + the device search layout."""
+
+    def __init__(self, handle):
+        self._h = handle
+
+    def __del__(self):
+        h, self._h = getattr(self, "_h", None), None
+        if h and _lib is not None:
+            _lib.s2lc_history_free(h)
+
+    @classmethod
+    def from_events(cls, events: Sequence[Event]) -> "History":
+        arr, keep = _to_c_events(events)
+        out = ctypes.c_void_p()
+        err = ctypes.create_string_buffer(1024)
+        rc = lib().s2lc_history_from_events(arr, len(events), ctypes.byref(out), err, 1024)
+        if rc:
+            raise S2LCError(rc, err.value.decode(errors="replace"))
+        return cls(out.value)
+
+    @classmethod
+    def from_jsonl(cls, data=None, path=None) -> "History":
+        out = ctypes.c_void_p()
+        err = ctypes.create_string_buffer(2048)
+        if data is not None:
+            if isinstance(data, str):
+                data = data.encode()
+            rc = lib().s2lc_load_jsonl(None, data, len(data), ctypes.byref(out), err, 2048)
+        else:
+            rc = lib().s2lc_load_jsonl(path.encode(), None, 0, ctypes.byref(out), err, 2048)
+        if rc:
+            raise S2LCError(rc, err.value.decode(errors="replace"))
+        return cls(out.value)
+
+    def info(self) -> dict:
+        i = c_history_info()
+        lib().s2lc_history_info_get(self._h, ctypes.byref(i))
+        return {k: getattr(i, k) for k, _ in c_history_info._fields_}
+
+    def __len__(self):
+        return lib().s2lc_history_event_count(self._h)
+
+    def events(self) -> List[Event]:
+        out = []
+        e = c_event()
+        for i in range(len(self)):
+            lib().s2lc_history_get_event(self._h, i, ctypes.byref(e))
+            if e.kind == CallEvent:
+                hs = [e.record_hashes[k] for k in range(e.n_record_hashes)] if e.n_record_hashes else []
+                v = StreamInput(InputType=e.input_type,
+                                SetFencingToken=e.set_fencing_token.decode() if e.set_fencing_token else None,
+                                BatchFencingToken=e.fencing_token.decode() if e.fencing_token else None,
+                                MatchSeqNum=e.match_seq_num if e.has_match_seq_num else None,
+                                NumRecords=e.num_records if e.has_num_records else None,
+                                RecordHashes=hs)
+            else:
+                v = StreamOutput(Failure=bool(e.failure), DefiniteFailure=bool(e.definite_failure),
+                                 Tail=e.tail if e.has_tail else None,
+                                 StreamHash=e.stream_hash if e.has_stream_hash else None)
+            out.append(Event(e.kind, v, e.op_id, e.client_id))
+        return out
+
+    def step(self, state: Tuple[int, int, int], op_index: int):
+        """s2Model.Step for dense op `op_index` from (tail, hash, token_id)."""
+        s = c_state(state[0], state[1], state[2], 0)
+        outs = (c_state * 2)()
+        n = lib().s2lc_step_cpu(self._h, ctypes.byref(s), op_index, outs)
+        if n < 0:
+            raise S2LCError(n, "step")
+        return [(outs[k].tail, outs[k].stream_hash, outs[k].token) for k in range(n)]
+
+    def replay(self, order: Sequence[int]) -> bool:
+        arr = (ctypes.c_uint32 * len(order))(*order)
+        return lib().s2lc_replay(self._h, arr, len(order)) == 0
+
+
+def events_from_reader(data) -> History:
+    """eventsFromReader (main.go:529-563): bytes/str JSONL -> History (raises on decode error)."""
+    return History.from_jsonl(data=data)
+
+
+def load_file(path: str) -> History:
+    return History.from_jsonl(path=path)
+
+
+@dataclass
+class CheckResult:
+    verdict: str
+    reason: str
+    configs_explored: int
+    rounds: int
+    n_ops: int
+    witness: Optional[List[int]]
+    device_ms: float
+
+
+def _convert(r: c_result) -> CheckResult:
+    w = [r.witness[k] for k in range(r.witness_len)] if r.witness else None
+    return CheckResult(_VERDICT[r.verdict], REASONS.get(r.reason, str(r.reason)), r.configs_explored,
+                       r.rounds, r.n_ops, w, r.device_ms)
+
+
+class Batch:
+    """Device-resident batch of histories (upload once, check repeatedly)."""
+
+    def __init__(self, checker: "Checker", histories: Sequence[History]):
+        self.checker = checker
+        self.histories = list(histories)
+        arr = (ctypes.c_void_p * len(self.histories))(*[h._h for h in self.histories])
+        out = ctypes.c_void_p()
+        rc = lib().s2lc_batch_create(checker._ctx, arr, len(self.histories), ctypes.byref(out))
+        if rc:
+            raise S2LCError(rc, checker.last_error())
+        self._b = out.value
+
+    def __del__(self):
+        b, self._b = getattr(self, "_b", None), None
+        if b and _lib is not None:
+            _lib.s2lc_batch_free(b)
+
+    def run(self):
+        rc = lib().s2lc_batch_run(self.checker._ctx, self._b)
+        if rc:
+            raise S2LCError(rc, self.checker.last_error())
+
+    def results(self, with_witness=True) -> List[CheckResult]:
+        n = len(self.histories)
+        res = (c_result * max(n, 1))()
+        rc = lib().s2lc_batch_results(self.checker._ctx, self._b, res, int(with_witness))
+        if rc:
+            raise S2LCError(rc, self.checker.last_error())
+        out = [_convert(res[i]) for i in range(n)]
+        for i in range(n):
+            lib().s2lc_result_free(ctypes.byref(res[i]))
+        return out
+
+    def check(self, with_witness=True) -> List[CheckResult]:
+        self.run()
+        return self.results(with_witness)
+
+    def stats(self) -> dict:
+        s = c_batch_stats()
+        lib().s2lc_batch_stats_get(self._b, ctypes.byref(s))
+        return {k: getattr(s, k) for k, _ in c_batch_stats._fields_}
+
+
+class Checker:
+    """An s2lc_ctx bound to one HIP device (and optionally an existing stream)."""
+
+    def __init__(self, device: int = -1, witness: bool = True, max_configs: int = 0, stream: int = 0):
+        o = c_opts()
+        o.struct_size = ctypes.sizeof(c_opts)
+        o.device = device
+        o.flags = 0 if witness else 1
+        o.max_configs = max_configs
+        o.stream = stream or None
+        st = ctypes.c_int(0)
+        ctx = lib().s2lc_create(ctypes.byref(o), ctypes.byref(st))
+        if not ctx:
+            raise S2LCError(st.value, "no usable HIP device for the S2 checker")
+        self._ctx = ctx
+
+    def __del__(self):
+        c, self._ctx = getattr(self, "_ctx", None), None
+        if c and _lib is not None:
+            _lib.s2lc_destroy(c)
+
+    def last_error(self) -> str:
+        return lib().s2lc_last_error(self._ctx).decode(errors="replace")
+
+    def check(self, h: History) -> CheckResult:
+        r = c_result()
+        rc = lib().s2lc_check(self._ctx, h._h, ctypes.byref(r))
+        if rc:
+            raise S2LCError(rc, self.last_error())
+        out = _convert(r)
+        lib().s2lc_result_free(ctypes.byref(r))
+        return out
+
+    def check_batch(self, hs: Sequence[History]) -> List[CheckResult]:
+        return Batch(self, hs).check()
+
+    def batch(self, hs: Sequence[History]) -> Batch:
+        return Batch(self, hs)
+
+
+_default_checker = None
+
+
+def check_events_verbose(model, events, timeout: float = 0):
+    """porcupine.CheckEventsVerbose(s2Model.ToModel(), events, timeout) on the GPU.
+
+    `model` is accepted for signature parity and ignored (the S2 model is built in).
+    Returns (verdict, info) with verdict in {Ok, Illegal, Unknown}; info carries the
+    witness linearization (op ids) for Ok, configs explored and rounds.
+    """
+    global _default_checker
+    if _default_checker is None:
+        _default_checker = Checker()
+    h = events if isinstance(events, History) else History.from_events(events)
+    r = _default_checker.check(h)
+    return r.verdict, r
+
+
+s2Model = None  # the S2 model lives on the device; kept for call-site parity
+
+
+# -------------------------------------------------------------- simulator ---
+def sim_params(workflow=WF_REGULAR, num_clients=5, ops_per_client=100, seed=1, **kw) -> c_sim_params:
+    p = c_sim_params()
+    lib().s2lc_sim_params_default(ctypes.byref(p))
+    p.workflow = workflow
+    p.num_clients = num_clients
+    p.ops_per_client = ops_per_client
+    p.seed = seed
+    for k, v in kw.items():
+        setattr(p, k, v)
+    return p
+
+
+def simulate_jsonl(**kw) -> bytes:
+    p = sim_params(**kw)
+    buf = ctypes.POINTER(ctypes.c_uint8)()
+    n = ctypes.c_size_t()
+    rc = lib().s2lc_simulate_jsonl(ctypes.byref(p), ctypes.byref(buf), ctypes.byref(n))
+    if rc:
+        raise S2LCError(rc, "simulate")
+    data = ctypes.string_at(buf, n.value)
+    lib().s2lc_free(buf)
+    return data
+
+
+def simulate_history(**kw) -> History:
+    p = sim_params(**kw)
+    out = ctypes.c_void_p()
+    rc = lib().s2lc_simulate_history(ctypes.byref(p), ctypes.byref(out))
+    if rc:
+        raise S2LCError(rc, "simulate")
+    return History(out.value)

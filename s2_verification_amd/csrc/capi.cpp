@@ -1,0 +1,464 @@
+// capi.cpp — the extern "C" boundary (include/s2lincheck.h). No exception
+// crosses it; every failure becomes a negative status + message.
+#include <hip/hip_runtime.h>
+#include <stdio.h>
+#include <stdlib.h>
+#include <string.h>
+
+#include <new>
+#include <string>
+#include <vector>
+
+#include "history.h"
+#include "s2lincheck.h"
+#include "search.h"
+
+namespace s2lc {
+int simulate(const s2lc_sim_params& p, History* h, std::string* jsonl);
+}
+
+using namespace s2lc;
+
+struct s2lc_history {
+  History h;
+};
+
+struct s2lc_ctx {
+  int device = 0;
+  hipStream_t stream = nullptr;
+  bool own_stream = false;
+  uint32_t flags = 0;
+  uint64_t max_configs = 0;
+  std::string err;
+};
+
+struct s2lc_batch {
+  DevBatch b;
+  RunStats stats;
+  bool ran = false;
+  bool witness = false;
+};
+
+static void set_err(char* err, size_t errlen, const std::string& msg) {
+  if (err && errlen) {
+    size_t n = std::min(errlen - 1, msg.size());
+    memcpy(err, msg.data(), n);
+    err[n] = 0;
+  }
+}
+
+extern "C" {
+
+const char* s2lc_version(void) { return "s2lincheck 0.1.0 (gfx950)"; }
+
+s2lc_ctx* s2lc_create(const s2lc_opts* opts, int* status) {
+  int st = 0;
+  s2lc_ctx* c = nullptr;
+  try {
+    int n = 0;
+    if (hipGetDeviceCount(&n) != hipSuccess || n <= 0) {
+      if (status) *status = S2LC_ENODEV;
+      return nullptr;
+    }
+    c = new s2lc_ctx();
+    int dev = -1;
+    if (opts && opts->struct_size >= sizeof(uint32_t) * 2) dev = opts->device;
+    if (dev < 0) {
+      if (hipGetDevice(&dev) != hipSuccess) dev = 0;
+    }
+    if (dev >= n) { delete c; if (status) *status = S2LC_ENODEV; return nullptr; }
+    if (hipSetDevice(dev) != hipSuccess) { delete c; if (status) *status = S2LC_EHIP; return nullptr; }
+    c->device = dev;
+    if (opts && opts->struct_size >= sizeof(s2lc_opts)) {
+      c->flags = opts->flags;
+      c->max_configs = opts->max_configs;
+      c->stream = (hipStream_t)opts->stream;
+    }
+    if (!c->stream) {
+      if (hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess) {
+        delete c;
+        if (status) *status = S2LC_EHIP;
+        return nullptr;
+      }
+      c->own_stream = true;
+    }
+  } catch (...) {
+    delete c;
+    if (status) *status = S2LC_ENOMEM;
+    return nullptr;
+  }
+  if (status) *status = st;
+  return c;
+}
+
+void s2lc_destroy(s2lc_ctx* c) {
+  if (!c) return;
+  if (c->own_stream && c->stream) (void)hipStreamDestroy(c->stream);
+  delete c;
+}
+
+const char* s2lc_last_error(const s2lc_ctx* c) { return c ? c->err.c_str() : "null context"; }
+
+// ------------------------------------------------------------- histories ---
+int s2lc_load_jsonl(const char* path, const uint8_t* buf, size_t len, s2lc_history** out, char* err,
+                    size_t errlen) {
+  if (!out) return S2LC_EINVAL;
+  *out = nullptr;
+  try {
+    std::vector<uint8_t> data;
+    if (!buf) {
+      if (!path) return S2LC_EINVAL;
+      FILE* f = strcmp(path, "-") == 0 ? stdin : fopen(path, "rb");
+      if (!f) {
+        set_err(err, errlen, std::string("open ") + path + ": " + strerror(errno));
+        return S2LC_EIO;
+      }
+      uint8_t tmp[1 << 16];
+      size_t n;
+      while ((n = fread(tmp, 1, sizeof tmp, f)) > 0) data.insert(data.end(), tmp, tmp + n);
+      const bool bad = ferror(f);
+      if (f != stdin) fclose(f);
+      if (bad) { set_err(err, errlen, std::string("read ") + path); return S2LC_EIO; }
+      buf = data.data();
+      len = data.size();
+    }
+    s2lc_history* h = new s2lc_history();
+    std::string e;
+    int rc = load_jsonl(buf, len, h->h, e);
+    if (rc) { set_err(err, errlen, e); delete h; return rc; }
+    rc = h->h.finalize();
+    if (rc) { set_err(err, errlen, h->h.error); delete h; return rc; }
+    *out = h;
+    return 0;
+  } catch (const std::bad_alloc&) {
+    set_err(err, errlen, "out of memory");
+    return S2LC_ENOMEM;
+  } catch (...) {
+    set_err(err, errlen, "internal error");
+    return S2LC_EINVAL;
+  }
+}
+
+int s2lc_history_from_events(const s2lc_event* ev, size_t n, s2lc_history** out, char* err, size_t errlen) {
+  if (!out || (!ev && n)) return S2LC_EINVAL;
+  *out = nullptr;
+  try {
+    s2lc_history* h = new s2lc_history();
+    History& H = h->h;
+    H.events.reserve(n);
+    for (size_t i = 0; i < n; ++i) {
+      const s2lc_event& x = ev[i];
+      Event e;
+      if (x.kind != S2LC_CALL_EVENT && x.kind != S2LC_RETURN_EVENT) {
+        set_err(err, errlen, "event " + std::to_string(i) + ": bad kind");
+        delete h;
+        return S2LC_EINVAL;
+      }
+      e.kind = x.kind;
+      e.op_id = x.op_id;
+      e.client_id = x.client_id;
+      if (x.kind == S2LC_CALL_EVENT) {
+        e.input_type = x.input_type;
+        e.has_num_records = x.has_num_records;
+        e.num_records = x.num_records;
+        e.has_msn = x.has_match_seq_num;
+        e.msn = x.match_seq_num;
+        e.set_tok = x.set_fencing_token ? H.intern(x.set_fencing_token) : 0;
+        e.batch_tok = x.fencing_token ? H.intern(x.fencing_token) : 0;
+        e.hash_off = H.pool.size();
+        e.hash_cnt = x.n_record_hashes;
+        if (x.n_record_hashes) {
+          if (!x.record_hashes) { delete h; set_err(err, errlen, "null record_hashes"); return S2LC_EINVAL; }
+          H.pool.insert(H.pool.end(), x.record_hashes, x.record_hashes + x.n_record_hashes);
+        }
+      } else {
+        e.failure = x.failure;
+        e.definite = x.definite_failure;
+        e.has_tail = x.has_tail;
+        e.tail = x.tail;
+        e.has_hash = x.has_stream_hash;
+        e.stream_hash = x.stream_hash;
+      }
+      H.events.push_back(e);
+    }
+    int rc = H.finalize();
+    if (rc) { set_err(err, errlen, H.error); delete h; return rc; }
+    *out = h;
+    return 0;
+  } catch (const std::bad_alloc&) {
+    set_err(err, errlen, "out of memory");
+    return S2LC_ENOMEM;
+  } catch (...) {
+    set_err(err, errlen, "internal error");
+    return S2LC_EINVAL;
+  }
+}
+
+void s2lc_history_free(s2lc_history* h) { delete h; }
+
+size_t s2lc_history_event_count(const s2lc_history* h) { return h ? h->h.events.size() : 0; }
+
+int s2lc_history_get_event(const s2lc_history* h, size_t i, s2lc_event* out) {
+  if (!h || !out || i >= h->h.events.size()) return S2LC_EINVAL;
+  const History& H = h->h;
+  const Event& e = H.events[i];
+  memset(out, 0, sizeof *out);
+  out->kind = e.kind;
+  out->op_id = e.op_id;
+  out->client_id = e.client_id;
+  if (e.kind == 0) {
+    out->input_type = e.input_type;
+    out->has_num_records = e.has_num_records;
+    out->num_records = e.num_records;
+    out->has_match_seq_num = e.has_msn;
+    out->match_seq_num = e.msn;
+    out->set_fencing_token = e.set_tok ? H.tokens[e.set_tok - 1].c_str() : nullptr;
+    out->fencing_token = e.batch_tok ? H.tokens[e.batch_tok - 1].c_str() : nullptr;
+    out->record_hashes = e.hash_cnt ? H.pool.data() + e.hash_off : nullptr;
+    out->n_record_hashes = e.hash_cnt;
+  } else {
+    out->failure = e.failure;
+    out->definite_failure = e.definite;
+    out->has_tail = e.has_tail;
+    out->tail = e.tail;
+    out->has_stream_hash = e.has_hash;
+    out->stream_hash = e.stream_hash;
+  }
+  return 0;
+}
+
+int s2lc_history_info_get(const s2lc_history* h, s2lc_history_info* out) {
+  if (!h || !out) return S2LC_EINVAL;
+  const History& H = h->h;
+  out->n_events = (uint32_t)H.events.size();
+  out->n_ops = H.n_ops;
+  out->n_chains = H.K;
+  out->n_tokens = (uint32_t)H.tokens.size();
+  out->n_record_hashes = H.pool.size();
+  out->structural = H.structural;
+  out->n_identity_ops = H.n_ident;
+  return 0;
+}
+
+// --------------------------------------------------------------- checker ---
+int s2lc_batch_create(s2lc_ctx* c, const s2lc_history* const* hs, size_t n, s2lc_batch** out) {
+  if (!c || !out || (!hs && n)) return S2LC_EINVAL;
+  *out = nullptr;
+  try {
+    if (hipSetDevice(c->device) != hipSuccess) { c->err = "hipSetDevice failed"; return S2LC_EHIP; }
+    s2lc_batch* b = new s2lc_batch();
+    b->b.device = c->device;
+    std::vector<const History*> v(n);
+    for (size_t i = 0; i < n; ++i) {
+      if (!hs[i]) { delete b; c->err = "null history"; return S2LC_EINVAL; }
+      v[i] = &hs[i]->h;
+    }
+    std::string e;
+    int rc = batch_upload(b->b, v, e);
+    if (rc) { c->err = e; batch_release(b->b); delete b; return rc; }
+    *out = b;
+    return 0;
+  } catch (const std::bad_alloc&) {
+    c->err = "out of memory";
+    return S2LC_ENOMEM;
+  } catch (...) {
+    c->err = "internal error";
+    return S2LC_EINVAL;
+  }
+}
+
+void s2lc_batch_free(s2lc_batch* b) {
+  if (!b) return;
+  (void)hipSetDevice(b->b.device);
+  batch_release(b->b);
+  delete b;
+}
+
+int s2lc_batch_run(s2lc_ctx* c, s2lc_batch* b) {
+  if (!c || !b) return S2LC_EINVAL;
+  try {
+    if (hipSetDevice(c->device) != hipSuccess) { c->err = "hipSetDevice failed"; return S2LC_EHIP; }
+    const bool witness = !(c->flags & S2LC_F_NO_WITNESS);
+    std::string e;
+    int rc = batch_run(b->b, c->stream, c->max_configs, witness, b->stats, e);
+    if (rc) { c->err = e; return rc; }
+    b->ran = true;
+    b->witness = witness;
+    return 0;
+  } catch (...) {
+    c->err = "internal error";
+    return S2LC_EINVAL;
+  }
+}
+
+int s2lc_batch_results(s2lc_ctx* c, s2lc_batch* b, s2lc_result* out, int with_witness) {
+  if (!c || !b || (!out && b->b.n_hist)) return S2LC_EINVAL;
+  if (!b->ran) { c->err = "batch has not been run"; return S2LC_EINVAL; }
+  try {
+    DevBatch& B = b->b;
+    const bool want_w = with_witness && b->witness;
+    if (want_w && B.n_hist) {
+      B.h_moves.resize(B.moves_cap);
+      if (hipMemcpy(B.h_moves.data(), B.moves, B.moves_cap * sizeof(uint32_t), hipMemcpyDeviceToHost) != hipSuccess) {
+        c->err = "copy witness moves";
+        return S2LC_EHIP;
+      }
+    }
+    for (uint32_t i = 0; i < B.n_hist; ++i) {
+      const HistResult& r = B.h_res[i];
+      s2lc_result& o = out[i];
+      memset(&o, 0, sizeof o);
+      o.verdict = (int32_t)r.verdict;
+      o.reason = (int32_t)r.reason;
+      o.configs_explored = r.configs;
+      o.rounds = r.rounds;
+      o.n_ops = B.src[i]->n_ops;
+      o.device_ms = b->stats.kernel_ms;
+      if (want_w && r.verdict == V_OK && r.has_witness == 1) {
+        const History& H = *B.src[i];
+        std::vector<uint32_t> order;
+        const bool ok = rebuild_linearization(H, B.h_moves.data() + r.witness_off, r.witness_len, r.p4 != 0, order) &&
+                        replay_order(H, order.data(), order.size());
+        if (!ok) {
+          o.reason = S2LC_R_WITNESS_INVALID;
+          continue;
+        }
+        o.witness = (int64_t*)malloc(sizeof(int64_t) * (order.size() ? order.size() : 1));
+        if (!o.witness) { c->err = "out of memory"; return S2LC_ENOMEM; }
+        for (size_t k = 0; k < order.size(); ++k) o.witness[k] = H.op_ids[order[k]];
+        o.witness_len = (uint32_t)order.size();
+      }
+    }
+    return 0;
+  } catch (const std::bad_alloc&) {
+    c->err = "out of memory";
+    return S2LC_ENOMEM;
+  } catch (...) {
+    c->err = "internal error";
+    return S2LC_EINVAL;
+  }
+}
+
+int s2lc_batch_check(s2lc_ctx* c, s2lc_batch* b, s2lc_result* out) {
+  int rc = s2lc_batch_run(c, b);
+  if (rc) return rc;
+  return s2lc_batch_results(c, b, out, 1);
+}
+
+int s2lc_batch_stats_get(const s2lc_batch* b, s2lc_batch_stats* out) {
+  if (!b || !out) return S2LC_EINVAL;
+  out->kernel_ms = b->stats.kernel_ms;
+  out->total_ms = b->stats.total_ms;
+  out->configs_explored = b->stats.configs;
+  out->children_generated = b->stats.children;
+  out->rounds = b->stats.rounds;
+  out->algo_bytes = b->stats.algo_bytes;
+  out->n_overflow = b->stats.n_overflow;
+  out->launches = b->stats.launches;
+  return 0;
+}
+
+int s2lc_check_batch(s2lc_ctx* c, const s2lc_history* const* hs, size_t n, s2lc_result* out) {
+  s2lc_batch* b = nullptr;
+  int rc = s2lc_batch_create(c, hs, n, &b);
+  if (rc) return rc;
+  rc = s2lc_batch_check(c, b, out);
+  s2lc_batch_free(b);
+  return rc;
+}
+
+int s2lc_check(s2lc_ctx* c, const s2lc_history* h, s2lc_result* out) {
+  if (!h) return S2LC_EINVAL;
+  const s2lc_history* one[1] = {h};
+  return s2lc_check_batch(c, one, 1, out);
+}
+
+void s2lc_result_free(s2lc_result* r) {
+  if (!r) return;
+  free(r->witness);
+  r->witness = nullptr;
+  r->witness_len = 0;
+}
+
+// ----------------------------------------------------------------- model ---
+int s2lc_step_cpu(const s2lc_history* h, const s2lc_state* s, uint32_t op, s2lc_state out[2]) {
+  if (!h || !s || !out) return S2LC_EINVAL;
+  const History& H = h->h;
+  if (op >= H.n_ops || H.op_call[op] == EV_INF || H.op_ret[op] == EV_INF) return S2LC_EINVAL;
+  const OpRec r = H.rec_of(op);
+  State st{s->tail, s->stream_hash, s->token};
+  State kids[2];
+  const int n = s2_step(r, st, H.pool.data(), kids);
+  for (int k = 0; k < n; ++k) {
+    out[k].tail = kids[k].tail;
+    out[k].stream_hash = kids[k].hash;
+    out[k].token = kids[k].tok;
+    out[k]._pad = 0;
+  }
+  return n;
+}
+
+uint64_t s2lc_chain_hash(uint64_t h, uint64_t r) { return chain_hash(h, r); }
+
+uint64_t s2lc_fold_record_hashes(uint64_t h, const uint64_t* r, size_t n) {
+  for (size_t i = 0; i < n; ++i) h = chain_hash(h, r[i]);
+  return h;
+}
+
+int s2lc_replay(const s2lc_history* h, const uint32_t* order, size_t n) {
+  if (!h || (!order && n)) return S2LC_EINVAL;
+  return replay_order(h->h, order, n) ? 0 : -1;
+}
+
+// ------------------------------------------------------------- simulator ---
+void s2lc_sim_params_default(s2lc_sim_params* p) {
+  if (!p) return;
+  memset(p, 0, sizeof *p);
+  p->struct_size = sizeof *p;
+  p->workflow = S2LC_WF_REGULAR;
+  p->num_clients = 5;       // collect-history.rs defaults
+  p->ops_per_client = 100;
+  p->seed = 1;
+  p->p_indefinite = 0.01;
+  p->p_definite = 0.02;
+  p->p_read_failure = 0.01;
+  p->p_check_tail_failure = 0.01;
+  p->max_client_ids = 20;
+}
+
+int s2lc_simulate_jsonl(const s2lc_sim_params* p, uint8_t** out, size_t* len) {
+  if (!p || !out || !len) return S2LC_EINVAL;
+  try {
+    std::string s;
+    int rc = simulate(*p, nullptr, &s);
+    if (rc) return rc;
+    uint8_t* m = (uint8_t*)malloc(s.size() + 1);
+    if (!m) return S2LC_ENOMEM;
+    memcpy(m, s.data(), s.size());
+    m[s.size()] = 0;
+    *out = m;
+    *len = s.size();
+    return 0;
+  } catch (...) {
+    return S2LC_ENOMEM;
+  }
+}
+
+int s2lc_simulate_history(const s2lc_sim_params* p, s2lc_history** out) {
+  if (!p || !out) return S2LC_EINVAL;
+  *out = nullptr;
+  try {
+    s2lc_history* h = new s2lc_history();
+    int rc = simulate(*p, &h->h, nullptr);
+    if (!rc) rc = h->h.finalize();
+    if (rc) { delete h; return rc; }
+    *out = h;
+    return 0;
+  } catch (...) {
+    return S2LC_ENOMEM;
+  }
+}
+
+void s2lc_free(void* p) { free(p); }
+
+}  // extern "C"

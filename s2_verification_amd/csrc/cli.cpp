@@ -1,0 +1,117 @@
+// cli.cpp — s2-porcupine: drop-in for golang/s2-porcupine/main.go:568-640.
+//   -file=<path> | -file - (stdin) | -version ; exit 0 = linearizable, 1 otherwise
+//   stderr: slog-style JSON lines ("passed: is linearizable" /
+//   "failed: is NOT linearizable" with res), "failed to decode history: ..."
+// The check runs on the GPU through libs2lincheck (s2lc_check).
+#include <stdio.h>
+#include <stdlib.h>
+#include <string.h>
+#include <time.h>
+
+#include <string>
+
+#include "s2lincheck.h"
+
+#ifndef S2LC_CLI_VERSION
+#define S2LC_CLI_VERSION "v0.4.1-gfx950"
+#endif
+
+static std::string now_rfc3339() {
+  char buf[64];
+  struct timespec ts;
+  clock_gettime(CLOCK_REALTIME, &ts);
+  struct tm tm;
+  localtime_r(&ts.tv_sec, &tm);
+  size_t n = strftime(buf, sizeof buf, "%Y-%m-%dT%H:%M:%S", &tm);
+  snprintf(buf + n, sizeof buf - n, ".%06ld", ts.tv_nsec / 1000);
+  n = strlen(buf);
+  strftime(buf + n, sizeof buf - n, "%z", &tm);
+  std::string s(buf);
+  if (s.size() >= 5) s.insert(s.size() - 2, ":");
+  return s;
+}
+
+static std::string jstr(const std::string& s) {
+  std::string o = "\"";
+  for (char c : s) {
+    if (c == '"' || c == '\\') { o += '\\'; o += c; }
+    else if ((unsigned char)c < 0x20) { char b[8]; snprintf(b, sizeof b, "\\u%04x", c); o += b; }
+    else o += c;
+  }
+  return o + "\"";
+}
+
+static void slog(const char* level, const std::string& msg, const std::string& extra = "") {
+  fprintf(stderr, "{\"time\":%s,\"level\":\"%s\",\"msg\":%s%s}\n", jstr(now_rfc3339()).c_str(), level,
+          jstr(msg).c_str(), extra.c_str());
+}
+
+int main(int argc, char** argv) {
+  const char* file = nullptr;
+  bool version = false;
+  for (int i = 1; i < argc; ++i) {  // Go flag syntax: -flag, --flag, -flag=value, -flag value
+    const char* a = argv[i];
+    if (a[0] != '-') break;
+    const char* n = a + 1;
+    if (*n == '-') ++n;
+    if (!strcmp(n, "version") || !strcmp(n, "version=true")) version = true;
+    else if (!strncmp(n, "file=", 5)) file = n + 5;
+    else if (!strcmp(n, "file") && i + 1 < argc) file = argv[++i];
+    else if (!strcmp(n, "h") || !strcmp(n, "help")) {
+      fprintf(stderr, "Usage of %s:\n  -file string\n    \tpath to JSONL records file (use '-' for stdin)\n  -version\n    \tshow version information\n", argv[0]);
+      return 0;
+    } else {
+      fprintf(stderr, "flag provided but not defined: %s\n", a);
+      return 2;
+    }
+  }
+  if (version) {
+    printf("s2-porcupine version %s\n", S2LC_CLI_VERSION);
+    return 0;
+  }
+  if (!file || !*file) {
+    fprintf(stderr, "usage: %s -file=records-<epoch>.jsonl\n", argv[0]);
+    return 1;
+  }
+  char err[1024] = {0};
+  s2lc_history* h = nullptr;
+  int rc = s2lc_load_jsonl(file, nullptr, 0, &h, err, sizeof err);
+  if (rc == S2LC_EIO) {
+    slog("ERROR", "open file", ",\"path\":" + jstr(file) + ",\"err\":" + jstr(err));
+    return 1;
+  }
+  if (rc) {
+    fprintf(stderr, "failed to decode history: %s\n", err);
+    return 1;
+  }
+  s2lc_opts o;
+  memset(&o, 0, sizeof o);
+  o.struct_size = sizeof o;
+  o.device = -1;
+  int st = 0;
+  s2lc_ctx* ctx = s2lc_create(&o, &st);
+  if (!ctx) {
+    fprintf(stderr, "s2-porcupine: no usable GPU (status %d)\n", st);
+    s2lc_history_free(h);
+    return 1;
+  }
+  s2lc_result r;
+  memset(&r, 0, sizeof r);
+  rc = s2lc_check(ctx, h, &r);
+  if (rc) {
+    fprintf(stderr, "s2-porcupine: check failed: %s\n", s2lc_last_error(ctx));
+    s2lc_destroy(ctx);
+    s2lc_history_free(h);
+    return 1;
+  }
+  const bool ok = r.verdict == S2LC_OK;
+  if (ok) {
+    slog("INFO", "passed: is linearizable");
+  } else {
+    slog("ERROR", "failed: is NOT linearizable", std::string(",\"res\":\"") + (r.verdict == S2LC_ILLEGAL ? "Illegal" : "Unknown") + "\"");
+  }
+  s2lc_result_free(&r);
+  s2lc_destroy(ctx);
+  s2lc_history_free(h);
+  return ok ? 0 : 1;
+}

@@ -1,0 +1,192 @@
+// history.cpp — History::finalize: validation, porcupine renumbering, op
+// classification and chain decomposition.
+//
+// Reference semantics:
+//   renumber / makeLinkedEntries / checkSingle  porcupine v1.0.3 (upstream)
+//   s2Model.Step                                main.go:264-335
+#include <algorithm>
+#include <queue>
+#include <unordered_map>
+
+#include "history.h"
+#include "s2lincheck.h"
+
+namespace s2lc {
+
+uint32_t History::intern(const std::string& s) {
+  for (size_t i = 0; i < tokens.size(); ++i)
+    if (tokens[i] == s) return (uint32_t)(i + 1);
+  tokens.push_back(s);
+  return (uint32_t)tokens.size();
+}
+
+static uint32_t classify(const Event& in, const Event& out) {
+  uint32_t f = in.input_type & OPF_KIND_MASK;
+  if (out.failure) f |= OPF_FAIL;
+  if (out.definite) f |= OPF_DEF;
+  if (out.has_tail) f |= OPF_HAS_TAIL;
+  if (out.has_hash) f |= OPF_HAS_HASH;
+  if (in.has_msn) f |= OPF_HAS_MSN;
+  if (in.input_type == S2LC_INPUT_APPEND) {
+    if (out.failure && out.definite) f |= OPF_CLS_E;       // main.go:283-285: {s}
+    else if (out.failure) f |= OPF_CLS_I;                  // main.go:286-300: {s} or {opt, s}
+    else f |= OPF_CLS_D | OPF_CONSTRAIN;                   // main.go:301-318: {} or {opt}
+  } else {
+    f |= OPF_CLS_E;                                        // main.go:320-331: {} or {s}
+    if (!out.failure || out.has_hash) f |= OPF_CONSTRAIN;
+  }
+  return f;
+}
+
+OpRec History::rec_of(uint32_t d) const {
+  const Event& in = events[op_call[d]];
+  const Event& out = events[op_ret[d]];
+  OpRec r{};
+  r.num_records = in.num_records;
+  r.msn = in.msn;
+  r.out_tail = out.tail;
+  r.out_hash = out.stream_hash;
+  r.sufmin = REQ_NONE;
+  r.call_ev = op_call[d];
+  r.ret_ev = op_ret[d];
+  r.hash_off = (uint32_t)in.hash_off;
+  r.hash_cnt = (uint32_t)in.hash_cnt;
+  r.batch_tok = (uint16_t)in.batch_tok;
+  r.set_tok = (uint16_t)in.set_tok;
+  r.flags = classify(in, out);
+  return r;
+}
+
+int History::finalize() {
+  status = 0;
+  error.clear();
+  structural = 0;
+  const size_t E = events.size();
+  if (E >= (size_t)EV_INF) { status = S2LC_EUNSUPPORTED; error = "too many events"; return status; }
+
+  // porcupine renumber(): ids -> 0..m-1 in order of first appearance.
+  std::unordered_map<int64_t, uint32_t> idmap;
+  idmap.reserve(E);
+  std::vector<uint32_t> dense(E);
+  std::vector<int64_t> ids;
+  for (size_t i = 0; i < E; ++i) {
+    auto it = idmap.find(events[i].op_id);
+    if (it == idmap.end()) {
+      it = idmap.emplace(events[i].op_id, (uint32_t)ids.size()).first;
+      ids.push_back(events[i].op_id);
+    }
+    dense[i] = it->second;
+  }
+  const uint32_t m = (uint32_t)ids.size();
+  std::vector<uint32_t> ncall(m, 0), nret(m, 0), call(m, EV_INF), ret(m, EV_INF);
+  for (size_t i = 0; i < E; ++i) {
+    const uint32_t d = dense[i];
+    if (events[i].kind == 0) { ncall[d]++; call[d] = (uint32_t)i; }
+    else { nret[d]++; ret[d] = (uint32_t)i; }
+  }
+  for (uint32_t d = 0; d < m; ++d) {
+    if (ncall[d] > 1 || nret[d] > 1) {
+      status = S2LC_EUNSUPPORTED;
+      error = "op_id " + std::to_string(ids[d]) + " has more than one Start or Finish";
+      return status;
+    }
+  }
+  // Validate what the Go model would dereference (main.go:279, 313, 327).
+  for (size_t i = 0; i < E; ++i) {
+    const Event& e = events[i];
+    if (e.kind == 0) {
+      if (e.input_type > 2) { status = S2LC_EINVAL; error = "unknown input type"; return status; }
+      if (e.input_type == S2LC_INPUT_APPEND && !e.has_num_records) {
+        status = S2LC_EINVAL; error = "append without num_records"; return status;
+      }
+    } else if (!e.failure && !e.has_tail) {
+      status = S2LC_EINVAL; error = "success output without tail"; return status;
+    }
+  }
+  for (uint32_t d = 0; d < m; ++d)
+    if (ncall[d] != 1 || nret[d] != 1 || ret[d] < call[d]) structural = S2LC_R_UNMATCHED;
+
+  n_ops = m;
+  op_ids = ids;
+  op_call = call;
+  op_ret = ret;
+  recs.clear(); rec_op.clear(); op_rec.assign(m, EV_INF); chain_start.clear(); K = 0;
+  n_ident = 0; hflags = 0; max_chain_len = 0;
+  if (structural) return 0;  // verdict fixed: checkSingle's list can never empty
+
+  // Well formed: each id's first event is its call, so dense order == call order.
+  // Overflow-free tail bound (enables the P1 prune).
+  uint64_t total = 0;
+  bool nowrap = true, zero_with_hashes = false;
+  for (uint32_t d = 0; d < m; ++d) {
+    const Event& in = events[call[d]];
+    if (in.input_type != S2LC_INPUT_APPEND) continue;
+    if (in.num_records > (1ull << 63) - total) nowrap = false;
+    else total += in.num_records;
+    if (in.num_records == 0 && in.hash_cnt > 0) zero_with_hashes = true;
+  }
+  if (nowrap) hflags |= H_NOWRAP;
+  if (nowrap && !zero_with_hashes) hflags |= H_P2OK;
+
+  // Greedy interval colouring (ops by call order; reuse the chain that
+  // finished earliest if it finished before this call): K = max overlap.
+  std::vector<std::vector<uint32_t>> chains;
+  using P = std::pair<uint32_t, uint32_t>;  // (last ret, chain)
+  std::priority_queue<P, std::vector<P>, std::greater<P>> heap;
+  for (uint32_t d = 0; d < m; ++d) {
+    uint32_t c;
+    if (!heap.empty() && heap.top().first < call[d]) { c = heap.top().second; heap.pop(); }
+    else { c = (uint32_t)chains.size(); chains.emplace_back(); }
+    chains[c].push_back(d);
+    heap.push({ret[d], c});
+  }
+  K = (uint32_t)chains.size();
+  chain_start.resize(K + 1);
+  uint32_t pos = 0;
+  for (uint32_t c = 0; c < K; ++c) {
+    chain_start[c] = pos;
+    pos += (uint32_t)chains[c].size() + 1;
+    max_chain_len = std::max<uint32_t>(max_chain_len, (uint32_t)chains[c].size());
+  }
+  chain_start[K] = pos;
+  recs.assign(pos, OpRec{});
+  rec_op.assign(pos, EV_INF);
+  for (uint32_t c = 0; c < K; ++c) {
+    uint32_t p = chain_start[c];
+    for (uint32_t d : chains[c]) {
+      OpRec& r = recs[p];
+      r = rec_of(d);
+      if (r.flags & OPF_CLS_E) n_ident++;
+      rec_op[p] = d;
+      op_rec[d] = p;
+      ++p;
+    }
+    OpRec& s = recs[p];  // sentinel
+    s.call_ev = EV_INF;
+    s.ret_ev = EV_INF;
+    s.flags = OPF_SENTINEL;
+    s.sufmin = REQ_NONE;
+    // suffix minimum of the pre-tail each constraining op requires
+    uint64_t run = REQ_NONE;
+    for (uint32_t q = p; q-- > chain_start[c];) {
+      OpRec& r = recs[q];
+      if (r.flags & OPF_CONSTRAIN) {
+        uint64_t req;
+        if ((r.flags & OPF_KIND_MASK) == S2LC_INPUT_APPEND)
+          req = r.out_tail >= r.num_records ? r.out_tail - r.num_records : 0;  // 0: unsatisfiable
+        else if (!(r.flags & OPF_FAIL))
+          req = r.out_tail;
+        else
+          req = REQ_HASH_ONLY;
+        if (req > REQ_HASH_ONLY) req = REQ_HASH_ONLY;
+        run = std::min(run, req);
+      }
+      r.sufmin = run;
+    }
+  }
+  if (tokens.size() > 0xFFFF) { status = S2LC_EUNSUPPORTED; error = "more than 65535 distinct fencing tokens"; }
+  if (pool.size() > 0xFFFFFFFFull) { status = S2LC_EUNSUPPORTED; error = "more than 2^32 record hashes"; }
+  return status;
+}
+
+}  // namespace s2lc

@@ -1,0 +1,69 @@
+// history.h — host-side history representation (C++).
+//
+// A History holds the porcupine event list (main.go:529-563 output) and the
+// derived search layout: dense op ids (porcupine renumber: first appearance),
+// greedy interval-colouring chains, and the chain-major OpRec table that the
+// gfx950 kernels read.
+#pragma once
+#include <stdint.h>
+
+#include <string>
+#include <vector>
+
+#include "model.h"
+
+namespace s2lc {
+
+struct Event {
+  int32_t kind = 0;  // 0 call, 1 return
+  int64_t op_id = 0;
+  int64_t client_id = 0;
+  uint8_t input_type = 0, has_num_records = 0, has_msn = 0;
+  uint64_t num_records = 0, msn = 0;
+  uint32_t set_tok = 0, batch_tok = 0;  // interned ids, 0 = nil
+  uint64_t hash_off = 0, hash_cnt = 0;  // into History::pool
+  uint8_t failure = 0, definite = 0, has_tail = 0, has_hash = 0;
+  uint64_t tail = 0, stream_hash = 0;
+};
+
+enum : uint16_t {
+  H_NOWRAP = 0x1,  // sum of all num_records <= 2^63: tails never wrap, P1 prune valid
+  H_P2OK = 0x2,    // NOWRAP and no 0-record append carries hashes: equal tail => equal hash needed
+};
+
+struct History {
+  // ---- porcupine events ----
+  std::vector<Event> events;
+  std::vector<uint64_t> pool;         // record hashes
+  std::vector<std::string> tokens;    // token id i+1 -> string
+
+  uint32_t intern(const std::string& s);
+
+  // ---- derived by finalize() ----
+  int status = 0;                     // 0 ok, else s2lc_status (EINVAL / EUNSUPPORTED)
+  std::string error;
+  int structural = 0;                 // 0 or S2LC_R_UNMATCHED
+  uint32_t n_ops = 0;
+  uint32_t n_ident = 0;
+  std::vector<uint32_t> op_call, op_ret;   // event index per dense op id
+  std::vector<int64_t> op_ids;            // original Event.Id per dense op id
+  uint32_t K = 0;                          // chains
+  std::vector<uint32_t> chain_start;       // K+1 record positions (sentinels included)
+  std::vector<OpRec> recs;                 // chain-major, hash_off relative to pool
+  std::vector<uint32_t> rec_op;            // record position -> dense op id (UINT32_MAX = sentinel)
+  std::vector<uint32_t> op_rec;            // dense op id -> record position
+  uint16_t hflags = 0;
+  uint32_t max_chain_len = 0;
+
+  // Validate, renumber, classify, decompose into chains. Idempotent.
+  int finalize();
+  // OpRec of dense op d built from its call/return events (sufmin unset).
+  OpRec rec_of(uint32_t d) const;
+};
+
+// JSONL loader (eventsFromReader, main.go:529-563). Returns 0 or S2LC_EDECODE.
+int load_jsonl(const uint8_t* buf, size_t len, History& h, std::string& err);
+
+// Deterministic simulator (collector workload, history.rs + collect-history.rs).
+struct SimParams;
+}  // namespace s2lc

@@ -1,0 +1,550 @@
+// jsonl.cpp — collector JSONL -> History. Restates eventsFromReader
+// (golang/s2-porcupine/main.go:529-563) with Go encoding/json semantics:
+//   * a stream of JSON values (json.Decoder): any whitespace separation, no
+//     line-length limit (main_test.go:34-101);
+//   * Record{event, client_id, op_id} struct fields match keys
+//     case-insensitively (Go's fold, incl. U+212A KELVIN / U+017F LONG S), the
+//     last duplicate wins, unknown keys are ignored, null leaves a field as is;
+//   * EventWrapper / StartEvent / FinishEvent custom unmarshalers
+//     (main.go:32-70, 100-156, 163-188): map keys "Start", "Finish", "Append",
+//     "AppendSuccess", ... match exactly; a duplicate "event" key re-runs the
+//     wrapper's unmarshaler on the same value (Start/Finish accumulate);
+//   * integers decode only from integer literals in range (strconv.ParseUint /
+//     ParseInt), strings are UTF-8-sanitised (invalid bytes -> U+FFFD);
+//   * len(record_hashes) != num_records is an error (main.go:62-64).
+#include <stdio.h>
+#include <string.h>
+
+#include <string>
+#include <vector>
+
+#include "history.h"
+#include "s2lincheck.h"
+
+namespace s2lc {
+namespace {
+
+enum JType : uint8_t { J_NULL, J_FALSE, J_TRUE, J_NUM, J_STR, J_ARR, J_OBJ };
+
+struct JNode {
+  JType t;
+  uint32_t a;  // NUM: offset of literal; STR: string index; ARR/OBJ: first child slot
+  uint32_t b;  // NUM: literal length; ARR/OBJ: child count
+};
+
+struct Parser {
+  const uint8_t* p;
+  const uint8_t* end;
+  const uint8_t* base;
+  std::vector<JNode> nodes;
+  std::vector<uint32_t> kids;       // ARR: node ids; OBJ: (key string id, node id) pairs
+  std::vector<std::string> strs;
+  std::string err;
+  int depth = 0;
+
+  void reset() { nodes.clear(); kids.clear(); strs.clear(); }
+  bool fail(const char* msg) {
+    if (err.empty()) {
+      char buf[160];
+      snprintf(buf, sizeof buf, "%s at offset %zu", msg, (size_t)(p - base));
+      err = buf;
+    }
+    return false;
+  }
+  void ws() {
+    while (p < end && (*p == ' ' || *p == '\t' || *p == '\n' || *p == '\r')) ++p;
+  }
+  static void put_utf8(std::string& s, uint32_t cp) {
+    if (cp < 0x80) s.push_back((char)cp);
+    else if (cp < 0x800) { s.push_back((char)(0xC0 | (cp >> 6))); s.push_back((char)(0x80 | (cp & 0x3F))); }
+    else if (cp < 0x10000) {
+      s.push_back((char)(0xE0 | (cp >> 12))); s.push_back((char)(0x80 | ((cp >> 6) & 0x3F)));
+      s.push_back((char)(0x80 | (cp & 0x3F)));
+    } else {
+      s.push_back((char)(0xF0 | (cp >> 18))); s.push_back((char)(0x80 | ((cp >> 12) & 0x3F)));
+      s.push_back((char)(0x80 | ((cp >> 6) & 0x3F))); s.push_back((char)(0x80 | (cp & 0x3F)));
+    }
+  }
+  bool hex4(uint32_t& v) {
+    if (end - p < 4) return fail("bad \\u escape");
+    v = 0;
+    for (int i = 0; i < 4; ++i) {
+      uint8_t c = p[i];
+      v <<= 4;
+      if (c >= '0' && c <= '9') v |= c - '0';
+      else if (c >= 'a' && c <= 'f') v |= c - 'a' + 10;
+      else if (c >= 'A' && c <= 'F') v |= c - 'A' + 10;
+      else return fail("bad \\u escape");
+    }
+    p += 4;
+    return true;
+  }
+  // Decode a string literal (p at opening quote) with Go's replacement rules.
+  bool str(std::string& out) {
+    ++p;
+    out.clear();
+    while (true) {
+      if (p >= end) return fail("unexpected end of input in string");
+      uint8_t c = *p;
+      if (c == '"') { ++p; return true; }
+      if (c < 0x20) return fail("invalid character in string literal");
+      if (c == '\\') {
+        ++p;
+        if (p >= end) return fail("unexpected end of input in string");
+        uint8_t e = *p++;
+        switch (e) {
+          case '"': out.push_back('"'); break;
+          case '\\': out.push_back('\\'); break;
+          case '/': out.push_back('/'); break;
+          case 'b': out.push_back('\b'); break;
+          case 'f': out.push_back('\f'); break;
+          case 'n': out.push_back('\n'); break;
+          case 'r': out.push_back('\r'); break;
+          case 't': out.push_back('\t'); break;
+          case 'u': {
+            uint32_t cp;
+            if (!hex4(cp)) return false;
+            if (cp >= 0xD800 && cp < 0xDC00) {  // high surrogate: needs a low one
+              if (end - p >= 6 && p[0] == '\\' && p[1] == 'u') {
+                const uint8_t* save = p;
+                p += 2;
+                uint32_t lo;
+                if (!hex4(lo)) return false;
+                if (lo >= 0xDC00 && lo < 0xE000) cp = 0x10000 + ((cp - 0xD800) << 10) + (lo - 0xDC00);
+                else { cp = 0xFFFD; p = save; }
+              } else cp = 0xFFFD;
+            } else if (cp >= 0xDC00 && cp < 0xE000) cp = 0xFFFD;
+            put_utf8(out, cp);
+            break;
+          }
+          default: return fail("invalid escape in string literal");
+        }
+        continue;
+      }
+      if (c < 0x80) { out.push_back((char)c); ++p; continue; }
+      // validate one UTF-8 sequence; invalid byte -> U+FFFD (Go decodeState.unquote)
+      int n = 0; uint32_t cp = 0, minv = 0;
+      if ((c & 0xE0) == 0xC0) { n = 2; cp = c & 0x1F; minv = 0x80; }
+      else if ((c & 0xF0) == 0xE0) { n = 3; cp = c & 0x0F; minv = 0x800; }
+      else if ((c & 0xF8) == 0xF0) { n = 4; cp = c & 0x07; minv = 0x10000; }
+      bool ok = n > 0 && end - p >= n;
+      for (int i = 1; ok && i < n; ++i) {
+        if ((p[i] & 0xC0) != 0x80) ok = false;
+        else cp = (cp << 6) | (p[i] & 0x3F);
+      }
+      if (ok && (cp < minv || cp > 0x10FFFF || (cp >= 0xD800 && cp < 0xE000))) ok = false;
+      if (ok) { out.append((const char*)p, (size_t)n); p += n; }
+      else { put_utf8(out, 0xFFFD); ++p; }
+    }
+  }
+  bool number(uint32_t& node) {
+    const uint8_t* s = p;
+    if (*p == '-') ++p;
+    if (p >= end) return fail("unexpected end of input in number");
+    if (*p == '0') ++p;
+    else if (*p >= '1' && *p <= '9') { while (p < end && *p >= '0' && *p <= '9') ++p; }
+    else return fail("invalid character in numeric literal");
+    if (p < end && *p == '.') {
+      ++p;
+      if (p >= end || *p < '0' || *p > '9') return fail("invalid character after decimal point");
+      while (p < end && *p >= '0' && *p <= '9') ++p;
+    }
+    if (p < end && (*p == 'e' || *p == 'E')) {
+      ++p;
+      if (p < end && (*p == '+' || *p == '-')) ++p;
+      if (p >= end || *p < '0' || *p > '9') return fail("invalid character in exponent");
+      while (p < end && *p >= '0' && *p <= '9') ++p;
+    }
+    node = (uint32_t)nodes.size();
+    nodes.push_back({J_NUM, (uint32_t)(s - base), (uint32_t)(p - s)});
+    return true;
+  }
+  bool lit(const char* w, JType t, uint32_t& node) {
+    size_t n = strlen(w);
+    if ((size_t)(end - p) < n) { p = end; return fail("unexpected end of input"); }
+    if (memcmp(p, w, n) != 0) return fail("invalid literal");
+    p += n;
+    node = (uint32_t)nodes.size();
+    nodes.push_back({t, 0, 0});
+    return true;
+  }
+  bool value(uint32_t& node) {
+    ws();
+    if (p >= end) return fail("unexpected end of JSON input");
+    uint8_t c = *p;
+    if (c == '{') {
+      if (++depth > 10000) return fail("exceeded max depth");
+      ++p;
+      std::vector<uint32_t> local;
+      ws();
+      if (p < end && *p == '}') { ++p; }
+      else {
+        while (true) {
+          ws();
+          if (p >= end) return fail("unexpected end of JSON input");
+          if (*p != '"') return fail("invalid character looking for beginning of object key string");
+          std::string key;
+          if (!str(key)) return false;
+          ws();
+          if (p >= end) return fail("unexpected end of JSON input");
+          if (*p != ':') return fail("invalid character after object key");
+          ++p;
+          uint32_t v;
+          if (!value(v)) return false;
+          local.push_back((uint32_t)strs.size());
+          strs.push_back(std::move(key));
+          local.push_back(v);
+          ws();
+          if (p >= end) return fail("unexpected end of JSON input");
+          if (*p == ',') { ++p; continue; }
+          if (*p == '}') { ++p; break; }
+          return fail("invalid character after object key:value pair");
+        }
+      }
+      --depth;
+      node = (uint32_t)nodes.size();
+      nodes.push_back({J_OBJ, (uint32_t)kids.size(), (uint32_t)(local.size() / 2)});
+      kids.insert(kids.end(), local.begin(), local.end());
+      return true;
+    }
+    if (c == '[') {
+      if (++depth > 10000) return fail("exceeded max depth");
+      ++p;
+      std::vector<uint32_t> local;
+      ws();
+      if (p < end && *p == ']') { ++p; }
+      else {
+        while (true) {
+          uint32_t v;
+          if (!value(v)) return false;
+          local.push_back(v);
+          ws();
+          if (p >= end) return fail("unexpected end of JSON input");
+          if (*p == ',') { ++p; continue; }
+          if (*p == ']') { ++p; break; }
+          return fail("invalid character after array element");
+        }
+      }
+      --depth;
+      node = (uint32_t)nodes.size();
+      nodes.push_back({J_ARR, (uint32_t)kids.size(), (uint32_t)local.size()});
+      kids.insert(kids.end(), local.begin(), local.end());
+      return true;
+    }
+    if (c == '"') {
+      std::string s;
+      if (!str(s)) return false;
+      node = (uint32_t)nodes.size();
+      nodes.push_back({J_STR, (uint32_t)strs.size(), 0});
+      strs.push_back(std::move(s));
+      return true;
+    }
+    if (c == '-' || (c >= '0' && c <= '9')) return number(node);
+    if (c == 't') return lit("true", J_TRUE, node);
+    if (c == 'f') return lit("false", J_FALSE, node);
+    if (c == 'n') return lit("null", J_NULL, node);
+    return fail("invalid character looking for beginning of value");
+  }
+};
+
+// ---------------------------------------------------------- Go decoding ---
+struct Dec {
+  Parser& P;
+  std::string err;
+  explicit Dec(Parser& p) : P(p) {}
+
+  const JNode& n(uint32_t i) const { return P.nodes[i]; }
+  const char* type_name(uint32_t i) const {
+    switch (n(i).t) {
+      case J_NULL: return "null";
+      case J_FALSE: case J_TRUE: return "bool";
+      case J_NUM: return "number";
+      case J_STR: return "string";
+      case J_ARR: return "array";
+      default: return "object";
+    }
+  }
+  bool type_err(uint32_t i, const char* go_type) {
+    if (err.empty()) err = std::string("json: cannot unmarshal ") + type_name(i) + " into Go value of type " + go_type;
+    return false;
+  }
+  // Go struct-field key match: bytes.EqualFold semantics against an ASCII
+  // lower-case field name (k and s also match U+212A and U+017F).
+  static bool fold_eq(const std::string& key, const char* field) {
+    size_t i = 0, j = 0, fl = strlen(field);
+    while (i < key.size()) {
+      if (j >= fl) return false;
+      unsigned char c = (unsigned char)key[i];
+      char f = field[j];
+      if (c < 0x80) {
+        char lc = (c >= 'A' && c <= 'Z') ? (char)(c + 32) : (char)c;
+        if (lc != f) return false;
+        ++i; ++j;
+        continue;
+      }
+      if (key.compare(i, 3, "\xE2\x84\xAA") == 0 && f == 'k') { i += 3; ++j; continue; }  // KELVIN SIGN
+      if (key.compare(i, 2, "\xC5\xBF") == 0 && f == 's') { i += 2; ++j; continue; }      // LONG S
+      return false;
+    }
+    return j == fl;
+  }
+  // Map lookup (exact key, last duplicate wins).
+  int64_t map_get(uint32_t obj, const char* key) const {
+    const JNode& o = n(obj);
+    int64_t found = -1;
+    for (uint32_t k = 0; k < o.b; ++k)
+      if (P.strs[P.kids[o.a + 2 * k]] == key) found = P.kids[o.a + 2 * k + 1];
+    return found;
+  }
+  bool u64(uint32_t i, uint64_t& v, const char* go_type = "uint64") {
+    const JNode& x = n(i);
+    if (x.t == J_NULL) return true;  // null into a non-pointer: no-op
+    if (x.t != J_NUM) return type_err(i, go_type);
+    const uint8_t* s = P.base + x.a;
+    uint64_t r = 0;
+    for (uint32_t k = 0; k < x.b; ++k) {
+      uint8_t c = s[k];
+      if (c < '0' || c > '9') return type_err(i, go_type);  // sign, fraction, exponent
+      if (r > (~0ull - (c - '0')) / 10) return type_err(i, go_type);
+      r = r * 10 + (c - '0');
+    }
+    v = r;
+    return true;
+  }
+  bool i64(uint32_t i, int64_t& v) {
+    const JNode& x = n(i);
+    if (x.t == J_NULL) return true;
+    if (x.t != J_NUM) return type_err(i, "int");
+    const uint8_t* s = P.base + x.a;
+    uint32_t k = 0;
+    bool neg = false;
+    if (x.b && s[0] == '-') { neg = true; k = 1; }
+    uint64_t r = 0;
+    for (; k < x.b; ++k) {
+      uint8_t c = s[k];
+      if (c < '0' || c > '9') return type_err(i, "int");
+      if (r > (~0ull - (c - '0')) / 10) return type_err(i, "int");
+      r = r * 10 + (c - '0');
+    }
+    if (!neg && r > (uint64_t)INT64_MAX) return type_err(i, "int");
+    if (neg && r > (uint64_t)INT64_MAX + 1) return type_err(i, "int");
+    v = neg ? (int64_t)(0 - r) : (int64_t)r;
+    return true;
+  }
+  bool opt_str(uint32_t i, bool& has, std::string& s) {
+    const JNode& x = n(i);
+    if (x.t == J_NULL) { has = false; return true; }
+    if (x.t != J_STR) return type_err(i, "string");
+    has = true;
+    s = P.strs[x.a];
+    return true;
+  }
+  bool opt_u64(uint32_t i, bool& has, uint64_t& v) {
+    if (n(i).t == J_NULL) { has = false; return true; }
+    v = 0;
+    if (!u64(i, v)) return false;
+    has = true;
+    return true;
+  }
+
+  // AppendArgs (main.go:18-24) decoded into call event e.
+  bool append_args(uint32_t i, Event& e, History& h, std::vector<uint64_t>& hashes) {
+    const JNode& x = n(i);
+    if (x.t == J_NULL) return true;
+    if (x.t != J_OBJ) return type_err(i, "main.AppendArgs");
+    bool has_set = false, has_tok = false;
+    std::string set_s, tok_s;
+    for (uint32_t k = 0; k < x.b; ++k) {
+      const std::string& key = P.strs[P.kids[x.a + 2 * k]];
+      uint32_t v = P.kids[x.a + 2 * k + 1];
+      if (fold_eq(key, "num_records")) { if (!u64(v, e.num_records)) return false; }
+      else if (fold_eq(key, "record_hashes")) {
+        const JNode& a = n(v);
+        if (a.t == J_NULL) { hashes.clear(); continue; }
+        if (a.t != J_ARR) return type_err(v, "[]uint64");
+        hashes.assign(a.b, 0);
+        for (uint32_t q = 0; q < a.b; ++q) {
+          uint64_t hv = 0;
+          if (!u64(P.kids[a.a + q], hv)) return false;
+          hashes[q] = hv;
+        }
+      } else if (fold_eq(key, "set_fencing_token")) { if (!opt_str(v, has_set, set_s)) return false; }
+      else if (fold_eq(key, "fencing_token")) { if (!opt_str(v, has_tok, tok_s)) return false; }
+      else if (fold_eq(key, "match_seq_num")) {
+        bool hm = false; uint64_t mv = 0;
+        if (!opt_u64(v, hm, mv)) return false;
+        e.has_msn = hm; e.msn = mv;
+      }
+    }
+    e.set_tok = has_set ? h.intern(set_s) : 0;
+    e.batch_tok = has_tok ? h.intern(tok_s) : 0;
+    return true;
+  }
+
+  // StartEvent.UnmarshalJSON, main.go:32-70 + inputFromStart, main.go:428-464
+  bool start(uint32_t i, Event& e, History& h, std::vector<uint64_t>& hashes, bool& appended) {
+    const JNode& x = n(i);
+    if (x.t == J_STR || x.t == J_NULL) {  // json.Unmarshal(data, &str) succeeds
+      const std::string s = x.t == J_STR ? P.strs[x.a] : std::string();
+      if (s == "CheckTail") { e.input_type = S2LC_INPUT_CHECK_TAIL; return true; }
+      if (s == "Read") { e.input_type = S2LC_INPUT_READ; return true; }
+      err = "parsing Start: unknown string start event: " + s;
+      return false;
+    }
+    if (x.t != J_OBJ) { type_err(i, "map[string]json.RawMessage"); err = "parsing Start: " + err; return false; }
+    int64_t a = map_get(i, "Append");
+    if (a < 0) { err = "parsing Start: unknown start event format"; return false; }
+    e.input_type = S2LC_INPUT_APPEND;
+    e.has_num_records = 1;
+    e.num_records = 0;
+    hashes.clear();
+    if (!append_args((uint32_t)a, e, h, hashes)) { err = "parsing Start: parsing Append args: " + err; return false; }
+    if ((uint64_t)hashes.size() != e.num_records) {
+      err = "parsing Start: append has " + std::to_string(hashes.size()) + " record_hashes but " +
+            std::to_string(e.num_records) + " records";
+      return false;
+    }
+    appended = true;
+    return true;
+  }
+
+  bool result_obj(uint32_t i, Event& e, bool read, const char* go_type) {
+    const JNode& x = n(i);
+    e.failure = 0; e.definite = 0; e.has_tail = 1; e.tail = 0;
+    e.has_hash = read ? 1 : 0; e.stream_hash = 0;
+    if (x.t == J_NULL) return true;
+    if (x.t != J_OBJ) return type_err(i, go_type);
+    for (uint32_t k = 0; k < x.b; ++k) {
+      const std::string& key = P.strs[P.kids[x.a + 2 * k]];
+      uint32_t v = P.kids[x.a + 2 * k + 1];
+      if (fold_eq(key, "tail")) { if (!u64(v, e.tail)) return false; }
+      else if (read && fold_eq(key, "stream_hash")) { if (!u64(v, e.stream_hash)) return false; }
+    }
+    return true;
+  }
+
+  // FinishEvent.UnmarshalJSON, main.go:100-156 + outputFromFinish, main.go:466-523
+  bool finish(uint32_t i, Event& e) {
+    const JNode& x = n(i);
+    if (x.t == J_STR || x.t == J_NULL) {
+      const std::string s = x.t == J_STR ? P.strs[x.a] : std::string();
+      e.has_tail = 0; e.has_hash = 0;
+      if (s == "AppendDefiniteFailure") { e.failure = 1; e.definite = 1; return true; }
+      if (s == "AppendIndefiniteFailure") { e.failure = 1; e.definite = 0; return true; }
+      if (s == "ReadFailure" || s == "CheckTailFailure") { e.failure = 1; e.definite = 1; return true; }
+      err = "parsing Finish: unknown string finish event: " + s;
+      return false;
+    }
+    if (x.t != J_OBJ) { type_err(i, "map[string]json.RawMessage"); err = "parsing Finish: " + err; return false; }
+    int64_t v;
+    if ((v = map_get(i, "AppendSuccess")) >= 0) {
+      if (!result_obj((uint32_t)v, e, false, "main.AppendSuccessResult")) { err = "parsing Finish: parsing AppendSuccess result: " + err; return false; }
+      return true;
+    }
+    if ((v = map_get(i, "ReadSuccess")) >= 0) {
+      if (!result_obj((uint32_t)v, e, true, "main.ReadSuccessResult")) { err = "parsing Finish: parsing ReadSuccess result: " + err; return false; }
+      return true;
+    }
+    if ((v = map_get(i, "CheckTailSuccess")) >= 0) {
+      if (!result_obj((uint32_t)v, e, false, "main.CheckTailSuccessResult")) { err = "parsing Finish: parsing CheckTailSuccess result: " + err; return false; }
+      return true;
+    }
+    err = "parsing Finish: unknown finish event format";
+    return false;
+  }
+};
+
+}  // namespace
+
+int load_jsonl(const uint8_t* buf, size_t len, History& h, std::string& err) {
+  Parser P;
+  P.base = buf;
+  P.p = buf;
+  P.end = buf + len;
+  std::vector<uint64_t> hashes;
+  while (true) {
+    P.ws();
+    if (P.p >= P.end) return 0;  // io.EOF
+    const size_t rec_off = (size_t)(P.p - buf);
+    P.reset();
+    uint32_t root;
+    if (!P.value(root)) {
+      err = "decode record at byte offset " + std::to_string((size_t)(P.p - buf)) + ": " + P.err;
+      return S2LC_EDECODE;
+    }
+    Dec D(P);
+    const JNode& r = P.nodes[root];
+    // Record{Event EventWrapper; ClientID int; OpID int} (main.go:190-194)
+    bool has_start = false, has_finish = false;
+    Event se, fe;       // accumulated Start / Finish across duplicate "event" keys
+    bool se_append = false;
+    std::vector<uint64_t> se_hashes;
+    int64_t client = 0, op = 0;
+    bool ok = true;
+    if (r.t == J_OBJ) {
+      for (uint32_t k = 0; k < r.b && ok; ++k) {
+        const std::string& key = P.strs[P.kids[r.a + 2 * k]];
+        uint32_t v = P.kids[r.a + 2 * k + 1];
+        if (Dec::fold_eq(key, "event")) {
+          // EventWrapper.UnmarshalJSON (main.go:163-188), called even for null
+          const JNode& ev = P.nodes[v];
+          if (ev.t != J_OBJ && ev.t != J_NULL) { ok = D.type_err(v, "map[string]json.RawMessage"); break; }
+          if (ev.t == J_OBJ) {
+            int64_t s = D.map_get(v, "Start");
+            if (s >= 0) {
+              Event tmp;
+              bool app = false;
+              std::vector<uint64_t> hs;
+              if (!D.start((uint32_t)s, tmp, h, hs, app)) { ok = false; break; }
+              se = tmp; se_append = app; se_hashes.swap(hs);
+              has_start = true;
+            }
+            int64_t f = D.map_get(v, "Finish");
+            if (f >= 0) {
+              Event tmp;
+              if (!D.finish((uint32_t)f, tmp)) { ok = false; break; }
+              fe = tmp;
+              has_finish = true;
+            }
+          }
+          if (has_start == has_finish) {
+            D.err = std::string("expected exactly one of Start/Finish, got Start=") + (has_start ? "true" : "false") +
+                    " Finish=" + (has_finish ? "true" : "false");
+            ok = false;
+          }
+        } else if (Dec::fold_eq(key, "client_id")) {
+          ok = D.i64(v, client);
+        } else if (Dec::fold_eq(key, "op_id")) {
+          ok = D.i64(v, op);
+        }
+      }
+    } else if (r.t != J_NULL) {
+      ok = D.type_err(root, "main.Record");
+    }
+    if (!ok) {
+      err = "decode record at byte offset " + std::to_string((size_t)(P.p - buf)) + ": " + D.err;
+      return S2LC_EDECODE;
+    }
+    Event e;
+    if (has_start) {
+      e = se;
+      e.kind = 0;
+      if (se_append) {
+        e.hash_off = h.pool.size();
+        e.hash_cnt = se_hashes.size();
+        h.pool.insert(h.pool.end(), se_hashes.begin(), se_hashes.end());
+      }
+    } else if (has_finish) {
+      e = fe;
+      e.kind = 1;
+    } else {
+      err = "record at byte offset " + std::to_string(rec_off) + " has neither Start nor Finish event";
+      return S2LC_EDECODE;
+    }
+    e.op_id = op;
+    e.client_id = client;
+    h.events.push_back(e);
+  }
+}
+
+}  // namespace s2lc

@@ -1,0 +1,103 @@
+// search.h — device data layout of the frontier search and its host launcher.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include <vector>
+
+#include "history.h"
+
+namespace s2lc {
+
+constexpr uint32_t TRACE_NONE = 0xFFFFFFFFu;
+constexpr uint32_t MOVE_IDENT = 0x10000u;   // I-op taken with its identity outcome
+
+struct HistDesc {
+  uint32_t rec_base;   // first OpRec of the history in the batch table
+  uint32_t cs_base;    // chain_start entries (K+1, absolute rec indices)
+  uint16_t K;
+  uint16_t flags;      // H_NOWRAP | H_P2OK
+  uint32_t n_ops;
+};
+
+struct TraceEnt {
+  uint32_t parent;  // trace index of the parent configuration
+  uint32_t move;    // chain | MOVE_IDENT
+};
+
+enum : uint32_t { V_OK = 0, V_ILLEGAL = 1, V_UNKNOWN = 2 };
+
+struct HistResult {
+  uint32_t verdict;
+  uint32_t reason;
+  uint32_t rounds;
+  uint32_t final_parent;  // trace index of the parent of the completing config
+  uint32_t final_move;    // move that produced it
+  uint32_t p4;            // completed by the "no constraining op left" rule
+  uint64_t configs;       // unique configurations inserted
+  uint64_t children;      // successor configurations generated
+  uint32_t witness_off;   // into the witness move buffer
+  uint32_t witness_len;   // moves written (rounds on the path)
+  uint32_t has_witness;   // 0 none, 1 moves valid, 2 pending (set by search, resolved by walk)
+  uint32_t _pad;
+};
+
+struct SearchGeom {
+  uint32_t block;      // threads per workgroup (64 or 256)
+  uint32_t kmax;       // 16 / 32 / 64 / 128
+  uint32_t fcap;       // frontier capacity per workgroup
+  uint32_t chunk;      // expansion items per chunk
+  uint32_t ht_slots;   // power of two
+  uint32_t grid;       // workgroups
+  size_t cfg_bytes;
+  size_t slab_bytes;
+};
+
+struct DevBatch {
+  int device = 0;
+  uint32_t n_hist = 0;
+  uint32_t kmax = 16;
+  OpRec* recs = nullptr;
+  uint64_t* pool = nullptr;
+  uint32_t* chain_start = nullptr;
+  HistDesc* hist = nullptr;
+  uint32_t* order = nullptr;        // LPT processing order
+  HistResult* res = nullptr;
+  uint32_t* moves = nullptr;        // witness moves (per history at witness_off)
+  uint32_t* counter = nullptr;      // work counters (scheduling)
+  TraceEnt* trace = nullptr;
+  unsigned long long* trace_head = nullptr;
+  uint64_t trace_cap = 0;
+  uint8_t* slab = nullptr;
+  size_t slab_cap = 0;
+  // host mirrors
+  std::vector<HistDesc> h_hist;
+  std::vector<HistResult> h_res;
+  std::vector<uint32_t> h_moves_off;  // witness_off per history
+  uint64_t moves_cap = 0;
+  std::vector<uint32_t> h_moves;
+  std::vector<const History*> src;    // host histories (not owned)
+  std::vector<uint32_t> forced;       // per history: 0 search, else verdict fixed on host
+  uint64_t algo_bytes_inputs = 0;
+};
+
+struct RunStats {
+  double kernel_ms = 0, total_ms = 0;
+  uint64_t configs = 0, children = 0, rounds = 0;
+  uint64_t algo_bytes = 0;
+  uint32_t n_overflow = 0, launches = 0;
+};
+
+int batch_upload(DevBatch& b, const std::vector<const History*>& hs, std::string& err);
+void batch_release(DevBatch& b);
+int batch_run(DevBatch& b, hipStream_t stream, uint64_t max_configs, bool witness, RunStats& st,
+              std::string& err);
+
+// Host reconstruction of a full linearization (dense op ids) from the device
+// move list; returns false if any move is not a legal successor.
+bool rebuild_linearization(const History& h, const uint32_t* moves, uint32_t n_moves, bool p4,
+                           std::vector<uint32_t>& order);
+// Powerset replay of a linearization through the CPU model (+ real-time check).
+bool replay_order(const History& h, const uint32_t* order, size_t n);
+
+}  // namespace s2lc

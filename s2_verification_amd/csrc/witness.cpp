@@ -1,0 +1,127 @@
+// witness.cpp — host-side witness reconstruction and CPU-model replay.
+//
+// The device records, per round, the move (chain, outcome) that produced each
+// surviving configuration. For an Ok verdict the move list is expanded here
+// into a full linearization (identity ops re-derived by the same closure) and
+// then replayed through the CPU model with porcupine's powerset semantics
+// (NondeterministicModel.ToModel, main.go:253-361) plus a real-time check:
+// every GPU witness must replay cleanly (BASELINE.json north_star).
+#include <algorithm>
+#include <vector>
+
+#include "search.h"
+
+namespace s2lc {
+
+namespace {
+
+struct HostCfg {
+  std::vector<uint32_t> cnt;
+  State s{0, 0, 0};
+};
+
+const OpRec& head(const History& h, const HostCfg& c, uint32_t q) { return h.recs[h.chain_start[q] + c.cnt[q]]; }
+
+uint32_t min_ret(const History& h, const HostCfg& c) {
+  uint32_t m = EV_INF;
+  for (uint32_t q = 0; q < h.K; ++q) m = std::min(m, head(h, c, q).ret_ev);
+  return m;
+}
+
+// Same closure as the device (search.hip), recording the ops it linearizes.
+void close(const History& h, HostCfg& c, std::vector<uint32_t>& order) {
+  for (;;) {
+    const uint32_t mr = min_ret(h, c);
+    if (mr == EV_INF) return;
+    bool changed = false;
+    for (uint32_t q = 0; q < h.K; ++q) {
+      for (;;) {
+        const OpRec& r = head(h, c, q);
+        if (!(r.flags & OPF_CLS_E) || r.call_ev >= mr || !ident_legal(r, c.s)) break;
+        order.push_back(h.rec_op[h.chain_start[q] + c.cnt[q]]);
+        c.cnt[q]++;
+        changed = true;
+      }
+    }
+    if (!changed) return;
+  }
+}
+
+}  // namespace
+
+bool rebuild_linearization(const History& h, const uint32_t* moves, uint32_t n_moves, bool p4,
+                           std::vector<uint32_t>& order) {
+  order.clear();
+  if (h.structural) return false;
+  HostCfg c;
+  c.cnt.assign(h.K, 0);
+  close(h, c, order);
+  for (uint32_t m = 0; m < n_moves; ++m) {
+    const uint32_t j = moves[m] & 0xFFFFu;
+    const bool ident = moves[m] & MOVE_IDENT;
+    if (j >= h.K) return false;
+    const OpRec& r = head(h, c, j);
+    if (r.flags & (OPF_SENTINEL | OPF_CLS_E)) return false;
+    if (r.call_ev >= min_ret(h, c)) return false;  // not minimal
+    State kids[2];
+    const int nk = s2_step(r, c.s, h.pool.data(), kids);
+    State want = c.s;
+    if (!ident) {
+      if (!append_guards_ok(r, c.s)) return false;
+      want = append_opt(r, c.s, h.pool.data());
+    }
+    bool found = false;
+    for (int k = 0; k < nk; ++k) found |= state_eq(kids[k], want);
+    if (!found) return false;
+    c.s = want;
+    order.push_back(h.rec_op[h.chain_start[j] + c.cnt[j]]);
+    c.cnt[j]++;
+    close(h, c, order);
+  }
+  if (order.size() != h.n_ops) {
+    if (!p4) return false;
+    // P4 completion: nothing left constrains the state; finish in return order.
+    std::vector<uint32_t> rest;
+    for (uint32_t q = 0; q < h.K; ++q)
+      for (uint32_t p = h.chain_start[q] + c.cnt[q]; p + 1 < h.chain_start[q + 1]; ++p) rest.push_back(h.rec_op[p]);
+    std::sort(rest.begin(), rest.end(), [&](uint32_t a, uint32_t b) { return h.op_ret[a] < h.op_ret[b]; });
+    order.insert(order.end(), rest.begin(), rest.end());
+  }
+  return order.size() == h.n_ops;
+}
+
+bool replay_order(const History& h, const uint32_t* order, size_t n) {
+  if (h.structural || n != h.n_ops) return false;
+  std::vector<uint8_t> seen(h.n_ops, 0);
+  for (size_t i = 0; i < n; ++i) {
+    if (order[i] >= h.n_ops || seen[order[i]]) return false;
+    seen[order[i]] = 1;
+  }
+  // real time: call(order[i]) < ret(order[k]) for all k > i
+  uint32_t later_min_ret = EV_INF;
+  for (size_t i = n; i-- > 0;) {
+    if (h.op_call[order[i]] >= later_min_ret) return false;
+    later_min_ret = std::min(later_min_ret, h.op_ret[order[i]]);
+  }
+  // powerset replay (ToModel().Step + merge)
+  std::vector<State> set{State{0, 0, 0}}, next;
+  for (size_t i = 0; i < n; ++i) {
+    const OpRec r = h.rec_of(order[i]);
+    next.clear();
+    for (const State& s : set) {
+      State kids[2];
+      const int nk = s2_step(r, s, h.pool.data(), kids);
+      for (int k = 0; k < nk; ++k) {
+        bool dup = false;
+        for (const State& x : next) if (state_eq(x, kids[k])) { dup = true; break; }
+        if (!dup) next.push_back(kids[k]);
+      }
+    }
+    if (next.empty()) return false;
+    if (next.size() > (1u << 16)) return false;
+    set.swap(next);
+  }
+  return true;
+}
+
+}  // namespace s2lc

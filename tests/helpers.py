@@ -1,0 +1,126 @@
+"""Test helpers: golden fixtures, event conversion, random small histories.
+
+Random histories come from a sequential ground-truth execution with random
+real-time intervals around each linearization point, then optional output
+perturbations, so both Ok and Illegal verdicts occur. Their verdict is
+decided by the oracle (WGL restatement, cross-checked by brute force).
+"""
+import json
+import os
+import random
+
+import s2_verification_amd as s2
+
+GOLDEN = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
+
+
+def golden(name):
+    with open(os.path.join(GOLDEN, name)) as f:
+        return json.load(f)
+
+
+def to_s2_events(events):
+    """oracle dict events -> s2_verification_amd.Event list."""
+    out = []
+    for e in events:
+        if e["kind"] == "call":
+            v = s2.StreamInput(InputType=e["input_type"], SetFencingToken=e.get("set_fencing_token"),
+                               BatchFencingToken=e.get("fencing_token"), MatchSeqNum=e.get("match_seq_num"),
+                               NumRecords=e.get("num_records"), RecordHashes=list(e.get("record_hashes") or []))
+            out.append(s2.Event(s2.CallEvent, v, e["op_id"], e.get("client_id", 0)))
+        else:
+            v = s2.StreamOutput(Failure=e["failure"], DefiniteFailure=e["definite_failure"], Tail=e.get("tail"),
+                                StreamHash=e.get("stream_hash"))
+            out.append(s2.Event(s2.ReturnEvent, v, e["op_id"], e.get("client_id", 0)))
+    return out
+
+
+def from_s2_events(events):
+    """s2_verification_amd.Event list -> oracle dict events."""
+    out = []
+    for e in events:
+        v = e.Value
+        if e.Kind == s2.CallEvent:
+            out.append({"kind": "call", "op_id": e.Id, "client_id": e.ClientId, "input_type": v.InputType,
+                        "num_records": v.NumRecords, "match_seq_num": v.MatchSeqNum,
+                        "set_fencing_token": v.SetFencingToken, "fencing_token": v.BatchFencingToken,
+                        "record_hashes": list(v.RecordHashes)})
+        else:
+            out.append({"kind": "return", "op_id": e.Id, "client_id": e.ClientId, "failure": v.Failure,
+                        "definite_failure": v.DefiniteFailure, "tail": v.Tail, "stream_hash": v.StreamHash})
+    return out
+
+
+def _fold(h, rs):
+    for r in rs:
+        h = s2.chain_hash(h, r)
+    return h
+
+
+def random_history(rng: random.Random, n_ops: int, n_clients: int = 3, p_perturb: float = 0.15,
+                   tokens=("aaaaaa", "bbbbbb")):
+    """A random small history over n_clients (events as oracle dicts)."""
+    tail, h, tok = 0, 0, None
+    ops = []
+    t = 0.0
+    for i in range(n_ops):
+        kind = rng.choice(["append", "append", "read", "check_tail"])
+        op = {"op_id": i, "client_id": rng.randrange(n_clients)}
+        lin = t = t + rng.random()
+        op["call"] = lin - rng.random() * 3.0
+        op["ret"] = lin + rng.random() * 3.0
+        if kind == "append":
+            nrec = rng.randint(0, 3)
+            hs = [rng.getrandbits(64) for _ in range(nrec)]
+            set_tok = rng.choice(tokens) if rng.random() < 0.15 else None
+            batch_tok = rng.choice(tokens) if rng.random() < 0.15 else None
+            msn = (tail if rng.random() < 0.7 else tail + rng.randint(1, 3)) if rng.random() < 0.3 else None
+            guards = (batch_tok is None or batch_tok == tok) and (msn is None or msn == tail)
+            r = rng.random()
+            call = {"input_type": 0, "num_records": nrec, "record_hashes": hs, "set_fencing_token": set_tok,
+                    "fencing_token": batch_tok, "match_seq_num": msn}
+            if r < 0.2:
+                applied = guards and rng.random() < 0.5
+                out = {"failure": True, "definite_failure": False, "tail": None, "stream_hash": None}
+            elif r < 0.3 or not guards:
+                applied = False
+                out = {"failure": True, "definite_failure": True, "tail": None, "stream_hash": None}
+            else:
+                applied = True
+                out = None
+            if applied:
+                tail += nrec
+                h = _fold(h, hs)
+                if set_tok is not None:
+                    tok = set_tok
+            if out is None:
+                out = {"failure": False, "definite_failure": False, "tail": tail, "stream_hash": None}
+        elif kind == "read":
+            call = {"input_type": 1}
+            if rng.random() < 0.1:
+                out = {"failure": True, "definite_failure": True, "tail": None, "stream_hash": None}
+            else:
+                out = {"failure": False, "definite_failure": False, "tail": tail, "stream_hash": h}
+        else:
+            call = {"input_type": 2}
+            if rng.random() < 0.1:
+                out = {"failure": True, "definite_failure": True, "tail": None, "stream_hash": None}
+            else:
+                out = {"failure": False, "definite_failure": False, "tail": tail, "stream_hash": None}
+        if rng.random() < p_perturb:
+            if out["tail"] is not None and rng.random() < 0.5:
+                out["tail"] += rng.choice([-1, 1]) if out["tail"] > 0 else 1
+            elif out["stream_hash"] is not None:
+                out["stream_hash"] ^= 1 << rng.randrange(64)
+            elif out["failure"] and kind == "append":
+                out["definite_failure"] = not out["definite_failure"]
+        op.update(call_fields=call, out=out)
+        ops.append(op)
+    evs = []
+    for op in ops:
+        evs.append((op["call"], 0, {"kind": "call", "op_id": op["op_id"], "client_id": op["client_id"],
+                                    **op["call_fields"]}))
+        evs.append((op["ret"], 1, {"kind": "return", "op_id": op["op_id"], "client_id": op["client_id"],
+                                   **op["out"]}))
+    evs.sort(key=lambda x: (x[0], x[1]))
+    return [e for _, _, e in evs]
