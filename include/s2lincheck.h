@@ -155,6 +155,8 @@ void s2lc_history_free(s2lc_history* h);
 size_t s2lc_history_event_count(const s2lc_history* h);
 /* Export event i (pointers stay valid while h lives). */
 int s2lc_history_get_event(const s2lc_history* h, size_t i, s2lc_event* out);
+/* Bulk export of events [0, n); equal token strings share one pointer. */
+int s2lc_history_get_events(const s2lc_history* h, s2lc_event* out, size_t n);
 
 typedef struct s2lc_history_info {
   uint32_t n_events;

@@ -227,3 +227,31 @@ def load_jsonl(text):
             events.append({"kind": "call", **base, **_start_to_input(ev["Start"])})
         else:
             events.append({"kind": "return", **base, **_finish_to_output(ev["Finish"])})
+
+
+def from_s2lc_numpy(ev):
+    """Product-exported events (numpy array in the s2lc_event layout, see
+    s2_verification_amd.History.events_numpy) -> EventArray for the oracle.
+
+    Token ids are re-derived from the exported string pointers (one pointer per
+    distinct token string within a history); record-hash pointers are used as
+    they are, so the source history must outlive the returned array.
+    """
+    n = len(ev)
+    arr = np.zeros(n, dtype=EVENT_DTYPE)
+    for f_src, f_dst in (("kind", "kind"), ("op_id", "op_id"), ("client_id", "client_id"),
+                         ("input_type", "input_type"), ("has_num_records", "has_num_records"),
+                         ("has_match_seq_num", "has_msn"), ("num_records", "num_records"),
+                         ("match_seq_num", "msn"), ("record_hashes", "hashes"), ("n_record_hashes", "n_hashes"),
+                         ("failure", "failure"), ("definite_failure", "definite"), ("has_tail", "has_tail"),
+                         ("has_stream_hash", "has_hash"), ("tail", "tail"), ("stream_hash", "stream_hash")):
+        arr[f_dst] = ev[f_src]
+    ptrs = np.concatenate([ev["set_fencing_token"], ev["fencing_token"]])
+    uniq, inv = np.unique(ptrs, return_inverse=True)
+    ids = inv.astype(np.int32) + (0 if uniq[0] == 0 else 1)  # pointer 0 (nil) -> id 0
+    arr["set_tok"] = ids[:n]
+    arr["batch_tok"] = ids[n:]
+    ea = EventArray.__new__(EventArray)
+    ea.arr = arr
+    ea.pool = None
+    return ea

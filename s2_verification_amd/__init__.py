@@ -20,6 +20,8 @@ from __future__ import annotations
 
 import ctypes
 import os
+
+import numpy as np
 from dataclasses import dataclass, field
 from typing import List, Optional, Sequence, Tuple
 
@@ -98,6 +100,19 @@ class c_sim_params(ctypes.Structure):
                 ("max_client_ids", ctypes.c_uint32)]
 
 
+def _np_field(t):
+    if t is ctypes.c_char_p or t is ctypes.POINTER(ctypes.c_uint64):
+        return np.dtype(np.uint64)  # pointers as integers
+    return np.dtype(t)
+
+
+# s2lc_event as a numpy structured dtype (bulk export without Python loops)
+EVENT_NP_DTYPE = np.dtype({"names": [f for f, _ in c_event._fields_],
+                           "formats": [_np_field(t) for _, t in c_event._fields_],
+                           "offsets": [getattr(c_event, f).offset for f, _ in c_event._fields_],
+                           "itemsize": ctypes.sizeof(c_event)})
+
+
 # Every symbol include/s2lincheck.h declares: (name, restype, argtypes)
 _P = ctypes.c_void_p
 SIGNATURES = [
@@ -112,6 +127,7 @@ SIGNATURES = [
     ("s2lc_history_free", None, [_P]),
     ("s2lc_history_event_count", ctypes.c_size_t, [_P]),
     ("s2lc_history_get_event", ctypes.c_int, [_P, ctypes.c_size_t, ctypes.POINTER(c_event)]),
+    ("s2lc_history_get_events", ctypes.c_int, [_P, _P, ctypes.c_size_t]),
     ("s2lc_history_info_get", ctypes.c_int, [_P, ctypes.POINTER(c_history_info)]),
     ("s2lc_check", ctypes.c_int, [_P, _P, ctypes.POINTER(c_result)]),
     ("s2lc_check_batch", ctypes.c_int, [_P, ctypes.POINTER(_P), ctypes.c_size_t, ctypes.POINTER(c_result)]),
@@ -298,6 +314,15 @@ class History:
                                  StreamHash=e.stream_hash if e.has_stream_hash else None)
             out.append(Event(e.kind, v, e.op_id, e.client_id))
         return out
+
+    def events_numpy(self):
+        """All events as a numpy structured array in the s2lc_event layout (zero Python loops)."""
+        n = len(self)
+        arr = np.zeros(n, dtype=EVENT_NP_DTYPE)
+        rc = lib().s2lc_history_get_events(self._h, arr.ctypes.data, n)
+        if rc:
+            raise S2LCError(rc, "get_events")
+        return arr
 
     def step(self, state: Tuple[int, int, int], op_index: int):
         """s2Model.Step for dense op `op_index` from (tail, hash, token_id)."""

@@ -227,6 +227,12 @@ int s2lc_history_get_event(const s2lc_history* h, size_t i, s2lc_event* out) {
   return 0;
 }
 
+int s2lc_history_get_events(const s2lc_history* h, s2lc_event* out, size_t n) {
+  if (!h || (!out && n) || n > h->h.events.size()) return S2LC_EINVAL;
+  for (size_t i = 0; i < n; ++i) s2lc_history_get_event(h, i, &out[i]);
+  return 0;
+}
+
 int s2lc_history_info_get(const s2lc_history* h, s2lc_history_info* out) {
   if (!h || !out) return S2LC_EINVAL;
   const History& H = h->h;

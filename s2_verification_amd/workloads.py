@@ -1,0 +1,43 @@
+"""The five BASELINE.json configurations as deterministic-simulator parameters.
+
+SURVEY.md §8(d): C1 regular 5x100 (seed 1), C2 match-seq-num 10x200 (seed 2),
+C3 fencing 16x500 (seed 3), C4 10k histories of 5-8 clients x 100 ops (seeds
+0..9999, clients = 5 + seed mod 4, workflow = seed mod 3, every 10th seed with
+an injected violation), C5 32x1000 (seed 5, raised indefinite-failure rate) and
+its non-linearizable variant.
+"""
+from . import (VIOL_DEFINITE_APPLIED, VIOL_NONE, VIOL_READ_HASH, VIOL_STALE_MSN, VIOL_TAIL, WF_FENCING,
+               WF_MATCH_SEQ_NUM, WF_REGULAR, simulate_history, simulate_jsonl)
+
+BASE = dict(p_indefinite=0.01, p_definite=0.02, p_read_failure=0.01, p_check_tail_failure=0.01)
+
+CONFIGS = {
+    "C1": dict(workflow=WF_REGULAR, num_clients=5, ops_per_client=100, seed=1, **BASE),
+    "C2": dict(workflow=WF_MATCH_SEQ_NUM, num_clients=10, ops_per_client=200, seed=2, **BASE),
+    "C3": dict(workflow=WF_FENCING, num_clients=16, ops_per_client=500, seed=3, **BASE),
+    "C5": dict(workflow=WF_REGULAR, num_clients=32, ops_per_client=1000, seed=5,
+               **{**BASE, "p_indefinite": 0.002}),
+    "C5bad": dict(workflow=WF_REGULAR, num_clients=32, ops_per_client=1000, seed=5, violation=VIOL_READ_HASH,
+                  **{**BASE, "p_indefinite": 0.002}),
+}
+
+_C4_VIOLS = [VIOL_READ_HASH, VIOL_TAIL, VIOL_DEFINITE_APPLIED, VIOL_STALE_MSN]
+
+
+def c4_params(seed: int) -> dict:
+    """One history of the C4 batch (DST seed `seed`)."""
+    wf = (WF_REGULAR, WF_MATCH_SEQ_NUM, WF_FENCING)[seed % 3]
+    viol = _C4_VIOLS[(seed // 10) % 4] if seed % 10 == 7 else VIOL_NONE
+    return dict(workflow=wf, num_clients=5 + seed % 4, ops_per_client=100, seed=seed, violation=viol, **BASE)
+
+
+def config_history(name: str):
+    return simulate_history(**CONFIGS[name])
+
+
+def config_jsonl(name: str) -> bytes:
+    return simulate_jsonl(**CONFIGS[name])
+
+
+def c4_histories(n: int = 10000, first_seed: int = 0):
+    return [simulate_history(**c4_params(s)) for s in range(first_seed, first_seed + n)]

@@ -1,0 +1,152 @@
+"""CPU: the product JSONL loader (eventsFromReader, main.go:529-563 semantics)."""
+import json
+import os
+
+import pytest
+
+import s2_verification_amd as s2
+from helpers import GOLDEN, golden, from_s2_events
+
+
+def load(text):
+    return s2.events_from_reader(text)
+
+
+def decode_fails(text):
+    with pytest.raises(s2.S2LCError) as ei:
+        load(text)
+    assert ei.value.status == -2
+    return str(ei.value)
+
+
+def test_rejects_malformed_json():
+    """TestEventsFromReaderRejectsMalformedJSON (main_test.go:103-108)."""
+    decode_fails('{"event":{"Start":"Read"},"client_id":1,"op_id":1')
+
+
+def test_read_success_stream_hash():
+    """TestEventsFromReaderDecodesReadSuccessStreamHash (main_test.go:110-126)."""
+    h = load('{"event":{"Finish":{"ReadSuccess":{"tail":7,"stream_hash":42}}},"client_id":1,"op_id":2}')
+    ev = h.events()
+    assert len(ev) == 1
+    assert ev[0].Value.StreamHash == 42 and ev[0].Value.Tail == 7
+
+
+def test_large_record_hash_line():
+    """TestEventsFromReaderHandlesLargeRecordHashLine (main_test.go:34-101): >64 KiB line, exact u64s."""
+    with open(os.path.join(GOLDEN, "ref_LargeRecordHashLine.jsonl"), "rb") as f:
+        data = f.read()
+    assert data.index(b"\n") > 64 * 1024
+    ev = load(data).events()
+    assert len(ev) == 2
+    assert ev[0].Value.RecordHashes == [2**64 - 1 - i for i in range(5000)]
+
+
+def test_golden_files_match_fixture_events():
+    for c in golden("reference_cases.json")["cases"]:
+        if not c.get("jsonl_file"):
+            continue
+        got = from_s2_events(s2.load_file(os.path.join(GOLDEN, c["jsonl_file"])).events())
+        want = c["events"]
+        assert len(got) == len(want)
+        for g, w in zip(got, want):
+            for k, v in w.items():
+                if k == "client_id":
+                    continue
+                assert g.get(k) == v, (c["name"], k, g, w)
+
+
+def test_num_records_mismatch():
+    decode_fails('{"event":{"Start":{"Append":{"num_records":2,"record_hashes":[1],'
+                 '"set_fencing_token":null,"fencing_token":null,"match_seq_num":null}}},"client_id":1,"op_id":1}')
+
+
+@pytest.mark.parametrize("text", [
+    '{"event":{"Start":"Write"},"client_id":1,"op_id":1}',                 # unknown string start
+    '{"event":{"Start":{"Foo":{}}},"client_id":1,"op_id":1}',              # unknown start object
+    '{"event":{"Start":5},"client_id":1,"op_id":1}',                       # number start
+    '{"event":{"Finish":"Boom"},"client_id":1,"op_id":1}',                 # unknown finish
+    '{"event":{"Finish":{"Nope":{}}},"client_id":1,"op_id":1}',            # unknown finish object
+    '{"event":{"Start":"Read","Finish":"ReadFailure"},"client_id":1,"op_id":1}',  # both
+    '{"event":{},"client_id":1,"op_id":1}',                                # neither
+    '{"event":null,"client_id":1,"op_id":1}',                              # null event
+    '{"client_id":1,"op_id":1}',                                           # no event
+    'null',                                                                # null record
+    '[1,2]',                                                               # array record
+    '{"event":{"Start":"Read"},"client_id":"1","op_id":1}',                # string id
+    '{"event":{"Start":"Read"},"client_id":1,"op_id":1.5}',                # fractional id
+    '{"event":{"Start":"Read"},"client_id":1,"op_id":1e3}',                # exponent id
+    '{"event":{"Start":{"Append":{"num_records":-1,"record_hashes":[]}}},"op_id":1}',  # negative u64
+    '{"event":{"Start":{"Append":{"num_records":18446744073709551616,"record_hashes":[]}}},"op_id":1}',
+    '{"event":{"Start":{"Append":{"num_records":0,"record_hashes":[],"set_fencing_token":5}}},"op_id":1}',
+    '{"event":{"Finish":{"AppendSuccess":{"tail":"4"}}},"op_id":1}',
+    '{"event":{"Start":"Read"},"op_id":01}',                               # leading zero
+    '{"event":{"Start":"Read"}} x',                                        # trailing garbage
+    '{"event":{"Start":"Read"},"event":{"Finish":"ReadFailure"},"op_id":1}',  # duplicate event key accumulates
+    '{"event":{"Start":"Re\\x"},"op_id":1}',                               # bad escape
+])
+def test_decode_errors(text):
+    decode_fails(text)
+
+
+def test_go_decoder_leniencies():
+    # case-insensitive struct keys, unknown keys ignored, null ids, any whitespace, no newlines needed
+    h = load('  {"EVENT":{"Start":"CheckTail"},"Client_Id":3,"OP_ID":9,"extra":[1,{"a":null}]}'
+             '{"event":{"Finish":{"CheckTailSuccess":{"TAIL":5,"junk":true}}},"client_id":null,"op_id":9}\n\n')
+    ev = h.events()
+    assert [e.Kind for e in ev] == [0, 1]
+    assert ev[0].Id == 9 and ev[0].ClientId == 3 and ev[0].Value.InputType == 2
+    assert ev[1].Value.Tail == 5 and ev[1].ClientId == 0
+    # Kelvin sign / long s fold like ASCII k / s in struct keys (Go encoding/json)
+    h = load('{"event":{"Start":{"Append":{"num_recordſ":1,"record_hashes":[7],'
+             '"fencing_toKen":"t"}}},"op_id":1}'.encode("utf-8"))
+    v = h.events()[0].Value
+    assert v.NumRecords == 1 and v.BatchFencingToken == "t"
+    # map keys ("Start", "Append", ...) are exact
+    decode_fails('{"event":{"start":"Read"},"op_id":1}')
+    # duplicate keys: last wins (maps and struct fields)
+    h = load('{"event":{"Start":"Read","Start":"CheckTail"},"op_id":1,"op_id":4}')
+    assert h.events()[0].Value.InputType == 2 and h.events()[0].Id == 4
+    # null Append payload = zero AppendArgs; null success payload = zero result
+    h = load('{"event":{"Start":{"Append":null}},"op_id":1}{"event":{"Finish":{"AppendSuccess":null}},"op_id":1}')
+    ev = h.events()
+    assert ev[0].Value.NumRecords == 0 and ev[1].Value.Tail == 0
+    # record_hashes null elements decode as 0; escapes decode
+    h = load('{"event":{"Start":{"Append":{"num_records":2,"record_hashes":[null,3],'
+             '"set_fencing_token":"\\u0041b"}}},"op_id":1}')
+    v = h.events()[0].Value
+    assert v.RecordHashes == [0, 3] and v.SetFencingToken == "Ab"
+    # empty input: no events
+    assert len(load("")) == 0
+    # string Start "Read" with unicode escape
+    assert load('{"event":{"Start":"Re\\u0061d"},"op_id":1}').events()[0].Value.InputType == 1
+
+
+def test_append_failure_mapping():
+    """outputFromFinish (main.go:466-523)."""
+    rows = {
+        '"AppendDefiniteFailure"': (True, True, None, None),
+        '"AppendIndefiniteFailure"': (True, False, None, None),
+        '"ReadFailure"': (True, True, None, None),
+        '"CheckTailFailure"': (True, True, None, None),
+        '{"AppendSuccess":{"tail":3}}': (False, False, 3, None),
+        '{"ReadSuccess":{"tail":3,"stream_hash":9}}': (False, False, 3, 9),
+        '{"CheckTailSuccess":{"tail":3}}': (False, False, 3, None),
+        '{"ReadSuccess":{}}': (False, False, 0, 0),
+    }
+    for fin, want in rows.items():
+        v = load('{"event":{"Finish":%s},"op_id":1}' % fin).events()[0].Value
+        assert (v.Failure, v.DefiniteFailure, v.Tail, v.StreamHash) == want, fin
+
+
+def test_simulator_jsonl_roundtrip():
+    """The simulator's JSONL and its direct history agree event for event."""
+    for wf in (0, 1, 2):
+        data = s2.simulate_jsonl(workflow=wf, num_clients=4, ops_per_client=50, seed=11, p_indefinite=0.05)
+        a = from_s2_events(load(data).events())
+        b = from_s2_events(s2.simulate_history(workflow=wf, num_clients=4, ops_per_client=50, seed=11,
+                                               p_indefinite=0.05).events())
+        assert a == b
+        # serde field order (history.rs:133-138)
+        first = json.loads(data.split(b"\n")[0])
+        assert list(first.keys()) == ["event", "client_id", "op_id"]

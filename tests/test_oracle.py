@@ -1,0 +1,75 @@
+"""CPU: the oracle (restatement of the reference) pinned against golden fixtures."""
+import random
+
+import oracle as orc
+from helpers import golden, random_history
+
+
+def test_chain_hash_reference_vectors():
+    """TestChainHashVectors (main_test.go:15-32) / chain_hash_vectors (history.rs:678-687)."""
+    g = golden("chain_hash_vectors.json")["reference"]
+    foo, bar, baz = g["xxh3"]
+    assert foo == 0xab6e5f64077e7d8a
+    h1 = orc.chain_hash(0, foo)
+    h2 = orc.chain_hash(h1, bar)
+    h3 = orc.chain_hash(h2, baz)
+    assert (h1, h2, h3) == (0x4d2b003ee417c3a5, 0x132e5d5dd7936edd, 0x732ee99abc5002ff)
+
+
+def test_chain_hash_xxhash_vectors():
+    g = golden("chain_hash_vectors.json")
+    for h, r, want in g["pairs"]:
+        assert orc.chain_hash(h, r) == want
+    for h, rs, want in g["folds"]:
+        assert orc.fold(h, rs) == want
+
+
+def test_reference_verdict_cases():
+    """The reference's 9 verdict tests + the large-line test, as fixtures."""
+    for c in golden("reference_cases.json")["cases"]:
+        v, _ = orc.check_wgl(c["events"])
+        assert v == c["expected"], c["name"]
+        b, _ = orc.check_brute(c["events"])
+        assert b == c["expected"], c["name"]
+
+
+def test_reference_jsonl_fixtures_decode_like_events():
+    import os
+    from helpers import GOLDEN
+    for c in golden("reference_cases.json")["cases"]:
+        if not c.get("jsonl_file"):
+            continue
+        with open(os.path.join(GOLDEN, c["jsonl_file"])) as f:
+            ev = orc.load_jsonl(f.read())
+        assert orc.check_wgl(ev)[0] == c["expected"]
+
+
+def test_wgl_matches_brute_force_on_random_histories():
+    rng = random.Random(12345)
+    seen = set()
+    for _ in range(1500):
+        ev = random_history(rng, rng.randint(0, 8), n_clients=rng.randint(1, 4))
+        w, _ = orc.check_wgl(ev)
+        b, _ = orc.check_brute(ev)
+        assert w == b, ev
+        seen.add(w)
+    assert seen == {"Ok", "Illegal"}
+
+
+def test_unmatched_events_are_illegal():
+    """A call without a return (or a return before its call) never leaves checkSingle's list."""
+    call = {"kind": "call", "op_id": 1, "input_type": 1}
+    ret = {"kind": "return", "op_id": 1, "failure": False, "definite_failure": False, "tail": 0,
+           "stream_hash": 0}
+    assert orc.check_wgl([call])[0] == "Illegal"
+    assert orc.check_wgl([ret])[0] == "Illegal"
+    assert orc.check_wgl([ret, call])[0] == "Illegal"
+    assert orc.check_wgl([call, ret])[0] == "Ok"
+    assert orc.check_wgl([])[0] == "Ok"
+
+
+def test_model_panics_are_reported():
+    """nil NumRecords on an append / nil Tail on a success: the Go model would panic."""
+    call = {"kind": "call", "op_id": 1, "input_type": 0, "num_records": None, "record_hashes": []}
+    ret = {"kind": "return", "op_id": 1, "failure": False, "definite_failure": False, "tail": 0}
+    assert orc.check_wgl([call, ret])[0] == "Panic"
