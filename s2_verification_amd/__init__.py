@@ -26,7 +26,7 @@ from dataclasses import dataclass, field
 from typing import List, Optional, Sequence, Tuple
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "libs2lincheck.so")
+LIB_PATH = os.environ.get("S2LC_LIB") or os.path.join(_HERE, "libs2lincheck.so")
 CLI_PATH = os.path.join(_HERE, "s2-porcupine")
 
 # ------------------------------------------------------------------ C ABI ---

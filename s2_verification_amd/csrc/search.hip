@@ -26,389 +26,11 @@
 
 #include "s2lincheck.h"
 #include "search.h"
+#include "search_dev.h"
 
 namespace s2lc {
 
 namespace {
-
-constexpr uint64_t HT_EMPTY = ~0ull;
-constexpr uint32_t STAGE_BIT = 0x80000000u;
-constexpr uint32_t SLOT_DEAD = 0xFFFFFFFFu;
-constexpr uint32_t TRACE_CHUNK = 4096;
-
-enum : int { CL_ALIVE = 0, CL_DEAD = 1, CL_COMPLETE = 2, CL_P4 = 3 };
-
-template <int KMAX>
-struct __attribute__((aligned(16))) Cfg {
-  uint64_t tail;
-  uint64_t hash;
-  uint32_t tok;
-  uint32_t minret;  // min return event over unlinearized ops (closure output)
-  uint32_t ptrace;  // trace index of the parent
-  uint32_t move;    // move that produced this configuration
-  uint32_t trace;   // own trace index (once in a frontier)
-  uint32_t slot;    // claimed table slot, SLOT_DEAD if dropped
-  uint64_t fp;      // fingerprint
-  uint16_t cnt[KMAX];
-};
-static_assert(sizeof(Cfg<16>) == 80, "cfg16");
-static_assert(sizeof(Cfg<32>) == 112, "cfg32");
-
-struct Params {
-  const OpRec* recs;
-  const uint64_t* pool;
-  const uint32_t* chain_start;
-  const HistDesc* hist;
-  const uint32_t* order;
-  uint32_t n_hist;
-  uint32_t* counter;
-  uint8_t* slab;
-  size_t slab_bytes;
-  uint32_t fcap, chunk, ht_mask;
-  TraceEnt* trace;
-  unsigned long long* trace_head;
-  uint64_t trace_cap;
-  HistResult* res;
-  uint64_t max_configs;
-  uint32_t witness;
-};
-
-__device__ __forceinline__ uint64_t mix64(uint64_t x) {
-  x ^= x >> 33;
-  x *= 0xff51afd7ed558ccdull;
-  x ^= x >> 33;
-  x *= 0xc4ceb9fe1a85ec53ull;
-  x ^= x >> 33;
-  return x;
-}
-
-__device__ __forceinline__ OpRec load_rec(const OpRec* p) {
-  // 64-byte record as four 16-byte loads
-  OpRec r;
-  const uint4* s = reinterpret_cast<const uint4*>(p);
-  uint4* d = reinterpret_cast<uint4*>(&r);
-  d[0] = s[0]; d[1] = s[1]; d[2] = s[2]; d[3] = s[3];
-  return r;
-}
-
-// Closure under minimal, legal identity ops + the P1/P2/P4 rules.
-template <int KMAX>
-__device__ int closure(Cfg<KMAX>* c, int K, const uint32_t* cs, const OpRec* __restrict__ recs, uint32_t hflags) {
-  const State s{c->tail, c->hash, c->tok};
-  const bool nowrap = hflags & H_NOWRAP;
-  const bool p2 = hflags & H_P2OK;
-  for (;;) {
-    uint32_t minret = EV_INF;
-    uint64_t bound = REQ_NONE;
-    for (int q = 0; q < K; ++q) {
-      const OpRec* r = &recs[cs[q] + c->cnt[q]];
-      minret = min(minret, r->ret_ev);
-      bound = min(bound, r->sufmin);
-    }
-    if (minret == EV_INF) return CL_COMPLETE;
-    if (nowrap && s.tail > bound) return CL_DEAD;  // P1: a pending observer needs a smaller tail
-    if (bound == REQ_NONE) return CL_P4;          // P4: nothing left constrains the state
-    bool changed = false;
-    for (int q = 0; q < K; ++q) {
-      uint32_t cq = c->cnt[q];
-      const uint32_t c0 = cq;
-      for (;;) {
-        const OpRec r = load_rec(&recs[cs[q] + cq]);
-        if (!(r.flags & OPF_CLS_E) || r.call_ev >= minret) break;
-        if (!ident_legal(r, s)) {
-          // P2: a minimal successful read at this tail with another hash can never pass
-          if (p2 && (r.flags & OPF_KIND_MASK) != 0 && !(r.flags & OPF_FAIL) && (r.flags & OPF_HAS_HASH) &&
-              r.out_tail == s.tail)
-            return CL_DEAD;
-          break;
-        }
-        ++cq;
-      }
-      if (cq != c0) { c->cnt[q] = (uint16_t)cq; changed = true; }
-    }
-    if (!changed) { c->minret = minret; return CL_ALIVE; }
-  }
-}
-
-template <int KMAX>
-__device__ __forceinline__ uint64_t fingerprint(const Cfg<KMAX>* c, int nw) {
-  uint64_t h = mix64(c->tail ^ 0x9E3779B97F4A7C15ull) ^ mix64(c->hash + 0x632BE59BD9B4E019ull * (c->tok + 1));
-  const uint4* w = reinterpret_cast<const uint4*>(c->cnt);
-  for (int q = 0; q < nw; ++q) {
-    const uint4 v = w[q];
-    h = mix64(h ^ ((uint64_t)v.x | ((uint64_t)v.y << 32)));
-    h = mix64(h + ((uint64_t)v.z | ((uint64_t)v.w << 32)));
-  }
-  return h;
-}
-
-template <int KMAX>
-__device__ __forceinline__ bool cfg_eq(const Cfg<KMAX>* a, const Cfg<KMAX>* b, int nw) {
-  if (a->tail != b->tail || a->hash != b->hash || a->tok != b->tok) return false;
-  const uint4* x = reinterpret_cast<const uint4*>(a->cnt);
-  const uint4* y = reinterpret_cast<const uint4*>(b->cnt);
-  for (int q = 0; q < nw; ++q) {
-    const uint4 u = x[q], v = y[q];
-    if (u.x != v.x || u.y != v.y || u.z != v.z || u.w != v.w) return false;
-  }
-  return true;
-}
-
-template <int KMAX>
-__device__ __forceinline__ void cfg_copy(Cfg<KMAX>* d, const Cfg<KMAX>* s) {
-  const uint4* x = reinterpret_cast<const uint4*>(s);
-  uint4* y = reinterpret_cast<uint4*>(d);
-#pragma unroll
-  for (int q = 0; q < (int)(sizeof(Cfg<KMAX>) / 16); ++q) y[q] = x[q];
-}
-
-template <int KMAX, int BT>
-__global__ __launch_bounds__(BT) void search_kernel(Params p) {
-  using C = Cfg<KMAX>;
-  __shared__ uint32_t s_cs[KMAX + 1];
-  __shared__ uint32_t s_h, s_nstage, s_nnext, s_found, s_overflow, s_children;
-  __shared__ uint32_t s_found_parent, s_found_move, s_found_p4;
-  __shared__ uint32_t s_tb, s_tleft, s_witness_ok;
-  __shared__ unsigned long long s_tbase;
-  __shared__ HistDesc s_hd;
-
-  const int tid = threadIdx.x;
-  uint8_t* slab = p.slab + (size_t)blockIdx.x * p.slab_bytes;
-  C* const fa = reinterpret_cast<C*>(slab);
-  C* const fb = fa + p.fcap;
-  C* const stage = fb + p.fcap;
-  unsigned long long* const ht = reinterpret_cast<unsigned long long*>(stage + 2 * p.chunk);
-  const uint32_t mask = p.ht_mask;
-
-  for (uint32_t i = tid; i <= mask; i += BT) ht[i] = HT_EMPTY;
-  if (tid == 0) { s_tleft = 0; s_tbase = 0; }
-  __syncthreads();
-
-  for (;;) {
-    if (tid == 0) s_h = atomicAdd(p.counter, 1u);
-    __syncthreads();
-    const uint32_t hi = s_h;
-    if (hi >= p.n_hist) break;
-    const uint32_t h = p.order[hi];
-    if (tid == 0) s_hd = p.hist[h];
-    __syncthreads();
-    const HistDesc hd = s_hd;
-    const int K = hd.K;
-    const int nw = (K + 7) >> 3;
-    const OpRec* __restrict__ recs = p.recs;
-    for (int j = tid; j <= K; j += BT) s_cs[j] = p.chain_start[hd.cs_base + j];
-    if (tid == 0) {
-      s_found = 0; s_overflow = 0; s_children = 0;
-      s_witness_ok = p.witness;
-      s_found_parent = TRACE_NONE; s_found_move = TRACE_NONE; s_found_p4 = 0;
-    }
-    __syncthreads();
-
-    // ---- initial configuration: (∅, (0, 0, nil)) closed ------------------
-    if (tid == 0) {
-      C* c = &fa[0];
-      for (int q = 0; q < KMAX; ++q) c->cnt[q] = 0;
-      c->tail = 0; c->hash = 0; c->tok = 0;
-      c->ptrace = TRACE_NONE; c->move = TRACE_NONE; c->slot = 0;
-      const int r = closure<KMAX>(c, K, s_cs, recs, hd.flags);
-      if (r == CL_DEAD) s_nnext = 0;
-      else s_nnext = 1;
-      if (r >= CL_COMPLETE) { s_found = 1; s_found_p4 = (r == CL_P4); }
-      uint32_t t = TRACE_NONE;
-      if (s_witness_ok) {
-        if (s_tleft == 0) {
-          const unsigned long long b = atomicAdd(p.trace_head, (unsigned long long)TRACE_CHUNK);
-          if (b + TRACE_CHUNK <= p.trace_cap) { s_tbase = b; s_tleft = TRACE_CHUNK; }
-          else s_witness_ok = 0;
-        }
-        if (s_witness_ok) {
-          t = (uint32_t)s_tbase; s_tbase += 1; s_tleft -= 1;
-          p.trace[t].parent = TRACE_NONE; p.trace[t].move = TRACE_NONE;
-        }
-      }
-      c->trace = t;
-    }
-    __syncthreads();
-
-    C* cur = fa;
-    C* nxt = fb;
-    uint32_t ncur = s_nnext;
-    uint64_t configs = ncur;
-    uint32_t rounds = 0;
-    uint32_t verdict = V_ILLEGAL, reason = S2LC_R_SEARCH_EXHAUSTED;
-    if (s_found) verdict = V_OK, reason = 0;
-
-    while (!s_found) {
-      if (ncur == 0) { verdict = V_ILLEGAL; reason = S2LC_R_SEARCH_EXHAUSTED; break; }
-      if (tid == 0) s_nnext = 0;
-      const uint32_t total = ncur * (uint32_t)K;
-      for (uint32_t base = 0; base < total; base += p.chunk) {
-        if (tid == 0) s_nstage = 0;
-        __syncthreads();
-        // ---- expand: one lane per (configuration, chain) -----------------
-        const uint32_t lim = min(total, base + p.chunk);
-        for (uint32_t it = base + tid; it < lim; it += BT) {
-          const uint32_t i = it / (uint32_t)K;
-          const uint32_t j = it - i * (uint32_t)K;
-          const C* pc = &cur[i];
-          const OpRec r = load_rec(&recs[s_cs[j] + pc->cnt[j]]);
-          if ((r.flags & (OPF_SENTINEL | OPF_CLS_E)) || r.call_ev >= pc->minret) continue;
-          const State s{pc->tail, pc->hash, pc->tok};
-          const bool g = append_guards_ok(r, s);
-          State kids[2];
-          uint32_t moves[2];
-          int nk = 0;
-          State opt{0, 0, 0};
-          if (g) opt = append_opt(r, s, p.pool);
-          if (r.flags & OPF_CLS_D) {
-            if (g && opt.tail == r.out_tail) { kids[nk] = opt; moves[nk++] = j; }
-          } else {  // indefinite: opt any time; identity only when it holds the minimal return
-            if (g) { kids[nk] = opt; moves[nk++] = j; }
-            if (r.ret_ev == pc->minret && !(g && state_eq(opt, s))) { kids[nk] = s; moves[nk++] = j | MOVE_IDENT; }
-          }
-          for (int q = 0; q < nk; ++q) {
-            const uint32_t k = atomicAdd(&s_nstage, 1u);
-            C* ch = &stage[k];
-            const uint4* src = reinterpret_cast<const uint4*>(pc->cnt);
-            uint4* dst = reinterpret_cast<uint4*>(ch->cnt);
-#pragma unroll
-            for (int w = 0; w < KMAX / 8; ++w) dst[w] = src[w];
-            ch->cnt[j] = (uint16_t)(ch->cnt[j] + 1);
-            ch->tail = kids[q].tail; ch->hash = kids[q].hash; ch->tok = kids[q].tok;
-            ch->ptrace = pc->trace;
-            ch->move = moves[q];
-            const int cr = closure<KMAX>(ch, K, s_cs, recs, hd.flags);
-            if (cr == CL_ALIVE) {
-              ch->fp = fingerprint<KMAX>(ch, nw);
-              ch->slot = 0;
-            } else {
-              ch->slot = SLOT_DEAD;
-              if (cr >= CL_COMPLETE && atomicCAS(&s_found, 0u, 1u) == 0u) {
-                s_found_parent = pc->trace; s_found_move = moves[q]; s_found_p4 = (cr == CL_P4);
-              }
-            }
-          }
-          if (nk) atomicAdd(&s_children, (uint32_t)nk);
-        }
-        __syncthreads();
-        const uint32_t ns = s_nstage;
-        // ---- dedupe: 64-bit CAS open addressing, full-key compare on tag hit
-        for (uint32_t k = tid; k < ns; k += BT) {
-          C* ch = &stage[k];
-          if (ch->slot == SLOT_DEAD) continue;
-          const uint64_t fp = ch->fp;
-          const uint32_t tag = (uint32_t)(fp >> 32);
-          const unsigned long long mine = ((unsigned long long)tag << 32) | (k | STAGE_BIT);
-          uint32_t slot = (uint32_t)fp & mask;
-          for (;;) {
-            const unsigned long long prev = atomicCAS(&ht[slot], HT_EMPTY, mine);
-            if (prev == HT_EMPTY) { ch->slot = slot; break; }
-            if ((uint32_t)(prev >> 32) == tag) {
-              const uint32_t ref = (uint32_t)prev;
-              const C* o = (ref & STAGE_BIT) ? &stage[ref & ~STAGE_BIT] : &nxt[ref];
-              if (cfg_eq<KMAX>(o, ch, nw)) { ch->slot = SLOT_DEAD; break; }
-            }
-            slot = (slot + 1) & mask;
-          }
-        }
-        __syncthreads();
-        // ---- compact survivors into the next frontier ---------------------
-        for (uint32_t k = tid; k < ns; k += BT) {
-          C* ch = &stage[k];
-          if (ch->slot == SLOT_DEAD) continue;
-          const uint32_t n = atomicAdd(&s_nnext, 1u);
-          if (n < p.fcap) {
-            cfg_copy<KMAX>(&nxt[n], ch);
-            ht[ch->slot] = ((unsigned long long)(uint32_t)(ch->fp >> 32) << 32) | n;
-          } else {
-            s_overflow = 1;
-          }
-        }
-        __syncthreads();
-        if (s_found || s_overflow) break;
-      }
-      if (s_overflow) {
-        for (uint32_t i = tid; i <= mask; i += BT) ht[i] = HT_EMPTY;
-        if (s_found) { verdict = V_OK; reason = 0; ++rounds; }
-        else { verdict = V_UNKNOWN; reason = S2LC_R_FRONTIER; }
-        __syncthreads();
-        break;
-      }
-      const uint32_t nn = min(s_nnext, p.fcap);
-      if (tid == 0) {
-        s_tb = TRACE_NONE;
-        if (s_witness_ok) {
-          if (s_tleft < nn) {
-            const unsigned long long want = max((unsigned long long)nn, (unsigned long long)TRACE_CHUNK);
-            const unsigned long long b = atomicAdd(p.trace_head, want);
-            if (b + want <= p.trace_cap) { s_tbase = b; s_tleft = (uint32_t)want; }
-            else s_witness_ok = 0;
-          }
-          if (s_witness_ok) { s_tb = (uint32_t)s_tbase; s_tbase += nn; s_tleft -= nn; }
-        }
-      }
-      __syncthreads();
-      const uint32_t tb = s_tb;
-      for (uint32_t n = tid; n < nn; n += BT) {
-        C* c = &nxt[n];
-        ht[c->slot] = HT_EMPTY;
-        if (tb != TRACE_NONE) {
-          c->trace = tb + n;
-          p.trace[tb + n].parent = c->ptrace;
-          p.trace[tb + n].move = c->move;
-        } else {
-          c->trace = TRACE_NONE;
-        }
-      }
-      __syncthreads();
-      configs += nn;
-      ++rounds;
-      if (s_found) { verdict = V_OK; reason = 0; break; }
-      if (p.max_configs && configs > p.max_configs) { verdict = V_UNKNOWN; reason = S2LC_R_BUDGET; break; }
-      C* t = cur; cur = nxt; nxt = t;
-      ncur = nn;
-    }
-    if (tid == 0) {
-      HistResult& R = p.res[h];
-      R.verdict = verdict;
-      R.reason = reason;
-      R.rounds = rounds;
-      R.configs = configs;
-      R.children = s_children;
-      R.p4 = s_found_p4;
-      R.final_parent = (verdict == V_OK && s_witness_ok) ? s_found_parent : TRACE_NONE;
-      R.final_move = s_found_move;
-      R.witness_len = 0;
-      R.has_witness = (verdict == V_OK && s_witness_ok) ? 2u : 0u;  // resolved by walk_kernel
-    }
-    __syncthreads();
-  }
-}
-
-// Witness extraction: one lane per history walks the parent chain backwards
-// and writes the move list in order.
-__global__ void walk_kernel(uint32_t n, HistResult* res, const TraceEnt* trace, uint32_t* moves) {
-  const uint32_t h = blockIdx.x * blockDim.x + threadIdx.x;
-  if (h >= n) return;
-  HistResult r = res[h];
-  if (r.verdict != V_OK || r.has_witness != 2u) return;
-  const uint32_t len = (r.final_move == TRACE_NONE) ? 0u : r.rounds;
-  uint32_t* out = moves + r.witness_off;
-  bool ok = true;
-  if (len) {
-    out[len - 1] = r.final_move;
-    uint32_t idx = r.final_parent;
-    uint32_t pos = len - 1;
-    while (pos > 0 && idx != TRACE_NONE) {
-      const TraceEnt e = trace[idx];
-      out[--pos] = e.move;
-      idx = e.parent;
-    }
-    ok = (pos == 0);
-  }
-  res[h].witness_len = ok ? len : 0u;
-  res[h].has_witness = ok ? 1u : 0u;
-}
 
 #define HIPCHK(x)                                                        \
   do {                                                                   \

@@ -1,0 +1,505 @@
+// search_dev.h — device side of the frontier search (included by search.hip).
+// See search.hip for the algorithm overview.
+#pragma once
+#include "s2lincheck.h"
+#include "search.h"
+
+namespace s2lc {
+namespace {
+
+constexpr uint64_t HT_EMPTY = ~0ull;
+constexpr uint32_t STAGE_BIT = 0x80000000u;
+constexpr uint32_t SLOT_DEAD = 0xFFFFFFFFu;
+constexpr uint32_t TRACE_CHUNK = 4096;
+
+enum : int { CL_ALIVE = 0, CL_DEAD = 1, CL_COMPLETE = 2, CL_P4 = 3 };
+
+#ifdef S2LC_DEBUG
+#define DCHECK(cond, ...)                                                    \
+  do {                                                                       \
+    if (!(cond)) {                                                           \
+      printf("S2LC DCHECK %s:%d: " #cond " | ", __FILE__, __LINE__);         \
+      printf(__VA_ARGS__);                                                   \
+      printf("\n");                                                          \
+    }                                                                        \
+  } while (0)
+#else
+#define DCHECK(cond, ...) do { } while (0)
+#endif
+
+template <int KMAX>
+struct __attribute__((aligned(16))) Cfg {
+  uint64_t tail;
+  uint64_t hash;
+  uint32_t tok;
+  uint32_t minret;  // min return event over unlinearized ops (closure output)
+  uint32_t ptrace;  // trace index of the parent
+  uint32_t move;    // move that produced this configuration
+  uint32_t trace;   // own trace index (once in a frontier)
+  uint32_t slot;    // claimed table slot, SLOT_DEAD if dropped
+  uint64_t fp;      // fingerprint
+  uint16_t cnt[KMAX];
+};
+static_assert(sizeof(Cfg<16>) == 80, "cfg16");
+static_assert(sizeof(Cfg<32>) == 112, "cfg32");
+
+struct Params {
+  const OpRec* recs;
+  const uint64_t* pool;
+  const uint32_t* chain_start;
+  const HistDesc* hist;
+  const uint32_t* order;
+  uint32_t n_hist;
+  uint32_t* counter;
+  uint8_t* slab;
+  size_t slab_bytes;
+  uint32_t fcap, chunk, ht_mask;
+  TraceEnt* trace;
+  unsigned long long* trace_head;
+  uint64_t trace_cap;
+  HistResult* res;
+  uint64_t max_configs;
+  uint32_t witness;
+};
+
+__device__ __forceinline__ uint64_t mix64(uint64_t x) {
+  x ^= x >> 33;
+  x *= 0xff51afd7ed558ccdull;
+  x ^= x >> 33;
+  x *= 0xc4ceb9fe1a85ec53ull;
+  x ^= x >> 33;
+  return x;
+}
+
+__device__ __forceinline__ OpRec load_rec(const OpRec* p) {
+  // 64-byte record as four 16-byte loads
+  OpRec r;
+  const uint4* s = reinterpret_cast<const uint4*>(p);
+  uint4* d = reinterpret_cast<uint4*>(&r);
+  d[0] = s[0]; d[1] = s[1]; d[2] = s[2]; d[3] = s[3];
+  return r;
+}
+
+// Closure under minimal, legal identity ops + the P1/P2/P4 rules.
+//
+// Latency-oriented: each pass fetches every chain head with independent loads
+// (blocks of 8 chains in flight) and, in the same pass, takes each head that is
+// an identity op, minimal under the previous pass's minret and legal at s.
+// Using the previous pass's minret is sound: minret only grows as ops are
+// linearized, so an op minimal under an older (smaller) minret is minimal now.
+// A pass that changes nothing has loaded exactly the final heads, so its
+// minret / bound are exact; it ends the closure once its eligibility test also
+// used that exact minret. Seeded with the parent's minret (a lower bound).
+//   OpRec bytes 16..31 = out_tail, out_hash; 32..47 = sufmin, call_ev, ret_ev;
+//   60..63 = flags.
+__device__ __forceinline__ uint4 ld16(const OpRec* r, int off) {
+  return *reinterpret_cast<const uint4*>(reinterpret_cast<const uint8_t*>(r) + off);
+}
+
+// One pass over a block of B chains: load every head (out_tail/out_hash,
+// sufmin/call/ret, flags) with independent loads, fold minret / bound, and
+// mark the heads that are identity ops, minimal under minret_prev and legal.
+template <int B>
+__device__ __forceinline__ uint32_t closure_block(const uint32_t* cb, int nq, int b, const uint32_t* cs,
+                                                  const OpRec* __restrict__ recs, const State& s,
+                                                  uint32_t minret_prev, bool p2, uint32_t& minret, uint64_t& bound,
+                                                  bool& dead) {
+  uint4 obs[B], mid[B];
+  uint32_t fl[B];
+#pragma unroll
+  for (int q = 0; q < B; ++q)
+    if (q < nq) {
+      DCHECK(cs[b + q] + cb[q] < cs[b + q + 1], "closure chain %d cnt %u start %u end %u", b + q, cb[q], cs[b + q], cs[b + q + 1]);
+      const OpRec* r = &recs[cs[b + q] + cb[q]];
+      obs[q] = ld16(r, 16);
+      mid[q] = ld16(r, 32);
+      fl[q] = r->flags;
+    }
+  uint32_t adv = 0;
+#pragma unroll
+  for (int q = 0; q < B; ++q) {
+    if (q >= nq) continue;
+    minret = min(minret, mid[q].w);
+    bound = min(bound, (uint64_t)mid[q].x | ((uint64_t)mid[q].y << 32));
+    const uint32_t f = fl[q];
+    if (!(f & OPF_CLS_E) || mid[q].z >= minret_prev) continue;
+    const uint64_t ot = (uint64_t)obs[q].x | ((uint64_t)obs[q].y << 32);
+    const uint64_t oh = (uint64_t)obs[q].z | ((uint64_t)obs[q].w << 32);
+    bool legal = true;
+    if ((f & OPF_KIND_MASK) != 0) {
+      if ((f & OPF_HAS_HASH) && s.hash != oh) legal = false;
+      if (!(f & OPF_FAIL) && s.tail != ot) legal = false;
+    }
+    if (legal) adv |= 1u << q;
+    // P2: a minimal successful read at this tail with another hash can never pass
+    else if (p2 && (f & OPF_KIND_MASK) != 0 && !(f & OPF_FAIL) && (f & OPF_HAS_HASH) && ot == s.tail)
+      dead = true;
+  }
+  return adv;
+}
+
+template <int KMAX>
+__device__ __forceinline__ int closure(Cfg<KMAX>* c, int K, const uint32_t* cs, const OpRec* __restrict__ recs, uint32_t hflags,
+                       uint32_t minret_seed) {
+  constexpr int B = 8;
+  constexpr bool REG = KMAX <= 32;  // counts held in registers (packed u16 pairs)
+  constexpr int NP = REG ? KMAX / 2 : 1;
+  const State s{c->tail, c->hash, c->tok};
+  const bool nowrap = hflags & H_NOWRAP;
+  const bool p2 = hflags & H_P2OK;
+  uint32_t pk[NP];
+  if constexpr (REG) {
+    const uint4* w = reinterpret_cast<const uint4*>(c->cnt);
+#pragma unroll
+    for (int q = 0; q < KMAX / 8; ++q) {
+      const uint4 v = w[q];
+      pk[4 * q] = v.x; pk[4 * q + 1] = v.y; pk[4 * q + 2] = v.z; pk[4 * q + 3] = v.w;
+    }
+  }
+  uint32_t minret_prev = minret_seed;
+  uint32_t minret = EV_INF;
+  uint64_t bound = REQ_NONE;
+  int result = CL_ALIVE;
+  for (;;) {
+    minret = EV_INF;
+    bound = REQ_NONE;
+    bool changed = false, dead = false;
+    if constexpr (REG) {
+#pragma unroll
+      for (int b = 0; b < KMAX; b += B) {
+        if (b >= K) break;
+        uint32_t cb[B];
+#pragma unroll
+        for (int q = 0; q < B; ++q) cb[q] = ((b + q) & 1) ? (pk[(b + q) >> 1] >> 16) : (pk[(b + q) >> 1] & 0xFFFFu);
+        const uint32_t adv = closure_block<B>(cb, min(B, K - b), b, cs, recs, s, minret_prev, p2, minret, bound, dead);
+        if (adv) {
+          changed = true;
+#pragma unroll
+          for (int q = 0; q < B; ++q)
+            if (adv & (1u << q)) pk[(b + q) >> 1] += ((b + q) & 1) ? 0x10000u : 1u;
+        }
+      }
+    } else {
+      for (int b = 0; b < K; b += B) {
+        const uint4 v = *reinterpret_cast<const uint4*>(&c->cnt[b]);
+        uint32_t cb[B] = {v.x & 0xFFFFu, v.x >> 16, v.y & 0xFFFFu, v.y >> 16,
+                          v.z & 0xFFFFu, v.z >> 16, v.w & 0xFFFFu, v.w >> 16};
+        const uint32_t adv = closure_block<B>(cb, min(B, K - b), b, cs, recs, s, minret_prev, p2, minret, bound, dead);
+        if (adv) {
+          changed = true;
+          uint4 o;
+          o.x = (cb[0] + ((adv >> 0) & 1)) | ((cb[1] + ((adv >> 1) & 1)) << 16);
+          o.y = (cb[2] + ((adv >> 2) & 1)) | ((cb[3] + ((adv >> 3) & 1)) << 16);
+          o.z = (cb[4] + ((adv >> 4) & 1)) | ((cb[5] + ((adv >> 5) & 1)) << 16);
+          o.w = (cb[6] + ((adv >> 6) & 1)) | ((cb[7] + ((adv >> 7) & 1)) << 16);
+          *reinterpret_cast<uint4*>(&c->cnt[b]) = o;
+        }
+      }
+    }
+    if (dead) { result = CL_DEAD; break; }
+    if (nowrap && s.tail > bound) { result = CL_DEAD; break; }  // P1: a pending observer needs a smaller tail
+    // Final only if nothing changed AND eligibility was judged with the exact minret.
+    if (!changed && minret == minret_prev) {
+      if (minret == EV_INF) result = CL_COMPLETE;
+      else if (bound == REQ_NONE) result = CL_P4;           // P4: nothing left constrains the state
+      break;
+    }
+    minret_prev = minret;
+  }
+  if constexpr (REG) {
+    uint4* w = reinterpret_cast<uint4*>(c->cnt);
+#pragma unroll
+    for (int q = 0; q < KMAX / 8; ++q) w[q] = make_uint4(pk[4 * q], pk[4 * q + 1], pk[4 * q + 2], pk[4 * q + 3]);
+  }
+  c->minret = minret;
+  return result;
+}
+
+template <int KMAX>
+__device__ __forceinline__ uint64_t fingerprint(const Cfg<KMAX>* c, int nw) {
+  uint64_t h = mix64(c->tail ^ 0x9E3779B97F4A7C15ull) ^ mix64(c->hash + 0x632BE59BD9B4E019ull * (c->tok + 1));
+  const uint4* w = reinterpret_cast<const uint4*>(c->cnt);
+  for (int q = 0; q < nw; ++q) {
+    const uint4 v = w[q];
+    h = mix64(h ^ ((uint64_t)v.x | ((uint64_t)v.y << 32)));
+    h = mix64(h + ((uint64_t)v.z | ((uint64_t)v.w << 32)));
+  }
+  return h;
+}
+
+template <int KMAX>
+__device__ __forceinline__ bool cfg_eq(const Cfg<KMAX>* a, const Cfg<KMAX>* b, int nw) {
+  if (a->tail != b->tail || a->hash != b->hash || a->tok != b->tok) return false;
+  const uint4* x = reinterpret_cast<const uint4*>(a->cnt);
+  const uint4* y = reinterpret_cast<const uint4*>(b->cnt);
+  for (int q = 0; q < nw; ++q) {
+    const uint4 u = x[q], v = y[q];
+    if (u.x != v.x || u.y != v.y || u.z != v.z || u.w != v.w) return false;
+  }
+  return true;
+}
+
+template <int KMAX>
+__device__ __forceinline__ void cfg_copy(Cfg<KMAX>* d, const Cfg<KMAX>* s) {
+  const uint4* x = reinterpret_cast<const uint4*>(s);
+  uint4* y = reinterpret_cast<uint4*>(d);
+#pragma unroll
+  for (int q = 0; q < (int)(sizeof(Cfg<KMAX>) / 16); ++q) y[q] = x[q];
+}
+
+template <int KMAX, int BT>
+__global__ __launch_bounds__(BT) void search_kernel(Params p) {
+  using C = Cfg<KMAX>;
+  __shared__ uint32_t s_cs[KMAX + 1];
+  __shared__ uint32_t s_h, s_nstage, s_nnext, s_found, s_overflow, s_children;
+  __shared__ uint32_t s_found_parent, s_found_move, s_found_p4;
+  __shared__ uint32_t s_tb, s_tleft, s_witness_ok;
+  __shared__ unsigned long long s_tbase;
+  __shared__ HistDesc s_hd;
+
+  const int tid = threadIdx.x;
+  uint8_t* slab = p.slab + (size_t)blockIdx.x * p.slab_bytes;
+  C* const fa = reinterpret_cast<C*>(slab);
+  C* const fb = fa + p.fcap;
+  C* const stage = fb + p.fcap;
+  unsigned long long* const ht = reinterpret_cast<unsigned long long*>(stage + 2 * p.chunk);
+  const uint32_t mask = p.ht_mask;
+
+  for (uint32_t i = tid; i <= mask; i += BT) ht[i] = HT_EMPTY;
+  if (tid == 0) { s_tleft = 0; s_tbase = 0; }
+  __syncthreads();
+
+  for (;;) {
+    if (tid == 0) s_h = atomicAdd(p.counter, 1u);
+    __syncthreads();
+    const uint32_t hi = s_h;
+    if (hi >= p.n_hist) break;
+    const uint32_t h = p.order[hi];
+    if (tid == 0) s_hd = p.hist[h];
+    __syncthreads();
+    const HistDesc hd = s_hd;
+    const int K = hd.K;
+    const int nw = (K + 7) >> 3;
+    const OpRec* __restrict__ recs = p.recs;
+    for (int j = tid; j <= K; j += BT) s_cs[j] = p.chain_start[hd.cs_base + j];
+    if (tid == 0) {
+      s_found = 0; s_overflow = 0; s_children = 0;
+      s_witness_ok = p.witness;
+      s_found_parent = TRACE_NONE; s_found_move = TRACE_NONE; s_found_p4 = 0;
+    }
+    __syncthreads();
+
+    // ---- initial configuration: (∅, (0, 0, nil)) closed ------------------
+    if (tid == 0) {
+      C* c = &fa[0];
+      for (int q = 0; q < KMAX; ++q) c->cnt[q] = 0;
+      c->tail = 0; c->hash = 0; c->tok = 0;
+      c->ptrace = TRACE_NONE; c->move = TRACE_NONE; c->slot = 0;
+      const int r = closure<KMAX>(c, K, s_cs, recs, hd.flags, 0u);
+      if (r == CL_DEAD) s_nnext = 0;
+      else s_nnext = 1;
+      if (r >= CL_COMPLETE) { s_found = 1; s_found_p4 = (r == CL_P4); }
+      uint32_t t = TRACE_NONE;
+      if (s_witness_ok) {
+        if (s_tleft == 0) {
+          const unsigned long long b = atomicAdd(p.trace_head, (unsigned long long)TRACE_CHUNK);
+          if (b + TRACE_CHUNK <= p.trace_cap) { s_tbase = b; s_tleft = TRACE_CHUNK; }
+          else s_witness_ok = 0;
+        }
+        if (s_witness_ok) {
+          t = (uint32_t)s_tbase; s_tbase += 1; s_tleft -= 1;
+          p.trace[t].parent = TRACE_NONE; p.trace[t].move = TRACE_NONE;
+        }
+      }
+      c->trace = t;
+    }
+    __syncthreads();
+
+    C* cur = fa;
+    C* nxt = fb;
+    uint32_t ncur = s_nnext;
+    uint64_t configs = ncur;
+    uint32_t rounds = 0;
+    uint32_t verdict = V_ILLEGAL, reason = S2LC_R_SEARCH_EXHAUSTED;
+    if (s_found) verdict = V_OK, reason = 0;
+
+    while (!s_found) {
+      if (ncur == 0) { verdict = V_ILLEGAL; reason = S2LC_R_SEARCH_EXHAUSTED; break; }
+      if (tid == 0) s_nnext = 0;
+      const uint32_t total = ncur * (uint32_t)K;
+      for (uint32_t base = 0; base < total; base += p.chunk) {
+        if (tid == 0) s_nstage = 0;
+        __syncthreads();
+        // ---- expand: one lane per (configuration, chain) -----------------
+        const uint32_t lim = min(total, base + p.chunk);
+        for (uint32_t it = base + tid; it < lim; it += BT) {
+          const uint32_t i = it / (uint32_t)K;
+          const uint32_t j = it - i * (uint32_t)K;
+          const C* pc = &cur[i];
+          DCHECK(i < ncur && s_cs[j] + pc->cnt[j] < s_cs[j + 1], "expand i %u ncur %u j %u cnt %u", i, ncur, j, (uint32_t)pc->cnt[j]);
+          const OpRec r = load_rec(&recs[s_cs[j] + pc->cnt[j]]);
+          if ((r.flags & (OPF_SENTINEL | OPF_CLS_E)) || r.call_ev >= pc->minret) continue;
+          const State s{pc->tail, pc->hash, pc->tok};
+          const bool g = append_guards_ok(r, s);
+          State kids[2];
+          uint32_t moves[2];
+          int nk = 0;
+          State opt{0, 0, 0};
+          if (g) opt = append_opt(r, s, p.pool);
+          if (r.flags & OPF_CLS_D) {
+            if (g && opt.tail == r.out_tail) { kids[nk] = opt; moves[nk++] = j; }
+          } else {  // indefinite: opt any time; identity only when it holds the minimal return
+            if (g) { kids[nk] = opt; moves[nk++] = j; }
+            if (r.ret_ev == pc->minret && !(g && state_eq(opt, s))) { kids[nk] = s; moves[nk++] = j | MOVE_IDENT; }
+          }
+#pragma unroll
+          for (int q = 0; q < 2; ++q) {
+            if (q >= nk) break;
+            const uint32_t k = atomicAdd(&s_nstage, 1u);
+            DCHECK(k < 2 * p.chunk, "stage k %u", k);
+            C* ch = &stage[k];
+            const uint4* src = reinterpret_cast<const uint4*>(pc->cnt);
+            uint4* dst = reinterpret_cast<uint4*>(ch->cnt);
+#pragma unroll
+            for (int w = 0; w < KMAX / 8; ++w) dst[w] = src[w];
+            ch->cnt[j] = (uint16_t)(ch->cnt[j] + 1);
+            ch->tail = kids[q].tail; ch->hash = kids[q].hash; ch->tok = kids[q].tok;
+            ch->ptrace = pc->trace;
+            ch->move = moves[q];
+            const int cr = closure<KMAX>(ch, K, s_cs, recs, hd.flags, pc->minret);
+            if (cr == CL_ALIVE) {
+              ch->fp = fingerprint<KMAX>(ch, nw);
+              ch->slot = 0;
+            } else {
+              ch->slot = SLOT_DEAD;
+              if (cr >= CL_COMPLETE && atomicCAS(&s_found, 0u, 1u) == 0u) {
+                s_found_parent = pc->trace; s_found_move = moves[q]; s_found_p4 = (cr == CL_P4);
+              }
+            }
+          }
+          if (nk) atomicAdd(&s_children, (uint32_t)nk);
+        }
+        __syncthreads();
+        const uint32_t ns = s_nstage;
+        // ---- dedupe: 64-bit CAS open addressing, full-key compare on tag hit
+        for (uint32_t k = tid; k < ns; k += BT) {
+          C* ch = &stage[k];
+          if (ch->slot == SLOT_DEAD) continue;
+          const uint64_t fp = ch->fp;
+          const uint32_t tag = (uint32_t)(fp >> 32);
+          const unsigned long long mine = ((unsigned long long)tag << 32) | (k | STAGE_BIT);
+          uint32_t slot = (uint32_t)fp & mask;
+          for (;;) {
+            const unsigned long long prev = atomicCAS(&ht[slot], HT_EMPTY, mine);
+            if (prev == HT_EMPTY) { ch->slot = slot; break; }
+            if ((uint32_t)(prev >> 32) == tag) {
+              const uint32_t ref = (uint32_t)prev;
+              DCHECK((ref & STAGE_BIT) ? (ref & ~STAGE_BIT) < 2 * p.chunk : ref < p.fcap, "ht ref %x slot %u", ref, slot);
+              const C* o = (ref & STAGE_BIT) ? &stage[ref & ~STAGE_BIT] : &nxt[ref];
+              if (cfg_eq<KMAX>(o, ch, nw)) { ch->slot = SLOT_DEAD; break; }
+            }
+            slot = (slot + 1) & mask;
+          }
+        }
+        __syncthreads();
+        // ---- compact survivors into the next frontier ---------------------
+        for (uint32_t k = tid; k < ns; k += BT) {
+          C* ch = &stage[k];
+          if (ch->slot == SLOT_DEAD) continue;
+          const uint32_t n = atomicAdd(&s_nnext, 1u);
+          if (n < p.fcap) {
+            cfg_copy<KMAX>(&nxt[n], ch);
+            ht[ch->slot] = ((unsigned long long)(uint32_t)(ch->fp >> 32) << 32) | n;
+          } else {
+            s_overflow = 1;
+          }
+        }
+        __syncthreads();
+        if (s_found || s_overflow) break;
+      }
+      if (s_overflow) {
+        for (uint32_t i = tid; i <= mask; i += BT) ht[i] = HT_EMPTY;
+        if (s_found) { verdict = V_OK; reason = 0; ++rounds; }
+        else { verdict = V_UNKNOWN; reason = S2LC_R_FRONTIER; }
+        __syncthreads();
+        break;
+      }
+      const uint32_t nn = min(s_nnext, p.fcap);
+      if (tid == 0) {
+        s_tb = TRACE_NONE;
+        if (s_witness_ok) {
+          if (s_tleft < nn) {
+            const unsigned long long want = max((unsigned long long)nn, (unsigned long long)TRACE_CHUNK);
+            const unsigned long long b = atomicAdd(p.trace_head, want);
+            if (b + want <= p.trace_cap) { s_tbase = b; s_tleft = (uint32_t)want; }
+            else s_witness_ok = 0;
+          }
+          if (s_witness_ok) { s_tb = (uint32_t)s_tbase; s_tbase += nn; s_tleft -= nn; }
+        }
+      }
+      __syncthreads();
+      const uint32_t tb = s_tb;
+      for (uint32_t n = tid; n < nn; n += BT) {
+        C* c = &nxt[n];
+        DCHECK(c->slot <= mask && (tb == TRACE_NONE || tb + n < p.trace_cap), "clear slot %u tb %u n %u", c->slot, tb, n);
+        ht[c->slot] = HT_EMPTY;
+        if (tb != TRACE_NONE) {
+          c->trace = tb + n;
+          p.trace[tb + n].parent = c->ptrace;
+          p.trace[tb + n].move = c->move;
+        } else {
+          c->trace = TRACE_NONE;
+        }
+      }
+      __syncthreads();
+      configs += nn;
+      ++rounds;
+      if (s_found) { verdict = V_OK; reason = 0; break; }
+      if (p.max_configs && configs > p.max_configs) { verdict = V_UNKNOWN; reason = S2LC_R_BUDGET; break; }
+      C* t = cur; cur = nxt; nxt = t;
+      ncur = nn;
+    }
+    if (tid == 0) {
+      HistResult& R = p.res[h];
+      R.verdict = verdict;
+      R.reason = reason;
+      R.rounds = rounds;
+      R.configs = configs;
+      R.children = s_children;
+      R.p4 = s_found_p4;
+      R.final_parent = (verdict == V_OK && s_witness_ok) ? s_found_parent : TRACE_NONE;
+      R.final_move = s_found_move;
+      R.witness_len = 0;
+      R.has_witness = (verdict == V_OK && s_witness_ok) ? 2u : 0u;  // resolved by walk_kernel
+    }
+    __syncthreads();
+  }
+}
+
+// Witness extraction: one lane per history walks the parent chain backwards
+// and writes the move list in order.
+__global__ void walk_kernel(uint32_t n, HistResult* res, const TraceEnt* trace, uint32_t* moves) {
+  const uint32_t h = blockIdx.x * blockDim.x + threadIdx.x;
+  if (h >= n) return;
+  HistResult r = res[h];
+  if (r.verdict != V_OK || r.has_witness != 2u) return;
+  const uint32_t len = (r.final_move == TRACE_NONE) ? 0u : r.rounds;
+  uint32_t* out = moves + r.witness_off;
+  bool ok = true;
+  if (len) {
+    out[len - 1] = r.final_move;
+    uint32_t idx = r.final_parent;
+    uint32_t pos = len - 1;
+    while (pos > 0 && idx != TRACE_NONE) {
+      const TraceEnt e = trace[idx];
+      out[--pos] = e.move;
+      idx = e.parent;
+    }
+    ok = (pos == 0);
+  }
+  res[h].witness_len = ok ? len : 0u;
+  res[h].has_witness = ok ? 1u : 0u;
+}
+
+}  // namespace
+}  // namespace s2lc
