@@ -57,6 +57,7 @@ struct DevBatch {
   int device = 0;
   uint32_t n_hist = 0;
   uint32_t kmax = 16;
+  uint32_t n_recs = 0, n_pool = 0;
   OpRec* recs = nullptr;
   uint64_t* pool = nullptr;
   uint32_t* chain_start = nullptr;

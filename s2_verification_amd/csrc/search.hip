@@ -144,6 +144,8 @@ int batch_upload(DevBatch& b, const std::vector<const History*>& hs, std::string
     return (uint64_t)b.h_hist[x].n_ops * b.h_hist[x].K > (uint64_t)b.h_hist[y].n_ops * b.h_hist[y].K;
   });
   b.moves_cap = moves_total;
+  b.n_recs = (uint32_t)recs.size();
+  b.n_pool = (uint32_t)pool.size();
   HIPCHK(hipMalloc(&b.recs, recs.size() * sizeof(OpRec)));
   HIPCHK(hipMalloc(&b.pool, pool.size() * sizeof(uint64_t)));
   HIPCHK(hipMalloc(&b.chain_start, cs.size() * sizeof(uint32_t)));
@@ -214,6 +216,13 @@ int batch_run(DevBatch& b, hipStream_t stream, uint64_t max_configs, bool witnes
   prm.fcap = g.fcap; prm.chunk = g.chunk; prm.ht_mask = g.ht_slots - 1;
   prm.trace = b.trace; prm.trace_head = b.trace_head; prm.trace_cap = witness ? b.trace_cap : 0;
   prm.res = b.res; prm.max_configs = max_configs; prm.witness = witness ? 1 : 0;
+  prm.n_recs = b.n_recs; prm.n_pool = b.n_pool; prm.n_res = b.n_hist;
+#ifdef S2LC_GUARD
+  {
+    uint32_t z[8] = {0};
+    HIPCHK(hipMemcpyToSymbol(HIP_SYMBOL(g_guard), z, sizeof z));
+  }
+#endif
 
   hipEvent_t e0, e1;
   HIPCHK(hipEventCreate(&e0));
@@ -228,6 +237,17 @@ int batch_run(DevBatch& b, hipStream_t stream, uint64_t max_configs, bool witnes
   HIPCHK(hipEventRecord(e1, stream));
   HIPCHK(hipMemcpyAsync(b.h_res.data(), b.res, b.n_hist * sizeof(HistResult), hipMemcpyDeviceToHost, stream));
   HIPCHK(hipStreamSynchronize(stream));
+#ifdef S2LC_GUARD
+  {
+    uint32_t gg[8];
+    HIPCHK(hipMemcpyFromSymbol(gg, HIP_SYMBOL(g_guard), sizeof gg));
+    if (gg[0]) {
+      err = "guard: " + std::to_string(gg[0]) + " violations, first at search_dev.h:" + std::to_string(gg[1]) +
+            " a=" + std::to_string(gg[2]) + " b=" + std::to_string(gg[3]);
+      return S2LC_EHIP;
+    }
+  }
+#endif
   float ms = 0;
   HIPCHK(hipEventElapsedTime(&ms, e0, e1));
   st.kernel_ms = ms;

@@ -27,6 +27,20 @@ enum : int { CL_ALIVE = 0, CL_DEAD = 1, CL_COMPLETE = 2, CL_P4 = 3 };
 #define DCHECK(cond, ...) do { } while (0)
 #endif
 
+// S2LC_GUARD: diagnostic build. Every computed index is range-checked; the
+// first violation is recorded in g_guard (read back by the host) and the
+// access is redirected to a safe index instead of faulting.
+#ifdef S2LC_GUARD
+__device__ uint32_t g_guard[8];
+__device__ __forceinline__ bool guard_ok(bool cond, uint32_t line, uint32_t a, uint32_t b) {
+  if (!cond && atomicAdd(&g_guard[0], 1u) == 0u) { g_guard[1] = line; g_guard[2] = a; g_guard[3] = b; }
+  return cond;
+}
+#define GUARD(cond, a, b) guard_ok((cond), __LINE__, (uint32_t)(a), (uint32_t)(b))
+#else
+#define GUARD(cond, a, b) true
+#endif
+
 template <int KMAX>
 struct __attribute__((aligned(16))) Cfg {
   uint64_t tail;
@@ -60,6 +74,7 @@ struct Params {
   HistResult* res;
   uint64_t max_configs;
   uint32_t witness;
+  uint32_t n_recs, n_pool, n_res;  // buffer sizes (guard build checks)
 };
 
 __device__ __forceinline__ uint64_t mix64(uint64_t x) {
@@ -107,14 +122,16 @@ __device__ __forceinline__ uint32_t closure_block(const uint32_t* cb, int nq, in
   uint4 obs[B], mid[B];
   uint32_t fl[B];
 #pragma unroll
-  for (int q = 0; q < B; ++q)
-    if (q < nq) {
-      DCHECK(cs[b + q] + cb[q] < cs[b + q + 1], "closure chain %d cnt %u start %u end %u", b + q, cb[q], cs[b + q], cs[b + q + 1]);
-      const OpRec* r = &recs[cs[b + q] + cb[q]];
-      obs[q] = ld16(r, 16);
-      mid[q] = ld16(r, 32);
-      fl[q] = r->flags;
-    }
+  for (int q = 0; q < B; ++q) {
+    // unconditional: chains >= K have count 0 and a valid record (see s_cs)
+    uint32_t idx = cs[b + q] + (q < nq ? cb[q] : 0u);
+    DCHECK(q >= nq || idx < cs[b + q + 1], "closure chain %d idx %u end %u", b + q, idx, cs[b + q + 1]);
+    if (!GUARD(q >= nq || idx < cs[b + q + 1], idx, cs[b + q + 1])) idx = cs[b + q];
+    const OpRec* r = &recs[idx];
+    obs[q] = ld16(r, 16);
+    mid[q] = ld16(r, 32);
+    fl[q] = r->flags;
+  }
   uint32_t adv = 0;
 #pragma unroll
   for (int q = 0; q < B; ++q) {
@@ -250,7 +267,7 @@ __device__ __forceinline__ void cfg_copy(Cfg<KMAX>* d, const Cfg<KMAX>* s) {
 template <int KMAX, int BT>
 __global__ __launch_bounds__(BT) void search_kernel(Params p) {
   using C = Cfg<KMAX>;
-  __shared__ uint32_t s_cs[KMAX + 1];
+  __shared__ uint32_t s_cs[KMAX + 1];  // chain starts; entries > K point at a sentinel
   __shared__ uint32_t s_h, s_nstage, s_nnext, s_found, s_overflow, s_children;
   __shared__ uint32_t s_found_parent, s_found_move, s_found_p4;
   __shared__ uint32_t s_tb, s_tleft, s_witness_ok;
@@ -274,14 +291,20 @@ __global__ __launch_bounds__(BT) void search_kernel(Params p) {
     __syncthreads();
     const uint32_t hi = s_h;
     if (hi >= p.n_hist) break;
-    const uint32_t h = p.order[hi];
+    uint32_t h = p.order[hi];
+    if (!GUARD(h < p.n_res, h, hi)) h = 0;
     if (tid == 0) s_hd = p.hist[h];
     __syncthreads();
     const HistDesc hd = s_hd;
     const int K = hd.K;
     const int nw = (K + 7) >> 3;
     const OpRec* __restrict__ recs = p.recs;
-    for (int j = tid; j <= K; j += BT) s_cs[j] = p.chain_start[hd.cs_base + j];
+    // Chains >= K point at a valid record (the last sentinel) so that closure
+    // can load all KMAX heads unconditionally; their results are ignored.
+    for (int j = tid; j <= KMAX; j += BT) {
+      const uint32_t last = p.chain_start[hd.cs_base + K];
+      s_cs[j] = j <= K ? p.chain_start[hd.cs_base + j] : (last > 0 ? last - 1 : 0);
+    }
     if (tid == 0) {
       s_found = 0; s_overflow = 0; s_children = 0;
       s_witness_ok = p.witness;
@@ -292,7 +315,8 @@ __global__ __launch_bounds__(BT) void search_kernel(Params p) {
     // ---- initial configuration: (∅, (0, 0, nil)) closed ------------------
     if (tid == 0) {
       C* c = &fa[0];
-      for (int q = 0; q < KMAX; ++q) c->cnt[q] = 0;
+#pragma unroll
+      for (int w = 0; w < KMAX / 8; ++w) reinterpret_cast<uint4*>(c->cnt)[w] = make_uint4(0, 0, 0, 0);
       c->tail = 0; c->hash = 0; c->tok = 0;
       c->ptrace = TRACE_NONE; c->move = TRACE_NONE; c->slot = 0;
       const int r = closure<KMAX>(c, K, s_cs, recs, hd.flags, 0u);
@@ -308,7 +332,7 @@ __global__ __launch_bounds__(BT) void search_kernel(Params p) {
         }
         if (s_witness_ok) {
           t = (uint32_t)s_tbase; s_tbase += 1; s_tleft -= 1;
-          p.trace[t].parent = TRACE_NONE; p.trace[t].move = TRACE_NONE;
+          if (GUARD((uint64_t)t < p.trace_cap, t, 0)) { p.trace[t].parent = TRACE_NONE; p.trace[t].move = TRACE_NONE; }
         }
       }
       c->trace = t;
@@ -318,6 +342,7 @@ __global__ __launch_bounds__(BT) void search_kernel(Params p) {
     C* cur = fa;
     C* nxt = fb;
     uint32_t ncur = s_nnext;
+    __syncthreads();  // every lane has read s_nnext before lane 0 resets it below
     uint64_t configs = ncur;
     uint32_t rounds = 0;
     uint32_t verdict = V_ILLEGAL, reason = S2LC_R_SEARCH_EXHAUSTED;
@@ -336,8 +361,10 @@ __global__ __launch_bounds__(BT) void search_kernel(Params p) {
           const uint32_t i = it / (uint32_t)K;
           const uint32_t j = it - i * (uint32_t)K;
           const C* pc = &cur[i];
-          DCHECK(i < ncur && s_cs[j] + pc->cnt[j] < s_cs[j + 1], "expand i %u ncur %u j %u cnt %u", i, ncur, j, (uint32_t)pc->cnt[j]);
-          const OpRec r = load_rec(&recs[s_cs[j] + pc->cnt[j]]);
+          const uint32_t cj = (reinterpret_cast<const uint32_t*>(pc->cnt)[j >> 1] >> (16 * (j & 1))) & 0xFFFFu;
+          DCHECK(i < ncur && s_cs[j] + cj < s_cs[j + 1], "expand i %u ncur %u j %u cnt %u", i, ncur, j, cj);
+          if (!GUARD(i < ncur && s_cs[j] + cj < s_cs[j + 1] && s_cs[j + 1] <= p.n_recs, i * 65536u + j, cj)) continue;
+          const OpRec r = load_rec(&recs[s_cs[j] + cj]);
           if ((r.flags & (OPF_SENTINEL | OPF_CLS_E)) || r.call_ev >= pc->minret) continue;
           const State s{pc->tail, pc->hash, pc->tok};
           const bool g = append_guards_ok(r, s);
@@ -345,6 +372,7 @@ __global__ __launch_bounds__(BT) void search_kernel(Params p) {
           uint32_t moves[2];
           int nk = 0;
           State opt{0, 0, 0};
+          if (!GUARD((uint64_t)r.hash_off + r.hash_cnt <= p.n_pool, r.hash_off, r.hash_cnt)) continue;
           if (g) opt = append_opt(r, s, p.pool);
           if (r.flags & OPF_CLS_D) {
             if (g && opt.tail == r.out_tail) { kids[nk] = opt; moves[nk++] = j; }
@@ -357,12 +385,26 @@ __global__ __launch_bounds__(BT) void search_kernel(Params p) {
             if (q >= nk) break;
             const uint32_t k = atomicAdd(&s_nstage, 1u);
             DCHECK(k < 2 * p.chunk, "stage k %u", k);
+            if (!GUARD(k < 2 * p.chunk, k, 0)) break;
             C* ch = &stage[k];
+            // child counts = parent counts with chain j advanced, built in
+            // registers and written with the same 16-byte type used to read them
             const uint4* src = reinterpret_cast<const uint4*>(pc->cnt);
             uint4* dst = reinterpret_cast<uint4*>(ch->cnt);
 #pragma unroll
-            for (int w = 0; w < KMAX / 8; ++w) dst[w] = src[w];
-            ch->cnt[j] = (uint16_t)(ch->cnt[j] + 1);
+            for (int w = 0; w < KMAX / 8; ++w) {
+              uint4 v = src[w];
+              if ((int)(j >> 3) == w) {
+                const uint32_t inc = (j & 1) ? 0x10000u : 1u;
+                switch ((j >> 1) & 3) {
+                  case 0: v.x += inc; break;
+                  case 1: v.y += inc; break;
+                  case 2: v.z += inc; break;
+                  default: v.w += inc; break;
+                }
+              }
+              dst[w] = v;
+            }
             ch->tail = kids[q].tail; ch->hash = kids[q].hash; ch->tok = kids[q].tok;
             ch->ptrace = pc->trace;
             ch->move = moves[q];
@@ -395,8 +437,10 @@ __global__ __launch_bounds__(BT) void search_kernel(Params p) {
             if ((uint32_t)(prev >> 32) == tag) {
               const uint32_t ref = (uint32_t)prev;
               DCHECK((ref & STAGE_BIT) ? (ref & ~STAGE_BIT) < 2 * p.chunk : ref < p.fcap, "ht ref %x slot %u", ref, slot);
-              const C* o = (ref & STAGE_BIT) ? &stage[ref & ~STAGE_BIT] : &nxt[ref];
-              if (cfg_eq<KMAX>(o, ch, nw)) { ch->slot = SLOT_DEAD; break; }
+              if (GUARD((ref & STAGE_BIT) ? (ref & ~STAGE_BIT) < 2 * p.chunk : ref < p.fcap, ref, slot)) {
+                const C* o = (ref & STAGE_BIT) ? &stage[ref & ~STAGE_BIT] : &nxt[ref];
+                if (cfg_eq<KMAX>(o, ch, nw)) { ch->slot = SLOT_DEAD; break; }
+              }
             }
             slot = (slot + 1) & mask;
           }
@@ -409,7 +453,8 @@ __global__ __launch_bounds__(BT) void search_kernel(Params p) {
           const uint32_t n = atomicAdd(&s_nnext, 1u);
           if (n < p.fcap) {
             cfg_copy<KMAX>(&nxt[n], ch);
-            ht[ch->slot] = ((unsigned long long)(uint32_t)(ch->fp >> 32) << 32) | n;
+            if (GUARD(ch->slot <= mask, ch->slot, n))
+              ht[ch->slot] = ((unsigned long long)(uint32_t)(ch->fp >> 32) << 32) | n;
           } else {
             s_overflow = 1;
           }
@@ -442,8 +487,8 @@ __global__ __launch_bounds__(BT) void search_kernel(Params p) {
       for (uint32_t n = tid; n < nn; n += BT) {
         C* c = &nxt[n];
         DCHECK(c->slot <= mask && (tb == TRACE_NONE || tb + n < p.trace_cap), "clear slot %u tb %u n %u", c->slot, tb, n);
-        ht[c->slot] = HT_EMPTY;
-        if (tb != TRACE_NONE) {
+        if (GUARD(c->slot <= mask, c->slot, n)) ht[c->slot] = HT_EMPTY;
+        if (tb != TRACE_NONE && GUARD((uint64_t)tb + n < p.trace_cap, tb, n)) {
           c->trace = tb + n;
           p.trace[tb + n].parent = c->ptrace;
           p.trace[tb + n].move = c->move;
