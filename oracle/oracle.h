@@ -74,6 +74,11 @@ int or_check_wgl(const or_event* ev, size_t n, int compute_partial, double timeo
 /* Independent brute force: every real-time-respecting order, powerset model.
  * Only for small histories (n_ops <= 20). */
 int or_check_brute(const or_event* ev, size_t n, or_stats* st);
+/* Independent CPU implementation of the GPU's reduced search (reduced.c):
+ * NOT a restatement of the reference; a cross-check where WGL cannot finish.
+ * st->cache_inserts = configurations, st->backtracks = rounds,
+ * st->max_state_set = widest frontier. */
+int or_check_reduced(const or_event* ev, size_t n, uint64_t max_configs, or_stats* st);
 
 #ifdef __cplusplus
 }

@@ -69,6 +69,8 @@ def lib():
         L.or_check_wgl.restype = ctypes.c_int
         L.or_check_wgl.argtypes = [ctypes.c_void_p, ctypes.c_size_t, ctypes.c_int, ctypes.c_double,
                                    ctypes.c_uint64, ctypes.POINTER(_Stats)]
+        L.or_check_reduced.restype = ctypes.c_int
+        L.or_check_reduced.argtypes = [ctypes.c_void_p, ctypes.c_size_t, ctypes.c_uint64, ctypes.POINTER(_Stats)]
         L.or_check_brute.restype = ctypes.c_int
         L.or_check_brute.argtypes = [ctypes.c_void_p, ctypes.c_size_t, ctypes.POINTER(_Stats)]
         _lib = L
@@ -161,6 +163,15 @@ def check_brute(events):
     st = _Stats()
     r = lib().or_check_brute(ea.ptr, len(ea), ctypes.byref(st))
     return _NAMES[r], {"steps": st.steps}
+
+
+def check_reduced(events, max_configs=0):
+    """CPU implementation of the GPU's reduced search (cross-check, not the reference)."""
+    ea = _as_array(events)
+    st = _Stats()
+    r = lib().or_check_reduced(ea.ptr, len(ea), int(max_configs), ctypes.byref(st))
+    return _NAMES[r], {"configs": st.cache_inserts, "rounds": st.backtracks, "max_frontier": st.max_state_set,
+                       "children": st.steps, "seconds": st.seconds}
 
 
 # ------------------------------------------------------------------ loader --

@@ -86,3 +86,69 @@ def test_simulated_vs_wgl(checker, wf):
     for i, (r, e) in enumerate(zip(res, expect)):
         assert r.verdict == e, (wf, i, r, e)
     assert "Ok" in expect and "Illegal" in expect
+
+
+@pytest.mark.parametrize("name", ["C1", "C2", "C3"])
+def test_configs_vs_wgl_and_reduced(checker, name):
+    """BASELINE configs C1-C3 (porcupine's DFS finishes on these)."""
+    from s2_verification_amd import workloads as W
+    h = W.config_history(name)
+    ea = orc.from_s2lc_numpy(h.events_numpy())
+    w, _ = orc.check_wgl(ea, timeout=120)
+    r_, _ = orc.check_reduced(ea)
+    g = checker.check(h)
+    assert w in ("Ok", "Illegal") and w == r_ == g.verdict, (name, w, r_, g)
+    if g.verdict == s2.Ok:
+        assert g.witness is not None and len(g.witness) == h.info()["n_ops"]
+
+
+@pytest.mark.parametrize("name,expect", [("C5", "Ok"), ("C5bad", "Illegal")])
+def test_single_hard_history(checker, name, expect):
+    """C5: 32 clients x 1000 ops. Porcupine's DFS does not finish (exponential
+    backtracking); verdict cross-checked by the CPU reduced search,
+    Ok witnesses replayed through the CPU model; the bad variant differs from the
+    clean one in exactly one ReadSuccess stream hash (Illegal by construction,
+    up to a 2^-64 hash collision)."""
+    from s2_verification_amd import workloads as W
+    h = W.config_history(name)
+    ea = orc.from_s2lc_numpy(h.events_numpy())
+    r_, st = orc.check_reduced(ea)
+    g = checker.check(h)
+    assert g.verdict == r_ == expect, (name, g, r_, st)
+    if expect == "Ok":
+        assert g.witness is not None and len(g.witness) == h.info()["n_ops"]
+    else:
+        good = W.config_history("C5").events()
+        bad = h.events()
+        diff = [i for i, (a, b) in enumerate(zip(good, bad)) if a != b]
+        assert len(good) == len(bad) and len(diff) == 1
+        assert bad[diff[0]].Value.StreamHash != good[diff[0]].Value.StreamHash
+
+
+def test_c4_sample_vs_wgl(checker):
+    """500 histories of the bench workload (all workflows, 10% injected violations)."""
+    from s2_verification_amd import workloads as W
+    hs = W.c4_histories(500)
+    expect = [orc.check_wgl(orc.from_s2lc_numpy(h.events_numpy()))[0] for h in hs]
+    res = checker.check_batch(hs)
+    assert [r.verdict for r in res] == expect
+    assert all(r.witness is not None for r in res if r.verdict == s2.Ok)
+
+
+def test_cli_verdicts_and_exit_codes():
+    import json
+    import subprocess
+    for c in golden("reference_cases.json")["cases"]:
+        if not c.get("jsonl_file"):
+            continue
+        p = subprocess.run([s2.CLI_PATH, "-file=" + os.path.join(GOLDEN, c["jsonl_file"])], capture_output=True,
+                           text=True, timeout=120)
+        line = json.loads(p.stderr.strip().splitlines()[-1])
+        if c["expected"] == "Ok":
+            assert p.returncode == 0 and line["msg"] == "passed: is linearizable", (c["name"], p.stderr)
+        else:
+            assert p.returncode == 1 and line["msg"] == "failed: is NOT linearizable" and line["res"] == "Illegal"
+    # stdin
+    with open(os.path.join(GOLDEN, "ref_BasicNoConcurrency.jsonl"), "rb") as f:
+        p = subprocess.run([s2.CLI_PATH, "-file", "-"], stdin=f, capture_output=True, timeout=120)
+    assert p.returncode == 0

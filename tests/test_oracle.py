@@ -73,3 +73,19 @@ def test_model_panics_are_reported():
     call = {"kind": "call", "op_id": 1, "input_type": 0, "num_records": None, "record_hashes": []}
     ret = {"kind": "return", "op_id": 1, "failure": False, "definite_failure": False, "tail": 0}
     assert orc.check_wgl([call, ret])[0] == "Panic"
+
+
+def test_reduced_search_matches_wgl():
+    """The CPU reduced search (cross-check oracle for C5) agrees with the WGL
+    restatement on random histories and on simulator histories."""
+    import s2_verification_amd as s2
+    rng = random.Random(99)
+    for _ in range(1500):
+        ev = random_history(rng, rng.randint(0, 9), n_clients=rng.randint(1, 4))
+        assert orc.check_reduced(ev)[0] == orc.check_wgl(ev)[0], ev
+    for wf in (0, 1, 2):
+        for seed in range(25):
+            h = s2.simulate_history(workflow=wf, num_clients=4 + seed % 4, ops_per_client=60, seed=seed,
+                                    violation=seed % 5, p_indefinite=0.03)
+            ea = orc.from_s2lc_numpy(h.events_numpy())
+            assert orc.check_reduced(ea)[0] == orc.check_wgl(ea)[0]
