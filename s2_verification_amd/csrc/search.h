@@ -43,14 +43,17 @@ struct HistResult {
 };
 
 struct SearchGeom {
+  bool shared;         // arrays in LDS (true) or in a per-workgroup HBM slab
   uint32_t block;      // threads per workgroup (64 or 256)
   uint32_t kmax;       // 16 / 32 / 64 / 128
   uint32_t fcap;       // frontier capacity per workgroup
+  uint32_t stage_cap;  // staging entries
   uint32_t chunk;      // expansion items per chunk
   uint32_t ht_slots;   // power of two
   uint32_t grid;       // workgroups
   size_t cfg_bytes;
-  size_t slab_bytes;
+  size_t slab_bytes;   // HBM bytes per workgroup (0 when shared)
+  size_t smem_bytes;   // dynamic LDS bytes per workgroup
 };
 
 struct DevBatch {
@@ -83,7 +86,8 @@ struct DevBatch {
 };
 
 struct RunStats {
-  double kernel_ms = 0, total_ms = 0;
+  double kernel_ms = 0, total_ms = 0, pass0_ms = 0;
+  uint32_t n_overflow2 = 0;
   uint64_t configs = 0, children = 0, rounds = 0;
   uint64_t algo_bytes = 0;
   uint32_t n_overflow = 0, launches = 0;

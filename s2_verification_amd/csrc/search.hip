@@ -41,45 +41,65 @@ namespace {
     }                                                                    \
   } while (0)
 
-template <int KMAX, int BT>
-hipError_t launch_search(const Params& prm, uint32_t grid, hipStream_t st) {
-  hipLaunchKernelGGL((search_kernel<KMAX, BT>), dim3(grid), dim3(BT), 0, st, prm);
+template <int KMAX, int BT, bool SHARED>
+hipError_t launch_search(const Params& prm, uint32_t grid, size_t smem, hipStream_t st) {
+  hipLaunchKernelGGL((search_kernel<KMAX, BT, SHARED>), dim3(grid), dim3(BT), smem, st, prm);
   return hipGetLastError();
 }
 
-hipError_t launch_dispatch(uint32_t kmax, uint32_t block, const Params& prm, uint32_t grid, hipStream_t st) {
+template <bool SHARED>
+hipError_t launch_kmax(uint32_t kmax, uint32_t block, const Params& prm, uint32_t grid, size_t smem, hipStream_t st) {
   if (block == 64) {
     switch (kmax) {
-      case 16: return launch_search<16, 64>(prm, grid, st);
-      case 32: return launch_search<32, 64>(prm, grid, st);
-      case 64: return launch_search<64, 64>(prm, grid, st);
-      default: return launch_search<128, 64>(prm, grid, st);
+      case 16: return launch_search<16, 64, SHARED>(prm, grid, smem, st);
+      case 32: return launch_search<32, 64, SHARED>(prm, grid, smem, st);
+      case 64: return launch_search<64, 64, SHARED>(prm, grid, smem, st);
+      default: return launch_search<128, 64, SHARED>(prm, grid, smem, st);
     }
   }
   switch (kmax) {
-    case 16: return launch_search<16, 256>(prm, grid, st);
-    case 32: return launch_search<32, 256>(prm, grid, st);
-    case 64: return launch_search<64, 256>(prm, grid, st);
-    default: return launch_search<128, 256>(prm, grid, st);
+    case 16: return launch_search<16, 256, SHARED>(prm, grid, smem, st);
+    case 32: return launch_search<32, 256, SHARED>(prm, grid, smem, st);
+    case 64: return launch_search<64, 256, SHARED>(prm, grid, smem, st);
+    default: return launch_search<128, 256, SHARED>(prm, grid, smem, st);
   }
 }
 
 size_t cfg_bytes(uint32_t kmax) { return 48 + 2 * (size_t)kmax; }
 
-SearchGeom make_geom(uint32_t kmax, uint32_t block, uint32_t fcap, uint32_t chunk, uint32_t grid) {
+size_t state_bytes(uint32_t kmax) {
+  switch (kmax) {
+    case 16: return wg_state_bytes<16>();
+    case 32: return wg_state_bytes<32>();
+    case 64: return wg_state_bytes<64>();
+    default: return wg_state_bytes<128>();
+  }
+}
+
+SearchGeom make_geom(uint32_t kmax, bool shared, uint32_t block, uint32_t fcap, uint32_t stage_cap, uint32_t chunk,
+                     uint32_t grid) {
   SearchGeom g;
   g.block = block;
   g.kmax = kmax;
   g.fcap = fcap;
   g.chunk = chunk;
+  g.stage_cap = stage_cap;
+  g.shared = shared;
   uint32_t ht = 16;
-  while (ht < 2 * (fcap + 2 * chunk)) ht <<= 1;
+  while (ht < 2 * (fcap + stage_cap)) ht <<= 1;
   g.ht_slots = ht;
   g.grid = grid;
   g.cfg_bytes = cfg_bytes(kmax);
-  g.slab_bytes = (2 * (size_t)fcap + 2 * (size_t)chunk) * g.cfg_bytes + (size_t)ht * 8;
-  g.slab_bytes = (g.slab_bytes + 255) & ~(size_t)255;
+  size_t arrays = (2 * (size_t)fcap + stage_cap) * g.cfg_bytes + (size_t)ht * 8;
+  arrays = (arrays + 255) & ~(size_t)255;
+  g.smem_bytes = state_bytes(kmax) + (shared ? arrays : 0);
+  g.slab_bytes = shared ? 0 : arrays;
   return g;
+}
+
+hipError_t launch_geom(const SearchGeom& g, const Params& prm, hipStream_t st) {
+  return g.shared ? launch_kmax<true>(g.kmax, g.block, prm, g.grid, g.smem_bytes, st)
+                  : launch_kmax<false>(g.kmax, g.block, prm, g.grid, g.smem_bytes, st);
 }
 
 }  // namespace
@@ -202,84 +222,99 @@ int batch_run(DevBatch& b, hipStream_t stream, uint64_t max_configs, bool witnes
     HIPCHK(hipMalloc(&b.trace, want * sizeof(TraceEnt)));
     b.trace_cap = want;
   }
-  // main pass: 64-lane workgroups, small frontier slabs, persistent grid
-  const uint32_t grid0 = std::max<uint32_t>(1, std::min<uint32_t>(n_search, (uint32_t)n_cu * 16));
-  SearchGeom g = make_geom(b.kmax, 64, 1024, 256, grid0);
-  size_t cap = b.slab_cap;
-  if (ensure((void**)&b.slab, cap, g.slab_bytes * g.grid, err)) return S2LC_EHIP;
-  b.slab_cap = cap;
 
   Params prm;
+  memset(&prm, 0, sizeof prm);
   prm.recs = b.recs; prm.pool = b.pool; prm.chain_start = b.chain_start; prm.hist = b.hist;
-  prm.order = b.order; prm.n_hist = n_search; prm.counter = b.counter;
-  prm.slab = b.slab; prm.slab_bytes = g.slab_bytes;
-  prm.fcap = g.fcap; prm.chunk = g.chunk; prm.ht_mask = g.ht_slots - 1;
   prm.trace = b.trace; prm.trace_head = b.trace_head; prm.trace_cap = witness ? b.trace_cap : 0;
   prm.res = b.res; prm.max_configs = max_configs; prm.witness = witness ? 1 : 0;
   prm.n_recs = b.n_recs; prm.n_pool = b.n_pool; prm.n_res = b.n_hist;
-#ifdef S2LC_GUARD
-  {
-    uint32_t z[8] = {0};
-    HIPCHK(hipMemcpyToSymbol(HIP_SYMBOL(g_guard), z, sizeof z));
-  }
-#endif
 
   hipEvent_t e0, e1;
   HIPCHK(hipEventCreate(&e0));
   HIPCHK(hipEventCreate(&e1));
   HIPCHK(hipMemsetAsync(b.counter, 0, 16 * sizeof(uint32_t), stream));
   HIPCHK(hipMemsetAsync(b.trace_head, 0, sizeof(unsigned long long), stream));
-  HIPCHK(hipEventRecord(e0, stream));
-  if (n_search) {
-    HIPCHK(launch_dispatch(g.kmax, g.block, prm, g.grid, stream));
-    st.launches++;
-  }
-  HIPCHK(hipEventRecord(e1, stream));
-  HIPCHK(hipMemcpyAsync(b.h_res.data(), b.res, b.n_hist * sizeof(HistResult), hipMemcpyDeviceToHost, stream));
-  HIPCHK(hipStreamSynchronize(stream));
-#ifdef S2LC_GUARD
-  {
-    uint32_t gg[8];
-    HIPCHK(hipMemcpyFromSymbol(gg, HIP_SYMBOL(g_guard), sizeof gg));
-    if (gg[0]) {
-      err = "guard: " + std::to_string(gg[0]) + " violations, first at search_dev.h:" + std::to_string(gg[1]) +
-            " a=" + std::to_string(gg[2]) + " b=" + std::to_string(gg[3]);
-      return S2LC_EHIP;
-    }
-  }
-#endif
-  float ms = 0;
-  HIPCHK(hipEventElapsedTime(&ms, e0, e1));
-  st.kernel_ms = ms;
 
-  // wide pass for frontier overflows: 256-lane workgroups, large slabs
-  std::vector<uint32_t> over;
-  for (uint32_t i = 0; i < b.n_hist; ++i)
-    if (!b.forced[i] && b.h_res[i].verdict == V_UNKNOWN && b.h_res[i].reason == S2LC_R_FRONTIER) over.push_back(i);
-  st.n_overflow = (uint32_t)over.size();
-  if (!over.empty()) {
-    size_t free_b = 0, total_b = 0;
-    HIPCHK(hipMemGetInfo(&free_b, &total_b));
-    uint32_t fcap = 1u << 20;
-    SearchGeom gw = make_geom(b.kmax, 256, fcap, 16384, 1);
-    while (gw.slab_bytes > free_b / 2 && fcap > 4096) { fcap >>= 1; gw = make_geom(b.kmax, 256, fcap, 16384, 1); }
-    uint32_t gridw = (uint32_t)std::min<size_t>(over.size(), std::max<size_t>(1, (free_b / 2) / gw.slab_bytes));
-    gridw = std::min<uint32_t>(gridw, (uint32_t)n_cu);
-    gw.grid = gridw;
-    if (ensure((void**)&b.slab, b.slab_cap, gw.slab_bytes * gw.grid, err)) return S2LC_EHIP;
-    uint32_t* d_over = nullptr;
-    HIPCHK(hipMalloc(&d_over, over.size() * sizeof(uint32_t)));
-    HIPCHK(hipMemcpyAsync(d_over, over.data(), over.size() * sizeof(uint32_t), hipMemcpyHostToDevice, stream));
-    Params pw = prm;
-    pw.order = d_over; pw.n_hist = (uint32_t)over.size(); pw.counter = b.counter + 4;
-    pw.slab = b.slab; pw.slab_bytes = gw.slab_bytes;
-    pw.fcap = gw.fcap; pw.chunk = gw.chunk; pw.ht_mask = gw.ht_slots - 1;
-    HIPCHK(launch_dispatch(gw.kmax, gw.block, pw, gw.grid, stream));
+  // Pass 0: LDS-resident search for every history (small frontier / staging).
+  // Pass 1: HBM slab, 64 lanes, frontier 1024, for the ones that outgrew LDS.
+  // Pass 2: HBM slab, 256 lanes, frontier up to 2^20.
+  const uint32_t lds_fcap = b.kmax <= 32 ? 16 : 8;
+  const uint32_t lds_stage = b.kmax <= 32 ? 64 : 32;
+  std::vector<uint32_t> todo;  // histories for passes >= 1
+  uint32_t* d_list = nullptr;
+  for (int pass = 0; pass < 3; ++pass) {
+    uint32_t n_pass = pass == 0 ? n_search : (uint32_t)todo.size();
+    if (n_pass == 0) break;
+    SearchGeom g;
+    if (pass == 0) {
+      g = make_geom(b.kmax, true, 64, lds_fcap, lds_stage, lds_stage, 1);
+      const uint32_t per_cu = std::max<uint32_t>(1, std::min<uint32_t>(16, (uint32_t)((160 * 1024) / g.smem_bytes)));
+      g.grid = std::max<uint32_t>(1, std::min<uint32_t>(n_pass, (uint32_t)n_cu * per_cu));
+    } else if (pass == 1) {
+      g = make_geom(b.kmax, false, 64, 1024, 512, 256, 1);
+      g.grid = std::max<uint32_t>(1, std::min<uint32_t>(n_pass, (uint32_t)n_cu * 16));
+    } else {
+      size_t free_b = 0, total_b = 0;
+      HIPCHK(hipMemGetInfo(&free_b, &total_b));
+      uint32_t fcap = 1u << 20;
+      g = make_geom(b.kmax, false, 256, fcap, 32768, 16384, 1);
+      while (g.slab_bytes > free_b / 2 && fcap > 4096) { fcap >>= 1; g = make_geom(b.kmax, false, 256, fcap, 32768, 16384, 1); }
+      g.grid = (uint32_t)std::min<size_t>(n_pass, std::max<size_t>(1, (free_b / 2) / g.slab_bytes));
+      g.grid = std::min<uint32_t>(g.grid, (uint32_t)n_cu);
+    }
+    if (!g.shared && ensure((void**)&b.slab, b.slab_cap, g.slab_bytes * g.grid, err)) return S2LC_EHIP;
+    Params pp = prm;
+    if (pass == 0) {
+      pp.order = b.order;
+    } else {
+      if (d_list) (void)hipFree(d_list);
+      d_list = nullptr;
+      HIPCHK(hipMalloc(&d_list, todo.size() * sizeof(uint32_t)));
+      HIPCHK(hipMemcpyAsync(d_list, todo.data(), todo.size() * sizeof(uint32_t), hipMemcpyHostToDevice, stream));
+      pp.order = d_list;
+    }
+    pp.n_hist = n_pass;
+    pp.counter = b.counter + 4 * pass;
+    pp.slab = b.slab;
+    pp.slab_bytes = g.slab_bytes;
+    pp.fcap = g.fcap; pp.chunk = g.chunk; pp.stage_cap = g.stage_cap; pp.ht_mask = g.ht_slots - 1;
+#ifdef S2LC_GUARD
+    {
+      uint32_t z[8] = {0};
+      HIPCHK(hipMemcpyToSymbol(HIP_SYMBOL(g_guard), z, sizeof z));
+    }
+#endif
+    HIPCHK(hipEventRecord(e0, stream));
+    HIPCHK(launch_geom(g, pp, stream));
+    HIPCHK(hipEventRecord(e1, stream));
     st.launches++;
     HIPCHK(hipMemcpyAsync(b.h_res.data(), b.res, b.n_hist * sizeof(HistResult), hipMemcpyDeviceToHost, stream));
     HIPCHK(hipStreamSynchronize(stream));
-    (void)hipFree(d_over);
+#ifdef S2LC_GUARD
+    {
+      uint32_t gg[8];
+      HIPCHK(hipMemcpyFromSymbol(gg, HIP_SYMBOL(g_guard), sizeof gg));
+      if (gg[0]) {
+        err = "guard: " + std::to_string(gg[0]) + " violations, first at search_dev.h:" + std::to_string(gg[1]) +
+              " a=" + std::to_string(gg[2]) + " b=" + std::to_string(gg[3]);
+        return S2LC_EHIP;
+      }
+    }
+#endif
+    float ms = 0;
+    HIPCHK(hipEventElapsedTime(&ms, e0, e1));
+    st.kernel_ms += ms;
+    if (pass == 0) st.pass0_ms = ms;
+    // histories that outgrew this pass's frontier go to the next pass
+    std::vector<uint32_t> next;
+    for (uint32_t i = 0; i < b.n_hist; ++i)
+      if (!b.forced[i] && b.h_res[i].verdict == V_UNKNOWN && b.h_res[i].reason == S2LC_R_FRONTIER) next.push_back(i);
+    if (pass == 0) st.n_overflow = (uint32_t)next.size();
+    else st.n_overflow2 += (uint32_t)next.size();
+    todo.swap(next);
   }
+  if (d_list) (void)hipFree(d_list);
   if (witness && b.n_hist) {
     hipLaunchKernelGGL(walk_kernel, dim3((b.n_hist + 255) / 256), dim3(256), 0, stream, b.n_hist, b.res,
                        (const TraceEnt*)b.trace, b.moves);

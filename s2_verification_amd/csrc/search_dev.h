@@ -68,6 +68,7 @@ struct Params {
   uint8_t* slab;
   size_t slab_bytes;
   uint32_t fcap, chunk, ht_mask;
+  uint32_t stage_cap;  // staging entries (2 * chunk in HBM mode; may be smaller in LDS mode)
   TraceEnt* trace;
   unsigned long long* trace_head;
   uint64_t trace_cap;
@@ -114,7 +115,7 @@ __device__ __forceinline__ uint4 ld16(const OpRec* r, int off) {
 // One pass over a block of B chains: load every head (out_tail/out_hash,
 // sufmin/call/ret, flags) with independent loads, fold minret / bound, and
 // mark the heads that are identity ops, minimal under minret_prev and legal.
-template <int B>
+template <int B, int KMAX_CS>
 __device__ __forceinline__ uint32_t closure_block(const uint32_t* cb, int nq, int b, const uint32_t* cs,
                                                   const OpRec* __restrict__ recs, const State& s,
                                                   uint32_t minret_prev, bool p2, uint32_t& minret, uint64_t& bound,
@@ -123,8 +124,9 @@ __device__ __forceinline__ uint32_t closure_block(const uint32_t* cb, int nq, in
   uint32_t fl[B];
 #pragma unroll
   for (int q = 0; q < B; ++q) {
-    // unconditional: chains >= K have count 0 and a valid record (see s_cs)
-    uint32_t idx = cs[b + q] + (q < nq ? cb[q] : 0u);
+    // unconditional: chains >= K read the history's last sentinel (cs[KMAX],
+    // see the kernel's chain-start fill); their results are ignored
+    uint32_t idx = q < nq ? cs[b + q] + cb[q] : cs[KMAX_CS];
     DCHECK(q >= nq || idx < cs[b + q + 1], "closure chain %d idx %u end %u", b + q, idx, cs[b + q + 1]);
     if (!GUARD(q >= nq || idx < cs[b + q + 1], idx, cs[b + q + 1])) idx = cs[b + q];
     const OpRec* r = &recs[idx];
@@ -188,7 +190,7 @@ __device__ __forceinline__ int closure(Cfg<KMAX>* c, int K, const uint32_t* cs, 
         uint32_t cb[B];
 #pragma unroll
         for (int q = 0; q < B; ++q) cb[q] = ((b + q) & 1) ? (pk[(b + q) >> 1] >> 16) : (pk[(b + q) >> 1] & 0xFFFFu);
-        const uint32_t adv = closure_block<B>(cb, min(B, K - b), b, cs, recs, s, minret_prev, p2, minret, bound, dead);
+        const uint32_t adv = closure_block<B, KMAX>(cb, min(B, K - b), b, cs, recs, s, minret_prev, p2, minret, bound, dead);
         if (adv) {
           changed = true;
 #pragma unroll
@@ -201,7 +203,7 @@ __device__ __forceinline__ int closure(Cfg<KMAX>* c, int K, const uint32_t* cs, 
         const uint4 v = *reinterpret_cast<const uint4*>(&c->cnt[b]);
         uint32_t cb[B] = {v.x & 0xFFFFu, v.x >> 16, v.y & 0xFFFFu, v.y >> 16,
                           v.z & 0xFFFFu, v.z >> 16, v.w & 0xFFFFu, v.w >> 16};
-        const uint32_t adv = closure_block<B>(cb, min(B, K - b), b, cs, recs, s, minret_prev, p2, minret, bound, dead);
+        const uint32_t adv = closure_block<B, KMAX>(cb, min(B, K - b), b, cs, recs, s, minret_prev, p2, minret, bound, dead);
         if (adv) {
           changed = true;
           uint4 o;
@@ -264,51 +266,72 @@ __device__ __forceinline__ void cfg_copy(Cfg<KMAX>* d, const Cfg<KMAX>* s) {
   for (int q = 0; q < (int)(sizeof(Cfg<KMAX>) / 16); ++q) y[q] = x[q];
 }
 
-template <int KMAX, int BT>
+// Per-workgroup scalars, at the start of dynamic LDS (one 16-byte-aligned
+// object, so the configuration arrays that follow stay 16-byte aligned).
+template <int KMAX>
+struct __attribute__((aligned(16))) WgState {
+  uint32_t cs[KMAX + 1];  // chain starts; entries > K point at a sentinel
+  uint32_t h, nstage, nnext, found, overflow, children;
+  uint32_t found_parent, found_move, found_p4;
+  uint32_t tb, tleft, witness_ok;
+  unsigned long long tbase;
+  HistDesc hd;
+};
+
+// Dynamic LDS declaration (overridable only by the test-only CPU emulator).
+#ifndef S2LC_DYNAMIC_LDS
+#define S2LC_DYNAMIC_LDS(name) extern __shared__ __attribute__((aligned(16))) uint8_t name[]
+#endif
+
+template <int KMAX>
+constexpr size_t wg_state_bytes() { return (sizeof(WgState<KMAX>) + 15) & ~(size_t)15; }
+
+// SHARED = true: frontier A/B, staging and the dedupe table live in LDS right
+// after WgState (sized by the host: fcap / stage_cap / ht_mask); a history that
+// outgrows them is flagged S2LC_R_FRONTIER and re-run in HBM mode.
+// SHARED = false: the same arrays live in a per-workgroup HBM slab.
+template <int KMAX, int BT, bool SHARED>
 __global__ __launch_bounds__(BT) void search_kernel(Params p) {
   using C = Cfg<KMAX>;
-  __shared__ uint32_t s_cs[KMAX + 1];  // chain starts; entries > K point at a sentinel
-  __shared__ uint32_t s_h, s_nstage, s_nnext, s_found, s_overflow, s_children;
-  __shared__ uint32_t s_found_parent, s_found_move, s_found_p4;
-  __shared__ uint32_t s_tb, s_tleft, s_witness_ok;
-  __shared__ unsigned long long s_tbase;
-  __shared__ HistDesc s_hd;
+  S2LC_DYNAMIC_LDS(smem);
+  WgState<KMAX>& S = *reinterpret_cast<WgState<KMAX>*>(smem);
 
   const int tid = threadIdx.x;
-  uint8_t* slab = p.slab + (size_t)blockIdx.x * p.slab_bytes;
+  uint8_t* slab = SHARED ? smem + wg_state_bytes<KMAX>() : p.slab + (size_t)blockIdx.x * p.slab_bytes;
   C* const fa = reinterpret_cast<C*>(slab);
   C* const fb = fa + p.fcap;
   C* const stage = fb + p.fcap;
-  unsigned long long* const ht = reinterpret_cast<unsigned long long*>(stage + 2 * p.chunk);
+  unsigned long long* const ht = reinterpret_cast<unsigned long long*>(stage + p.stage_cap);
   const uint32_t mask = p.ht_mask;
 
   for (uint32_t i = tid; i <= mask; i += BT) ht[i] = HT_EMPTY;
-  if (tid == 0) { s_tleft = 0; s_tbase = 0; }
+  if (tid == 0) { S.tleft = 0; S.tbase = 0; }
   __syncthreads();
 
   for (;;) {
-    if (tid == 0) s_h = atomicAdd(p.counter, 1u);
+    if (tid == 0) S.h = atomicAdd(p.counter, 1u);
     __syncthreads();
-    const uint32_t hi = s_h;
+    const uint32_t hi = S.h;
     if (hi >= p.n_hist) break;
     uint32_t h = p.order[hi];
     if (!GUARD(h < p.n_res, h, hi)) h = 0;
-    if (tid == 0) s_hd = p.hist[h];
+    if (tid == 0) S.hd = p.hist[h];
     __syncthreads();
-    const HistDesc hd = s_hd;
+    const HistDesc hd = S.hd;
     const int K = hd.K;
     const int nw = (K + 7) >> 3;
     const OpRec* __restrict__ recs = p.recs;
-    // Chains >= K point at a valid record (the last sentinel) so that closure
-    // can load all KMAX heads unconditionally; their results are ignored.
+    // cs[0..K] are the chain starts (cs[K] = end); cs[K+1..KMAX] hold the index
+    // of the history's last sentinel, which closure loads for unused chain
+    // slots so that every head load is in bounds and unconditional.
     for (int j = tid; j <= KMAX; j += BT) {
-      const uint32_t last = p.chain_start[hd.cs_base + K];
-      s_cs[j] = j <= K ? p.chain_start[hd.cs_base + j] : (last > 0 ? last - 1 : 0);
+      const uint32_t end = p.chain_start[hd.cs_base + K];
+      S.cs[j] = j <= K ? p.chain_start[hd.cs_base + j] : (end > 0 ? end - 1 : 0);
     }
     if (tid == 0) {
-      s_found = 0; s_overflow = 0; s_children = 0;
-      s_witness_ok = p.witness;
-      s_found_parent = TRACE_NONE; s_found_move = TRACE_NONE; s_found_p4 = 0;
+      S.found = 0; S.overflow = 0; S.children = 0;
+      S.witness_ok = p.witness;
+      S.found_parent = TRACE_NONE; S.found_move = TRACE_NONE; S.found_p4 = 0;
     }
     __syncthreads();
 
@@ -319,19 +342,19 @@ __global__ __launch_bounds__(BT) void search_kernel(Params p) {
       for (int w = 0; w < KMAX / 8; ++w) reinterpret_cast<uint4*>(c->cnt)[w] = make_uint4(0, 0, 0, 0);
       c->tail = 0; c->hash = 0; c->tok = 0;
       c->ptrace = TRACE_NONE; c->move = TRACE_NONE; c->slot = 0;
-      const int r = closure<KMAX>(c, K, s_cs, recs, hd.flags, 0u);
-      if (r == CL_DEAD) s_nnext = 0;
-      else s_nnext = 1;
-      if (r >= CL_COMPLETE) { s_found = 1; s_found_p4 = (r == CL_P4); }
+      const int r = closure<KMAX>(c, K, S.cs, recs, hd.flags, 0u);
+      if (r == CL_DEAD) S.nnext = 0;
+      else S.nnext = 1;
+      if (r >= CL_COMPLETE) { S.found = 1; S.found_p4 = (r == CL_P4); }
       uint32_t t = TRACE_NONE;
-      if (s_witness_ok) {
-        if (s_tleft == 0) {
+      if (S.witness_ok) {
+        if (S.tleft == 0) {
           const unsigned long long b = atomicAdd(p.trace_head, (unsigned long long)TRACE_CHUNK);
-          if (b + TRACE_CHUNK <= p.trace_cap) { s_tbase = b; s_tleft = TRACE_CHUNK; }
-          else s_witness_ok = 0;
+          if (b + TRACE_CHUNK <= p.trace_cap) { S.tbase = b; S.tleft = TRACE_CHUNK; }
+          else S.witness_ok = 0;
         }
-        if (s_witness_ok) {
-          t = (uint32_t)s_tbase; s_tbase += 1; s_tleft -= 1;
+        if (S.witness_ok) {
+          t = (uint32_t)S.tbase; S.tbase += 1; S.tleft -= 1;
           if (GUARD((uint64_t)t < p.trace_cap, t, 0)) { p.trace[t].parent = TRACE_NONE; p.trace[t].move = TRACE_NONE; }
         }
       }
@@ -341,19 +364,19 @@ __global__ __launch_bounds__(BT) void search_kernel(Params p) {
 
     C* cur = fa;
     C* nxt = fb;
-    uint32_t ncur = s_nnext;
-    __syncthreads();  // every lane has read s_nnext before lane 0 resets it below
+    uint32_t ncur = S.nnext;
+    __syncthreads();  // every lane has read S.nnext before lane 0 resets it below
     uint64_t configs = ncur;
     uint32_t rounds = 0;
     uint32_t verdict = V_ILLEGAL, reason = S2LC_R_SEARCH_EXHAUSTED;
-    if (s_found) verdict = V_OK, reason = 0;
+    if (S.found) verdict = V_OK, reason = 0;
 
-    while (!s_found) {
+    while (!S.found) {
       if (ncur == 0) { verdict = V_ILLEGAL; reason = S2LC_R_SEARCH_EXHAUSTED; break; }
-      if (tid == 0) s_nnext = 0;
+      if (tid == 0) S.nnext = 0;
       const uint32_t total = ncur * (uint32_t)K;
       for (uint32_t base = 0; base < total; base += p.chunk) {
-        if (tid == 0) s_nstage = 0;
+        if (tid == 0) S.nstage = 0;
         __syncthreads();
         // ---- expand: one lane per (configuration, chain) -----------------
         const uint32_t lim = min(total, base + p.chunk);
@@ -362,9 +385,9 @@ __global__ __launch_bounds__(BT) void search_kernel(Params p) {
           const uint32_t j = it - i * (uint32_t)K;
           const C* pc = &cur[i];
           const uint32_t cj = (reinterpret_cast<const uint32_t*>(pc->cnt)[j >> 1] >> (16 * (j & 1))) & 0xFFFFu;
-          DCHECK(i < ncur && s_cs[j] + cj < s_cs[j + 1], "expand i %u ncur %u j %u cnt %u", i, ncur, j, cj);
-          if (!GUARD(i < ncur && s_cs[j] + cj < s_cs[j + 1] && s_cs[j + 1] <= p.n_recs, i * 65536u + j, cj)) continue;
-          const OpRec r = load_rec(&recs[s_cs[j] + cj]);
+          DCHECK(i < ncur && S.cs[j] + cj < S.cs[j + 1], "expand i %u ncur %u j %u cnt %u", i, ncur, j, cj);
+          if (!GUARD(i < ncur && S.cs[j] + cj < S.cs[j + 1] && S.cs[j + 1] <= p.n_recs, i * 65536u + j, cj)) continue;
+          const OpRec r = load_rec(&recs[S.cs[j] + cj]);
           if ((r.flags & (OPF_SENTINEL | OPF_CLS_E)) || r.call_ev >= pc->minret) continue;
           const State s{pc->tail, pc->hash, pc->tok};
           const bool g = append_guards_ok(r, s);
@@ -383,9 +406,8 @@ __global__ __launch_bounds__(BT) void search_kernel(Params p) {
 #pragma unroll
           for (int q = 0; q < 2; ++q) {
             if (q >= nk) break;
-            const uint32_t k = atomicAdd(&s_nstage, 1u);
-            DCHECK(k < 2 * p.chunk, "stage k %u", k);
-            if (!GUARD(k < 2 * p.chunk, k, 0)) break;
+            const uint32_t k = atomicAdd(&S.nstage, 1u);
+            if (k >= p.stage_cap) { S.overflow = 1; break; }  // LDS staging full: re-run in HBM mode
             C* ch = &stage[k];
             // child counts = parent counts with chain j advanced, built in
             // registers and written with the same 16-byte type used to read them
@@ -408,21 +430,21 @@ __global__ __launch_bounds__(BT) void search_kernel(Params p) {
             ch->tail = kids[q].tail; ch->hash = kids[q].hash; ch->tok = kids[q].tok;
             ch->ptrace = pc->trace;
             ch->move = moves[q];
-            const int cr = closure<KMAX>(ch, K, s_cs, recs, hd.flags, pc->minret);
+            const int cr = closure<KMAX>(ch, K, S.cs, recs, hd.flags, pc->minret);
             if (cr == CL_ALIVE) {
               ch->fp = fingerprint<KMAX>(ch, nw);
               ch->slot = 0;
             } else {
               ch->slot = SLOT_DEAD;
-              if (cr >= CL_COMPLETE && atomicCAS(&s_found, 0u, 1u) == 0u) {
-                s_found_parent = pc->trace; s_found_move = moves[q]; s_found_p4 = (cr == CL_P4);
+              if (cr >= CL_COMPLETE && atomicCAS(&S.found, 0u, 1u) == 0u) {
+                S.found_parent = pc->trace; S.found_move = moves[q]; S.found_p4 = (cr == CL_P4);
               }
             }
           }
-          if (nk) atomicAdd(&s_children, (uint32_t)nk);
+          if (nk) atomicAdd(&S.children, (uint32_t)nk);
         }
         __syncthreads();
-        const uint32_t ns = s_nstage;
+        const uint32_t ns = min(S.nstage, p.stage_cap);
         // ---- dedupe: 64-bit CAS open addressing, full-key compare on tag hit
         for (uint32_t k = tid; k < ns; k += BT) {
           C* ch = &stage[k];
@@ -436,8 +458,8 @@ __global__ __launch_bounds__(BT) void search_kernel(Params p) {
             if (prev == HT_EMPTY) { ch->slot = slot; break; }
             if ((uint32_t)(prev >> 32) == tag) {
               const uint32_t ref = (uint32_t)prev;
-              DCHECK((ref & STAGE_BIT) ? (ref & ~STAGE_BIT) < 2 * p.chunk : ref < p.fcap, "ht ref %x slot %u", ref, slot);
-              if (GUARD((ref & STAGE_BIT) ? (ref & ~STAGE_BIT) < 2 * p.chunk : ref < p.fcap, ref, slot)) {
+              DCHECK((ref & STAGE_BIT) ? (ref & ~STAGE_BIT) < p.stage_cap : ref < p.fcap, "ht ref %x slot %u", ref, slot);
+              if (GUARD((ref & STAGE_BIT) ? (ref & ~STAGE_BIT) < p.stage_cap : ref < p.fcap, ref, slot)) {
                 const C* o = (ref & STAGE_BIT) ? &stage[ref & ~STAGE_BIT] : &nxt[ref];
                 if (cfg_eq<KMAX>(o, ch, nw)) { ch->slot = SLOT_DEAD; break; }
               }
@@ -450,40 +472,40 @@ __global__ __launch_bounds__(BT) void search_kernel(Params p) {
         for (uint32_t k = tid; k < ns; k += BT) {
           C* ch = &stage[k];
           if (ch->slot == SLOT_DEAD) continue;
-          const uint32_t n = atomicAdd(&s_nnext, 1u);
+          const uint32_t n = atomicAdd(&S.nnext, 1u);
           if (n < p.fcap) {
             cfg_copy<KMAX>(&nxt[n], ch);
             if (GUARD(ch->slot <= mask, ch->slot, n))
               ht[ch->slot] = ((unsigned long long)(uint32_t)(ch->fp >> 32) << 32) | n;
           } else {
-            s_overflow = 1;
+            S.overflow = 1;
           }
         }
         __syncthreads();
-        if (s_found || s_overflow) break;
+        if (S.found || S.overflow) break;
       }
-      if (s_overflow) {
+      if (S.overflow) {
         for (uint32_t i = tid; i <= mask; i += BT) ht[i] = HT_EMPTY;
-        if (s_found) { verdict = V_OK; reason = 0; ++rounds; }
+        if (S.found) { verdict = V_OK; reason = 0; ++rounds; }
         else { verdict = V_UNKNOWN; reason = S2LC_R_FRONTIER; }
         __syncthreads();
         break;
       }
-      const uint32_t nn = min(s_nnext, p.fcap);
+      const uint32_t nn = min(S.nnext, p.fcap);
       if (tid == 0) {
-        s_tb = TRACE_NONE;
-        if (s_witness_ok) {
-          if (s_tleft < nn) {
+        S.tb = TRACE_NONE;
+        if (S.witness_ok) {
+          if (S.tleft < nn) {
             const unsigned long long want = max((unsigned long long)nn, (unsigned long long)TRACE_CHUNK);
             const unsigned long long b = atomicAdd(p.trace_head, want);
-            if (b + want <= p.trace_cap) { s_tbase = b; s_tleft = (uint32_t)want; }
-            else s_witness_ok = 0;
+            if (b + want <= p.trace_cap) { S.tbase = b; S.tleft = (uint32_t)want; }
+            else S.witness_ok = 0;
           }
-          if (s_witness_ok) { s_tb = (uint32_t)s_tbase; s_tbase += nn; s_tleft -= nn; }
+          if (S.witness_ok) { S.tb = (uint32_t)S.tbase; S.tbase += nn; S.tleft -= nn; }
         }
       }
       __syncthreads();
-      const uint32_t tb = s_tb;
+      const uint32_t tb = S.tb;
       for (uint32_t n = tid; n < nn; n += BT) {
         C* c = &nxt[n];
         DCHECK(c->slot <= mask && (tb == TRACE_NONE || tb + n < p.trace_cap), "clear slot %u tb %u n %u", c->slot, tb, n);
@@ -499,7 +521,7 @@ __global__ __launch_bounds__(BT) void search_kernel(Params p) {
       __syncthreads();
       configs += nn;
       ++rounds;
-      if (s_found) { verdict = V_OK; reason = 0; break; }
+      if (S.found) { verdict = V_OK; reason = 0; break; }
       if (p.max_configs && configs > p.max_configs) { verdict = V_UNKNOWN; reason = S2LC_R_BUDGET; break; }
       C* t = cur; cur = nxt; nxt = t;
       ncur = nn;
@@ -510,12 +532,12 @@ __global__ __launch_bounds__(BT) void search_kernel(Params p) {
       R.reason = reason;
       R.rounds = rounds;
       R.configs = configs;
-      R.children = s_children;
-      R.p4 = s_found_p4;
-      R.final_parent = (verdict == V_OK && s_witness_ok) ? s_found_parent : TRACE_NONE;
-      R.final_move = s_found_move;
+      R.children = S.children;
+      R.p4 = S.found_p4;
+      R.final_parent = (verdict == V_OK && S.witness_ok) ? S.found_parent : TRACE_NONE;
+      R.final_move = S.found_move;
       R.witness_len = 0;
-      R.has_witness = (verdict == V_OK && s_witness_ok) ? 2u : 0u;  // resolved by walk_kernel
+      R.has_witness = (verdict == V_OK && S.witness_ok) ? 2u : 0u;  // resolved by walk_kernel
     }
     __syncthreads();
   }

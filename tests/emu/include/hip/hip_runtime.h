@@ -32,10 +32,14 @@ struct dim3 {
 namespace emu {
 inline thread_local uint32_t tid_x = 0, bid_x = 0, bdim_x = 1;
 inline std::barrier<>* g_barrier = nullptr;
+inline uint8_t* g_dyn_lds = nullptr;
 struct Idx { uint32_t x; };
 template <typename K, typename... A>
-void launch(K kernel, dim3 grid, dim3 block, A... args) {
+void launch(K kernel, dim3 grid, dim3 block, size_t smem, A... args) {
+  std::vector<uint8_t> lds(smem + 16);
   for (uint32_t b = 0; b < grid.x; ++b) {
+    memset(lds.data(), 0xA5, lds.size());  // LDS is not zeroed between workgroups either
+    g_dyn_lds = (uint8_t*)(((uintptr_t)lds.data() + 15) & ~(uintptr_t)15);
     std::barrier<> bar(block.x);
     g_barrier = &bar;
     std::vector<std::thread> th;
@@ -100,4 +104,6 @@ inline hipError_t hipEventDestroy(hipEvent_t) { return hipSuccess; }
 inline hipError_t hipEventRecord(hipEvent_t, hipStream_t) { return hipSuccess; }
 inline hipError_t hipEventElapsedTime(float* ms, hipEvent_t, hipEvent_t) { *ms = 0.f; return hipSuccess; }
 inline hipError_t hipGetLastError() { return hipSuccess; }
-#define hipLaunchKernelGGL(kernel, grid, block, shmem, stream, ...) emu::launch(kernel, grid, block, __VA_ARGS__)
+#define hipLaunchKernelGGL(kernel, grid, block, shmem, stream, ...) emu::launch(kernel, grid, block, shmem, __VA_ARGS__)
+// dynamic LDS of the emulated workgroup
+#define S2LC_DYNAMIC_LDS(name) uint8_t* name = emu::g_dyn_lds
