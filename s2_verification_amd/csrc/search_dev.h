@@ -391,21 +391,25 @@ __global__ __launch_bounds__(BT) void search_kernel(Params p) {
           if ((r.flags & (OPF_SENTINEL | OPF_CLS_E)) || r.call_ev >= pc->minret) continue;
           const State s{pc->tail, pc->hash, pc->tok};
           const bool g = append_guards_ok(r, s);
-          State kids[2];
-          uint32_t moves[2];
-          int nk = 0;
           State opt{0, 0, 0};
           if (!GUARD((uint64_t)r.hash_off + r.hash_cnt <= p.n_pool, r.hash_off, r.hash_cnt)) continue;
           if (g) opt = append_opt(r, s, p.pool);
+          // children as two named slots (a runtime-indexed array would go to scratch)
+          bool take_opt, take_id;
           if (r.flags & OPF_CLS_D) {
-            if (g && opt.tail == r.out_tail) { kids[nk] = opt; moves[nk++] = j; }
+            take_opt = g && opt.tail == r.out_tail;
+            take_id = false;
           } else {  // indefinite: opt any time; identity only when it holds the minimal return
-            if (g) { kids[nk] = opt; moves[nk++] = j; }
-            if (r.ret_ev == pc->minret && !(g && state_eq(opt, s))) { kids[nk] = s; moves[nk++] = j | MOVE_IDENT; }
+            take_opt = g;
+            take_id = r.ret_ev == pc->minret && !(g && state_eq(opt, s));
           }
+          const int nk = (int)take_opt + (int)take_id;
 #pragma unroll
           for (int q = 0; q < 2; ++q) {
             if (q >= nk) break;
+            const bool is_opt = (q == 0) && take_opt;
+            const State kid = is_opt ? opt : s;
+            const uint32_t mv = is_opt ? j : (j | MOVE_IDENT);
             const uint32_t k = atomicAdd(&S.nstage, 1u);
             if (k >= p.stage_cap) { S.overflow = 1; break; }  // LDS staging full: re-run in HBM mode
             C* ch = &stage[k];
@@ -427,9 +431,9 @@ __global__ __launch_bounds__(BT) void search_kernel(Params p) {
               }
               dst[w] = v;
             }
-            ch->tail = kids[q].tail; ch->hash = kids[q].hash; ch->tok = kids[q].tok;
+            ch->tail = kid.tail; ch->hash = kid.hash; ch->tok = kid.tok;
             ch->ptrace = pc->trace;
-            ch->move = moves[q];
+            ch->move = mv;
             const int cr = closure<KMAX>(ch, K, S.cs, recs, hd.flags, pc->minret);
             if (cr == CL_ALIVE) {
               ch->fp = fingerprint<KMAX>(ch, nw);
@@ -437,7 +441,7 @@ __global__ __launch_bounds__(BT) void search_kernel(Params p) {
             } else {
               ch->slot = SLOT_DEAD;
               if (cr >= CL_COMPLETE && atomicCAS(&S.found, 0u, 1u) == 0u) {
-                S.found_parent = pc->trace; S.found_move = moves[q]; S.found_p4 = (cr == CL_P4);
+                S.found_parent = pc->trace; S.found_move = mv; S.found_p4 = (cr == CL_P4);
               }
             }
           }
