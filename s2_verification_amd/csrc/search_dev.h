@@ -335,120 +335,110 @@ __global__ __launch_bounds__(BT) void search_kernel(Params p) {
     }
     __syncthreads();
 
-    // ---- initial configuration: (∅, (0, 0, nil)) closed ------------------
-    if (tid == 0) {
-      C* c = &fa[0];
-#pragma unroll
-      for (int w = 0; w < KMAX / 8; ++w) reinterpret_cast<uint4*>(c->cnt)[w] = make_uint4(0, 0, 0, 0);
-      c->tail = 0; c->hash = 0; c->tok = 0;
-      c->ptrace = TRACE_NONE; c->move = TRACE_NONE; c->slot = 0;
-      const int r = closure<KMAX>(c, K, S.cs, recs, hd.flags, 0u);
-      if (r == CL_DEAD) S.nnext = 0;
-      else S.nnext = 1;
-      if (r >= CL_COMPLETE) { S.found = 1; S.found_p4 = (r == CL_P4); }
-      uint32_t t = TRACE_NONE;
-      if (S.witness_ok) {
-        if (S.tleft == 0) {
-          const unsigned long long b = atomicAdd(p.trace_head, (unsigned long long)TRACE_CHUNK);
-          if (b + TRACE_CHUNK <= p.trace_cap) { S.tbase = b; S.tleft = TRACE_CHUNK; }
-          else S.witness_ok = 0;
-        }
-        if (S.witness_ok) {
-          t = (uint32_t)S.tbase; S.tbase += 1; S.tleft -= 1;
-          if (GUARD((uint64_t)t < p.trace_cap, t, 0)) { p.trace[t].parent = TRACE_NONE; p.trace[t].move = TRACE_NONE; }
-        }
-      }
-      c->trace = t;
-    }
-    __syncthreads();
-
+    // Round 0 stages the initial configuration (∅, (0, 0, nil)) as its only
+    // "child"; every later round stages the children of the frontier. Each
+    // round then runs: close (one lane per staged child) -> dedupe -> compact.
     C* cur = fa;
     C* nxt = fb;
-    uint32_t ncur = S.nnext;
-    __syncthreads();  // every lane has read S.nnext before lane 0 resets it below
-    uint64_t configs = ncur;
+    uint32_t ncur = 0;
+    uint64_t configs = 0;
     uint32_t rounds = 0;
     uint32_t verdict = V_ILLEGAL, reason = S2LC_R_SEARCH_EXHAUSTED;
-    if (S.found) verdict = V_OK, reason = 0;
-
-    while (!S.found) {
-      if (ncur == 0) { verdict = V_ILLEGAL; reason = S2LC_R_SEARCH_EXHAUSTED; break; }
+    for (bool init = true;; init = false) {
+      if (!init && ncur == 0) { verdict = V_ILLEGAL; reason = S2LC_R_SEARCH_EXHAUSTED; break; }
       if (tid == 0) S.nnext = 0;
-      const uint32_t total = ncur * (uint32_t)K;
+      const uint32_t total = init ? 1u : ncur * (uint32_t)K;
       for (uint32_t base = 0; base < total; base += p.chunk) {
         if (tid == 0) S.nstage = 0;
         __syncthreads();
-        // ---- expand: one lane per (configuration, chain) -----------------
-        const uint32_t lim = min(total, base + p.chunk);
-        for (uint32_t it = base + tid; it < lim; it += BT) {
-          const uint32_t i = it / (uint32_t)K;
-          const uint32_t j = it - i * (uint32_t)K;
-          const C* pc = &cur[i];
-          const uint32_t cj = (reinterpret_cast<const uint32_t*>(pc->cnt)[j >> 1] >> (16 * (j & 1))) & 0xFFFFu;
-          DCHECK(i < ncur && S.cs[j] + cj < S.cs[j + 1], "expand i %u ncur %u j %u cnt %u", i, ncur, j, cj);
-          if (!GUARD(i < ncur && S.cs[j] + cj < S.cs[j + 1] && S.cs[j + 1] <= p.n_recs, i * 65536u + j, cj)) continue;
-          const OpRec r = load_rec(&recs[S.cs[j] + cj]);
-          if ((r.flags & (OPF_SENTINEL | OPF_CLS_E)) || r.call_ev >= pc->minret) continue;
-          const State s{pc->tail, pc->hash, pc->tok};
-          const bool g = append_guards_ok(r, s);
-          State opt{0, 0, 0};
-          if (!GUARD((uint64_t)r.hash_off + r.hash_cnt <= p.n_pool, r.hash_off, r.hash_cnt)) continue;
-          if (g) opt = append_opt(r, s, p.pool);
-          // children as two named slots (a runtime-indexed array would go to scratch)
-          bool take_opt, take_id;
-          if (r.flags & OPF_CLS_D) {
-            take_opt = g && opt.tail == r.out_tail;
-            take_id = false;
-          } else {  // indefinite: opt any time; identity only when it holds the minimal return
-            take_opt = g;
-            take_id = r.ret_ev == pc->minret && !(g && state_eq(opt, s));
+        // ---- expand: one lane per (configuration, chain); raw children ---
+        if (init) {
+          if (tid == 0) {
+            C* c = &stage[0];
+#pragma unroll
+            for (int w = 0; w < KMAX / 8; ++w) reinterpret_cast<uint4*>(c->cnt)[w] = make_uint4(0, 0, 0, 0);
+            c->tail = 0; c->hash = 0; c->tok = 0;
+            c->minret = 0;  // closure seed: a lower bound of the true minret
+            c->ptrace = TRACE_NONE; c->move = TRACE_NONE;
+            S.nstage = 1;
           }
-          const int nk = (int)take_opt + (int)take_id;
+        } else {
+          const uint32_t lim = min(total, base + p.chunk);
+          for (uint32_t it = base + tid; it < lim; it += BT) {
+            const uint32_t i = it / (uint32_t)K;
+            const uint32_t j = it - i * (uint32_t)K;
+            const C* pc = &cur[i];
+            const uint32_t cj = (reinterpret_cast<const uint32_t*>(pc->cnt)[j >> 1] >> (16 * (j & 1))) & 0xFFFFu;
+            DCHECK(i < ncur && S.cs[j] + cj < S.cs[j + 1], "expand i %u ncur %u j %u cnt %u", i, ncur, j, cj);
+            if (!GUARD(i < ncur && S.cs[j] + cj < S.cs[j + 1] && S.cs[j + 1] <= p.n_recs, i * 65536u + j, cj)) continue;
+            const OpRec r = load_rec(&recs[S.cs[j] + cj]);
+            if ((r.flags & (OPF_SENTINEL | OPF_CLS_E)) || r.call_ev >= pc->minret) continue;
+            const State s{pc->tail, pc->hash, pc->tok};
+            const bool g = append_guards_ok(r, s);
+            State opt{0, 0, 0};
+            if (!GUARD((uint64_t)r.hash_off + r.hash_cnt <= p.n_pool, r.hash_off, r.hash_cnt)) continue;
+            if (g) opt = append_opt(r, s, p.pool);
+            // children as two named slots (a runtime-indexed array would go to scratch)
+            bool take_opt, take_id;
+            if (r.flags & OPF_CLS_D) {
+              take_opt = g && opt.tail == r.out_tail;
+              take_id = false;
+            } else {  // indefinite: opt any time; identity only when it holds the minimal return
+              take_opt = g;
+              take_id = r.ret_ev == pc->minret && !(g && state_eq(opt, s));
+            }
+            const int nk = (int)take_opt + (int)take_id;
+            if (nk) atomicAdd(&S.children, (uint32_t)nk);
 #pragma unroll
-          for (int q = 0; q < 2; ++q) {
-            if (q >= nk) break;
-            const bool is_opt = (q == 0) && take_opt;
-            const State kid = is_opt ? opt : s;
-            const uint32_t mv = is_opt ? j : (j | MOVE_IDENT);
-            const uint32_t k = atomicAdd(&S.nstage, 1u);
-            if (k >= p.stage_cap) { S.overflow = 1; break; }  // LDS staging full: re-run in HBM mode
-            C* ch = &stage[k];
-            // child counts = parent counts with chain j advanced, built in
-            // registers and written with the same 16-byte type used to read them
-            const uint4* src = reinterpret_cast<const uint4*>(pc->cnt);
-            uint4* dst = reinterpret_cast<uint4*>(ch->cnt);
+            for (int q = 0; q < 2; ++q) {
+              if (q >= nk) break;
+              const bool is_opt = (q == 0) && take_opt;
+              const State kid = is_opt ? opt : s;
+              const uint32_t k = atomicAdd(&S.nstage, 1u);
+              if (k >= p.stage_cap) { S.overflow = 1; break; }  // staging full: re-run in a bigger pass
+              C* ch = &stage[k];
+              // child counts = parent counts with chain j advanced, built in
+              // registers and written with the same 16-byte type used to read them
+              const uint4* src = reinterpret_cast<const uint4*>(pc->cnt);
+              uint4* dst = reinterpret_cast<uint4*>(ch->cnt);
 #pragma unroll
-            for (int w = 0; w < KMAX / 8; ++w) {
-              uint4 v = src[w];
-              if ((int)(j >> 3) == w) {
-                const uint32_t inc = (j & 1) ? 0x10000u : 1u;
-                switch ((j >> 1) & 3) {
-                  case 0: v.x += inc; break;
-                  case 1: v.y += inc; break;
-                  case 2: v.z += inc; break;
-                  default: v.w += inc; break;
+              for (int w = 0; w < KMAX / 8; ++w) {
+                uint4 v = src[w];
+                if ((int)(j >> 3) == w) {
+                  const uint32_t inc = (j & 1) ? 0x10000u : 1u;
+                  switch ((j >> 1) & 3) {
+                    case 0: v.x += inc; break;
+                    case 1: v.y += inc; break;
+                    case 2: v.z += inc; break;
+                    default: v.w += inc; break;
+                  }
                 }
+                dst[w] = v;
               }
-              dst[w] = v;
-            }
-            ch->tail = kid.tail; ch->hash = kid.hash; ch->tok = kid.tok;
-            ch->ptrace = pc->trace;
-            ch->move = mv;
-            const int cr = closure<KMAX>(ch, K, S.cs, recs, hd.flags, pc->minret);
-            if (cr == CL_ALIVE) {
-              ch->fp = fingerprint<KMAX>(ch, nw);
-              ch->slot = 0;
-            } else {
-              ch->slot = SLOT_DEAD;
-              if (cr >= CL_COMPLETE && atomicCAS(&S.found, 0u, 1u) == 0u) {
-                S.found_parent = pc->trace; S.found_move = mv; S.found_p4 = (cr == CL_P4);
-              }
+              ch->tail = kid.tail; ch->hash = kid.hash; ch->tok = kid.tok;
+              ch->minret = pc->minret;  // closure seed
+              ch->ptrace = pc->trace;
+              ch->move = is_opt ? j : (j | MOVE_IDENT);
             }
           }
-          if (nk) atomicAdd(&S.children, (uint32_t)nk);
         }
         __syncthreads();
         const uint32_t ns = min(S.nstage, p.stage_cap);
+        // ---- close: one lane per staged child ------------------------------
+        for (uint32_t k = tid; k < ns; k += BT) {
+          C* ch = &stage[k];
+          const int cr = closure<KMAX>(ch, K, S.cs, recs, hd.flags, ch->minret);
+          if (cr == CL_ALIVE) {
+            ch->fp = fingerprint<KMAX>(ch, nw);
+            ch->slot = 0;
+          } else {
+            ch->slot = SLOT_DEAD;
+            if (cr >= CL_COMPLETE && atomicCAS(&S.found, 0u, 1u) == 0u) {
+              S.found_parent = ch->ptrace; S.found_move = ch->move; S.found_p4 = (cr == CL_P4);
+            }
+          }
+        }
+        __syncthreads();
         // ---- dedupe: 64-bit CAS open addressing, full-key compare on tag hit
         for (uint32_t k = tid; k < ns; k += BT) {
           C* ch = &stage[k];
@@ -490,7 +480,7 @@ __global__ __launch_bounds__(BT) void search_kernel(Params p) {
       }
       if (S.overflow) {
         for (uint32_t i = tid; i <= mask; i += BT) ht[i] = HT_EMPTY;
-        if (S.found) { verdict = V_OK; reason = 0; ++rounds; }
+        if (S.found) { verdict = V_OK; reason = 0; rounds += init ? 0u : 1u; }
         else { verdict = V_UNKNOWN; reason = S2LC_R_FRONTIER; }
         __syncthreads();
         break;
@@ -524,7 +514,7 @@ __global__ __launch_bounds__(BT) void search_kernel(Params p) {
       }
       __syncthreads();
       configs += nn;
-      ++rounds;
+      rounds += init ? 0u : 1u;
       if (S.found) { verdict = V_OK; reason = 0; break; }
       if (p.max_configs && configs > p.max_configs) { verdict = V_UNKNOWN; reason = S2LC_R_BUDGET; break; }
       C* t = cur; cur = nxt; nxt = t;
