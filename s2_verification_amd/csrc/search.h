@@ -51,6 +51,7 @@ struct SearchGeom {
   uint32_t chunk;      // expansion items per chunk
   uint32_t ht_slots;   // power of two
   uint32_t grid;       // workgroups
+  uint32_t win_recs;   // LDS record window (records; shared mode only)
   size_t cfg_bytes;
   size_t slab_bytes;   // HBM bytes per workgroup (0 when shared)
   size_t smem_bytes;   // dynamic LDS bytes per workgroup

@@ -17,6 +17,7 @@
 // (configuration, chain) candidate. Frontier, staging and table live in a
 // per-workgroup HBM slab (L2-resident at these sizes); chain offsets in LDS.
 #include <hip/hip_runtime.h>
+#include <stdio.h>
 #include <string.h>
 
 #include <algorithm>
@@ -77,7 +78,7 @@ size_t state_bytes(uint32_t kmax) {
 }
 
 SearchGeom make_geom(uint32_t kmax, bool shared, uint32_t block, uint32_t fcap, uint32_t stage_cap, uint32_t chunk,
-                     uint32_t grid) {
+                     uint32_t grid, size_t lds_budget) {
   SearchGeom g;
   g.block = block;
   g.kmax = kmax;
@@ -91,6 +92,15 @@ SearchGeom make_geom(uint32_t kmax, bool shared, uint32_t block, uint32_t fcap, 
   g.grid = grid;
   g.cfg_bytes = cfg_bytes(kmax);
   size_t arrays = (2 * (size_t)fcap + stage_cap) * g.cfg_bytes + (size_t)ht * 8;
+  g.win_recs = 0;
+  if (shared) {
+    // the rest of the per-workgroup LDS budget holds the record window
+    // (at most WIN_ITEMS 16-byte pieces per lane, i.e. 2 records per lane)
+    const size_t used = state_bytes(kmax) + arrays;
+    const size_t cap = (size_t)WIN_ITEMS * block / 4;
+    g.win_recs = used < lds_budget ? (uint32_t)std::min(cap, (lds_budget - used) / sizeof(OpRec)) : 0;
+    arrays += (size_t)g.win_recs * sizeof(OpRec);
+  }
   arrays = (arrays + 255) & ~(size_t)255;
   g.smem_bytes = state_bytes(kmax) + (shared ? arrays : 0);
   g.slab_bytes = shared ? 0 : arrays;
@@ -239,8 +249,12 @@ int batch_run(DevBatch& b, hipStream_t stream, uint64_t max_configs, bool witnes
   // Pass 0: LDS-resident search for every history (small frontier / staging).
   // Pass 1: HBM slab, 64 lanes, frontier 1024, for the ones that outgrew LDS.
   // Pass 2: HBM slab, 256 lanes, frontier up to 2^20.
-  const uint32_t lds_fcap = b.kmax <= 32 ? 16 : 8;
-  const uint32_t lds_stage = b.kmax <= 32 ? 64 : 32;
+  // Pass 0 sizing: one wave per workgroup; the LDS budget per workgroup is
+  // what the kernel's register occupancy allows (16 / 12 workgroups per CU for
+  // KMAX 16 / 32), so LDS never limits residency below the register limit.
+  const uint32_t lds_fcap = 8;
+  const uint32_t lds_stage = 32;
+  const size_t lds_budget = b.kmax <= 16 ? 10240 : b.kmax <= 32 ? 13312 : 0;
   std::vector<uint32_t> todo;  // histories for passes >= 1
   uint32_t* d_list = nullptr;
   for (int pass = 0; pass < 3; ++pass) {
@@ -248,18 +262,18 @@ int batch_run(DevBatch& b, hipStream_t stream, uint64_t max_configs, bool witnes
     if (n_pass == 0) break;
     SearchGeom g;
     if (pass == 0) {
-      g = make_geom(b.kmax, true, 64, lds_fcap, lds_stage, lds_stage, 1);
+      g = make_geom(b.kmax, true, 64, lds_fcap, lds_stage, lds_stage, 1, lds_budget);
       const uint32_t per_cu = std::max<uint32_t>(1, std::min<uint32_t>(16, (uint32_t)((160 * 1024) / g.smem_bytes)));
       g.grid = std::max<uint32_t>(1, std::min<uint32_t>(n_pass, (uint32_t)n_cu * per_cu));
     } else if (pass == 1) {
-      g = make_geom(b.kmax, false, 64, 1024, 512, 256, 1);
+      g = make_geom(b.kmax, false, 64, 1024, 512, 256, 1, 0);
       g.grid = std::max<uint32_t>(1, std::min<uint32_t>(n_pass, (uint32_t)n_cu * 16));
     } else {
       size_t free_b = 0, total_b = 0;
       HIPCHK(hipMemGetInfo(&free_b, &total_b));
       uint32_t fcap = 1u << 20;
-      g = make_geom(b.kmax, false, 256, fcap, 32768, 16384, 1);
-      while (g.slab_bytes > free_b / 2 && fcap > 4096) { fcap >>= 1; g = make_geom(b.kmax, false, 256, fcap, 32768, 16384, 1); }
+      g = make_geom(b.kmax, false, 256, fcap, 32768, 16384, 1, 0);
+      while (g.slab_bytes > free_b / 2 && fcap > 4096) { fcap >>= 1; g = make_geom(b.kmax, false, 256, fcap, 32768, 16384, 1, 0); }
       g.grid = (uint32_t)std::min<size_t>(n_pass, std::max<size_t>(1, (free_b / 2) / g.slab_bytes));
       g.grid = std::min<uint32_t>(g.grid, (uint32_t)n_cu);
     }
@@ -279,10 +293,17 @@ int batch_run(DevBatch& b, hipStream_t stream, uint64_t max_configs, bool witnes
     pp.slab = b.slab;
     pp.slab_bytes = g.slab_bytes;
     pp.fcap = g.fcap; pp.chunk = g.chunk; pp.stage_cap = g.stage_cap; pp.ht_mask = g.ht_slots - 1;
+    pp.win_recs = g.win_recs;
 #ifdef S2LC_GUARD
     {
       uint32_t z[8] = {0};
       HIPCHK(hipMemcpyToSymbol(HIP_SYMBOL(g_guard), z, sizeof z));
+    }
+#endif
+#ifdef S2LC_PROF
+    {
+      unsigned long long z[16] = {0};
+      HIPCHK(hipMemcpyToSymbol(HIP_SYMBOL(g_prof), z, sizeof z));
     }
 #endif
     HIPCHK(hipEventRecord(e0, stream));
@@ -304,6 +325,20 @@ int batch_run(DevBatch& b, hipStream_t stream, uint64_t max_configs, bool witnes
 #endif
     float ms = 0;
     HIPCHK(hipEventElapsedTime(&ms, e0, e1));
+#ifdef S2LC_PROF
+    {
+      unsigned long long gp[16];
+      HIPCHK(hipMemcpyFromSymbol(gp, HIP_SYMBOL(g_prof), sizeof gp));
+      const double rounds = gp[8] ? (double)gp[8] : 1.0;
+      fprintf(stderr,
+              "[s2lc prof] pass %d kmax %d hist %u ms %.3f rounds %llu | cycles/round setup %.0f expand %.0f close %.0f "
+              "dedupe %.0f compact %.0f finalize %.0f | closure passes/call %.2f calls/round %.2f | refills/round %.3f "
+              "win_recs %u smem %zu grid %u\n",
+              pass, g.kmax, n_pass, ms, gp[8], gp[0] / rounds, gp[1] / rounds, gp[2] / rounds, gp[3] / rounds,
+              gp[4] / rounds, gp[5] / rounds, gp[7] ? (double)gp[6] / gp[7] : 0.0, gp[7] / rounds, gp[9] / rounds,
+              g.win_recs, g.smem_bytes, g.grid);
+    }
+#endif
     st.kernel_ms += ms;
     if (pass == 0) st.pass0_ms = ms;
     // histories that outgrew this pass's frontier go to the next pass

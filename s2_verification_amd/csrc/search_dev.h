@@ -41,6 +41,29 @@ __device__ __forceinline__ bool guard_ok(bool cond, uint32_t line, uint32_t a, u
 #define GUARD(cond, a, b) true
 #endif
 
+// S2LC_PROF: diagnostic build. Lane 0 of every workgroup stamps clock64()
+// after each phase barrier and adds the per-phase cycles to g_prof (read back
+// and printed by the host); closure passes / calls are counted too.
+//   g_prof[0..5]: setup, expand, close, dedupe, compact, finalize (cycles)
+//   g_prof[6]: closure passes  g_prof[7]: closure calls  g_prof[8]: rounds
+//   g_prof[9]: record-window refills
+#ifdef S2LC_PROF
+__device__ unsigned long long g_prof[16];
+__shared__ uint32_t s_prof_cl[3];  // per-workgroup closure passes / calls / window refills
+#define PROF_DECL unsigned long long prof_t = clock64(), prof_acc[6] = {0, 0, 0, 0, 0, 0}; \
+  if (tid == 0) { s_prof_cl[0] = 0; s_prof_cl[1] = 0; s_prof_cl[2] = 0; }
+#define PROF_STAMP(i) do { if (tid == 0) { const unsigned long long t_ = clock64(); prof_acc[i] += t_ - prof_t; prof_t = t_; } } while (0)
+#define PROF_FLUSH() do { if (tid == 0) { for (int i_ = 0; i_ < 6; ++i_) { atomicAdd(&g_prof[i_], prof_acc[i_]); prof_acc[i_] = 0; } \
+  atomicAdd(&g_prof[6], (unsigned long long)s_prof_cl[0]); atomicAdd(&g_prof[7], (unsigned long long)s_prof_cl[1]); \
+  atomicAdd(&g_prof[9], (unsigned long long)s_prof_cl[2]); s_prof_cl[0] = 0; s_prof_cl[1] = 0; s_prof_cl[2] = 0; } } while (0)
+#define PROF_ADD(i, v) atomicAdd(&g_prof[i], (unsigned long long)(v))
+#else
+#define PROF_DECL do { } while (0)
+#define PROF_STAMP(i) do { } while (0)
+#define PROF_FLUSH() do { } while (0)
+#define PROF_ADD(i, v) do { } while (0)
+#endif
+
 template <int KMAX>
 struct __attribute__((aligned(16))) Cfg {
   uint64_t tail;
@@ -76,6 +99,7 @@ struct Params {
   uint64_t max_configs;
   uint32_t witness;
   uint32_t n_recs, n_pool, n_res;  // buffer sizes (guard build checks)
+  uint32_t win_recs;               // LDS record-window capacity (SHARED mode; 0 = none)
 };
 
 __device__ __forceinline__ uint64_t mix64(uint64_t x) {
@@ -112,12 +136,27 @@ __device__ __forceinline__ uint4 ld16(const OpRec* r, int off) {
   return *reinterpret_cast<const uint4*>(reinterpret_cast<const uint8_t*>(r) + off);
 }
 
+// Where a chain's records are read from. In LDS mode the workgroup keeps a
+// window of W records per chain (chain j's records wb[j] .. wb[j]+W-1, copied
+// from HBM by all lanes when the frontier nears the window's end); a record
+// outside the window is read from HBM. W = 0 disables the window.
+struct RecSrc {
+  const OpRec* __restrict__ recs;  // HBM, chain-major
+  const uint32_t* cs;              // LDS chain starts
+  const OpRec* win;                // LDS window, chain j at win[j * W]
+  const uint32_t* wb;              // LDS per-chain window base (count)
+  uint32_t W;
+  __device__ __forceinline__ const OpRec* at(int j, uint32_t c) const {
+    const uint32_t o = c - wb[j];
+    return o < W ? &win[j * W + o] : &recs[cs[j] + c];
+  }
+};
+
 // One pass over a block of B chains: load every head (out_tail/out_hash,
 // sufmin/call/ret, flags) with independent loads, fold minret / bound, and
 // mark the heads that are identity ops, minimal under minret_prev and legal.
 template <int B, int KMAX_CS>
-__device__ __forceinline__ uint32_t closure_block(const uint32_t* cb, int nq, int b, const uint32_t* cs,
-                                                  const OpRec* __restrict__ recs, const State& s,
+__device__ __forceinline__ uint32_t closure_block(const uint32_t* cb, int nq, int b, const RecSrc& src, const State& s,
                                                   uint32_t minret_prev, bool p2, uint32_t& minret, uint64_t& bound,
                                                   bool& dead) {
   uint4 obs[B], mid[B];
@@ -126,10 +165,10 @@ __device__ __forceinline__ uint32_t closure_block(const uint32_t* cb, int nq, in
   for (int q = 0; q < B; ++q) {
     // unconditional: chains >= K read the history's last sentinel (cs[KMAX],
     // see the kernel's chain-start fill); their results are ignored
-    uint32_t idx = q < nq ? cs[b + q] + cb[q] : cs[KMAX_CS];
-    DCHECK(q >= nq || idx < cs[b + q + 1], "closure chain %d idx %u end %u", b + q, idx, cs[b + q + 1]);
-    if (!GUARD(q >= nq || idx < cs[b + q + 1], idx, cs[b + q + 1])) idx = cs[b + q];
-    const OpRec* r = &recs[idx];
+    const uint32_t* cs = src.cs;
+    DCHECK(q >= nq || cs[b + q] + cb[q] < cs[b + q + 1], "closure chain %d cnt %u end %u", b + q, cb[q], cs[b + q + 1]);
+    const bool ok = q < nq && GUARD(cs[b + q] + cb[q] < cs[b + q + 1], cs[b + q] + cb[q], cs[b + q + 1]);
+    const OpRec* r = ok ? src.at(b + q, cb[q]) : &src.recs[cs[KMAX_CS]];
     obs[q] = ld16(r, 16);
     mid[q] = ld16(r, 32);
     fl[q] = r->flags;
@@ -158,8 +197,7 @@ __device__ __forceinline__ uint32_t closure_block(const uint32_t* cb, int nq, in
 }
 
 template <int KMAX>
-__device__ __forceinline__ int closure(Cfg<KMAX>* c, int K, const uint32_t* cs, const OpRec* __restrict__ recs, uint32_t hflags,
-                       uint32_t minret_seed) {
+__device__ __forceinline__ int closure(Cfg<KMAX>* c, int K, const RecSrc& src, uint32_t hflags, uint32_t minret_seed) {
   constexpr int B = 8;
   constexpr bool REG = KMAX <= 32;  // counts held in registers (packed u16 pairs)
   constexpr int NP = REG ? KMAX / 2 : 1;
@@ -179,7 +217,13 @@ __device__ __forceinline__ int closure(Cfg<KMAX>* c, int K, const uint32_t* cs, 
   uint32_t minret = EV_INF;
   uint64_t bound = REQ_NONE;
   int result = CL_ALIVE;
+#ifdef S2LC_PROF
+  uint32_t passes = 0;
+#endif
   for (;;) {
+#ifdef S2LC_PROF
+    ++passes;
+#endif
     minret = EV_INF;
     bound = REQ_NONE;
     bool changed = false, dead = false;
@@ -190,7 +234,7 @@ __device__ __forceinline__ int closure(Cfg<KMAX>* c, int K, const uint32_t* cs, 
         uint32_t cb[B];
 #pragma unroll
         for (int q = 0; q < B; ++q) cb[q] = ((b + q) & 1) ? (pk[(b + q) >> 1] >> 16) : (pk[(b + q) >> 1] & 0xFFFFu);
-        const uint32_t adv = closure_block<B, KMAX>(cb, min(B, K - b), b, cs, recs, s, minret_prev, p2, minret, bound, dead);
+        const uint32_t adv = closure_block<B, KMAX>(cb, min(B, K - b), b, src, s, minret_prev, p2, minret, bound, dead);
         if (adv) {
           changed = true;
 #pragma unroll
@@ -203,7 +247,7 @@ __device__ __forceinline__ int closure(Cfg<KMAX>* c, int K, const uint32_t* cs, 
         const uint4 v = *reinterpret_cast<const uint4*>(&c->cnt[b]);
         uint32_t cb[B] = {v.x & 0xFFFFu, v.x >> 16, v.y & 0xFFFFu, v.y >> 16,
                           v.z & 0xFFFFu, v.z >> 16, v.w & 0xFFFFu, v.w >> 16};
-        const uint32_t adv = closure_block<B, KMAX>(cb, min(B, K - b), b, cs, recs, s, minret_prev, p2, minret, bound, dead);
+        const uint32_t adv = closure_block<B, KMAX>(cb, min(B, K - b), b, src, s, minret_prev, p2, minret, bound, dead);
         if (adv) {
           changed = true;
           uint4 o;
@@ -231,6 +275,10 @@ __device__ __forceinline__ int closure(Cfg<KMAX>* c, int K, const uint32_t* cs, 
     for (int q = 0; q < KMAX / 8; ++q) w[q] = make_uint4(pk[4 * q], pk[4 * q + 1], pk[4 * q + 2], pk[4 * q + 3]);
   }
   c->minret = minret;
+#ifdef S2LC_PROF
+  atomicAdd(&s_prof_cl[0], passes);
+  atomicAdd(&s_prof_cl[1], 1u);
+#endif
   return result;
 }
 
@@ -271,6 +319,7 @@ __device__ __forceinline__ void cfg_copy(Cfg<KMAX>* d, const Cfg<KMAX>* s) {
 template <int KMAX>
 struct __attribute__((aligned(16))) WgState {
   uint32_t cs[KMAX + 1];  // chain starts; entries > K point at a sentinel
+  uint32_t wb[KMAX];      // record-window base (count) per chain
   uint32_t h, nstage, nnext, found, overflow, children;
   uint32_t found_parent, found_move, found_p4;
   uint32_t tb, tleft, witness_ok;
@@ -285,6 +334,70 @@ struct __attribute__((aligned(16))) WgState {
 
 template <int KMAX>
 constexpr size_t wg_state_bytes() { return (sizeof(WgState<KMAX>) + 15) & ~(size_t)15; }
+
+// 16-byte global -> LDS copy without a register round trip (overridable only by
+// the test-only CPU emulator).
+#ifndef S2LC_GLDS16
+#define S2LC_GLDS16(gsrc, lds_base) \
+  __builtin_amdgcn_global_load_lds((gsrc), (__attribute__((address_space(3))) void*)(lds_base), 16, 0, 0)
+#define S2LC_WAIT_ALL() __builtin_amdgcn_s_waitcnt(0)
+#endif
+
+// Record-window refill (LDS mode). Chain j's window
+// must start at or below every frontier configuration's count on j (counts only
+// grow, so every later configuration stays at or above it); it is re-based to
+// the frontier minimum when some configuration has come within a quarter
+// window of its end. All lanes copy, at most WIN_ITEMS 16-byte pieces each, by
+// LDS-DMA: every piece is in flight at once, so a refill costs one HBM latency.
+constexpr int WIN_ITEMS = 8;
+template <int KMAX, int BT>
+__device__ __noinline__ void window_refill(WgState<KMAX>& S, OpRec* win, const OpRec* __restrict__ recs,
+                                              const Cfg<KMAX>* cur, uint32_t ncur, int K, uint32_t W, bool init) {
+  const int tid = threadIdx.x;
+  bool flag = false;
+  uint32_t lo = 0;
+  if (tid < K) {
+    if (init) {
+      flag = true;
+    } else {
+      lo = 0xFFFFu;
+      uint32_t hi = 0;
+#pragma unroll 1
+      for (uint32_t i = 0; i < ncur; ++i) {
+        const uint32_t c = cur[i].cnt[tid];
+        lo = min(lo, c);
+        hi = max(hi, c);
+      }
+      flag = hi + (W >> 2) >= S.wb[tid] + W;
+    }
+  }
+  if (!__syncthreads_or(flag)) return;
+#ifdef S2LC_PROF
+  if (tid == 0) ++s_prof_cl[2];
+#endif
+  if (tid < K) S.wb[tid] = lo;
+  __syncthreads();
+  // LDS-DMA: lane l of a wave-instruction writes window bytes base + 16*l, so
+  // piece `it` lands at win + 16*it; the global source address is per lane.
+  const uint32_t per = W * 4, n = (uint32_t)K * per;
+  const uint4* __restrict__ src = reinterpret_cast<const uint4*>(recs);
+  uint4* w4 = reinterpret_cast<uint4*>(win);
+  // not unrolled: an LDS-DMA has no destination register, so iterations never wait
+#pragma unroll 1
+  for (int k = 0; k < WIN_ITEMS; ++k) {
+    const uint32_t base = k * BT;
+    if (base >= n) break;
+    const uint32_t it = base + tid;
+    if (it < n) {
+      const uint32_t j = it / per;
+      const uint32_t o = it - j * per;  // 16-byte piece within the chain's window
+      const uint32_t g = S.cs[j] + S.wb[j] + (o >> 2);
+      if (g < S.cs[j + 1]) S2LC_GLDS16(&src[4 * (size_t)g + (o & 3)], w4 + base);
+    }
+  }
+  S2LC_WAIT_ALL();
+  __syncthreads();
+}
 
 // SHARED = true: frontier A/B, staging and the dedupe table live in LDS right
 // after WgState (sized by the host: fcap / stage_cap / ht_mask); a history that
@@ -303,10 +416,12 @@ __global__ __launch_bounds__(BT) void search_kernel(Params p) {
   C* const stage = fb + p.fcap;
   unsigned long long* const ht = reinterpret_cast<unsigned long long*>(stage + p.stage_cap);
   const uint32_t mask = p.ht_mask;
+  OpRec* const win = SHARED ? reinterpret_cast<OpRec*>(ht + mask + 1) : nullptr;
 
   for (uint32_t i = tid; i <= mask; i += BT) ht[i] = HT_EMPTY;
   if (tid == 0) { S.tleft = 0; S.tbase = 0; }
   __syncthreads();
+  PROF_DECL;
 
   for (;;) {
     if (tid == 0) S.h = atomicAdd(p.counter, 1u);
@@ -327,13 +442,18 @@ __global__ __launch_bounds__(BT) void search_kernel(Params p) {
     for (int j = tid; j <= KMAX; j += BT) {
       const uint32_t end = p.chain_start[hd.cs_base + K];
       S.cs[j] = j <= K ? p.chain_start[hd.cs_base + j] : (end > 0 ? end - 1 : 0);
+      if (j < KMAX) S.wb[j] = 0;
     }
+    // record window: W records per chain (0 in HBM mode or when K is too large)
+    const uint32_t W = SHARED ? min(p.win_recs / (uint32_t)K, (uint32_t)(WIN_ITEMS * BT / 4) / (uint32_t)K) : 0u;
+    const RecSrc src{recs, S.cs, win, S.wb, W};
     if (tid == 0) {
       S.found = 0; S.overflow = 0; S.children = 0;
       S.witness_ok = p.witness;
       S.found_parent = TRACE_NONE; S.found_move = TRACE_NONE; S.found_p4 = 0;
     }
     __syncthreads();
+    PROF_STAMP(0);
 
     // Round 0 stages the initial configuration (∅, (0, 0, nil)) as its only
     // "child"; every later round stages the children of the frontier. Each
@@ -347,10 +467,12 @@ __global__ __launch_bounds__(BT) void search_kernel(Params p) {
     for (bool init = true;; init = false) {
       if (!init && ncur == 0) { verdict = V_ILLEGAL; reason = S2LC_R_SEARCH_EXHAUSTED; break; }
       if (tid == 0) S.nnext = 0;
+      if (SHARED && W) window_refill<KMAX, BT>(S, win, recs, cur, ncur, K, W, init);
       const uint32_t total = init ? 1u : ncur * (uint32_t)K;
       for (uint32_t base = 0; base < total; base += p.chunk) {
         if (tid == 0) S.nstage = 0;
         __syncthreads();
+        PROF_STAMP(5);
         // ---- expand: one lane per (configuration, chain); raw children ---
         if (init) {
           if (tid == 0) {
@@ -371,7 +493,7 @@ __global__ __launch_bounds__(BT) void search_kernel(Params p) {
             const uint32_t cj = (reinterpret_cast<const uint32_t*>(pc->cnt)[j >> 1] >> (16 * (j & 1))) & 0xFFFFu;
             DCHECK(i < ncur && S.cs[j] + cj < S.cs[j + 1], "expand i %u ncur %u j %u cnt %u", i, ncur, j, cj);
             if (!GUARD(i < ncur && S.cs[j] + cj < S.cs[j + 1] && S.cs[j + 1] <= p.n_recs, i * 65536u + j, cj)) continue;
-            const OpRec r = load_rec(&recs[S.cs[j] + cj]);
+            const OpRec r = load_rec(src.at(j, cj));
             if ((r.flags & (OPF_SENTINEL | OPF_CLS_E)) || r.call_ev >= pc->minret) continue;
             const State s{pc->tail, pc->hash, pc->tok};
             const bool g = append_guards_ok(r, s);
@@ -423,11 +545,12 @@ __global__ __launch_bounds__(BT) void search_kernel(Params p) {
           }
         }
         __syncthreads();
+        PROF_STAMP(1);
         const uint32_t ns = min(S.nstage, p.stage_cap);
         // ---- close: one lane per staged child ------------------------------
         for (uint32_t k = tid; k < ns; k += BT) {
           C* ch = &stage[k];
-          const int cr = closure<KMAX>(ch, K, S.cs, recs, hd.flags, ch->minret);
+          const int cr = closure<KMAX>(ch, K, src, hd.flags, ch->minret);
           if (cr == CL_ALIVE) {
             ch->fp = fingerprint<KMAX>(ch, nw);
             ch->slot = 0;
@@ -439,6 +562,7 @@ __global__ __launch_bounds__(BT) void search_kernel(Params p) {
           }
         }
         __syncthreads();
+        PROF_STAMP(2);
         // ---- dedupe: 64-bit CAS open addressing, full-key compare on tag hit
         for (uint32_t k = tid; k < ns; k += BT) {
           C* ch = &stage[k];
@@ -462,6 +586,7 @@ __global__ __launch_bounds__(BT) void search_kernel(Params p) {
           }
         }
         __syncthreads();
+        PROF_STAMP(3);
         // ---- compact survivors into the next frontier ---------------------
         for (uint32_t k = tid; k < ns; k += BT) {
           C* ch = &stage[k];
@@ -476,6 +601,7 @@ __global__ __launch_bounds__(BT) void search_kernel(Params p) {
           }
         }
         __syncthreads();
+        PROF_STAMP(4);
         if (S.found || S.overflow) break;
       }
       if (S.overflow) {
@@ -483,6 +609,7 @@ __global__ __launch_bounds__(BT) void search_kernel(Params p) {
         if (S.found) { verdict = V_OK; reason = 0; rounds += init ? 0u : 1u; }
         else { verdict = V_UNKNOWN; reason = S2LC_R_FRONTIER; }
         __syncthreads();
+        PROF_STAMP(5);
         break;
       }
       const uint32_t nn = min(S.nnext, p.fcap);
@@ -499,6 +626,7 @@ __global__ __launch_bounds__(BT) void search_kernel(Params p) {
         }
       }
       __syncthreads();
+      PROF_STAMP(5);
       const uint32_t tb = S.tb;
       for (uint32_t n = tid; n < nn; n += BT) {
         C* c = &nxt[n];
@@ -513,6 +641,7 @@ __global__ __launch_bounds__(BT) void search_kernel(Params p) {
         }
       }
       __syncthreads();
+      PROF_STAMP(5);
       configs += nn;
       rounds += init ? 0u : 1u;
       if (S.found) { verdict = V_OK; reason = 0; break; }
@@ -532,8 +661,11 @@ __global__ __launch_bounds__(BT) void search_kernel(Params p) {
       R.final_move = S.found_move;
       R.witness_len = 0;
       R.has_witness = (verdict == V_OK && S.witness_ok) ? 2u : 0u;  // resolved by walk_kernel
+      PROF_ADD(8, rounds);
     }
     __syncthreads();
+    PROF_STAMP(5);
+    PROF_FLUSH();
   }
 }
 

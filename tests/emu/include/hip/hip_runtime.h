@@ -55,6 +55,22 @@ void launch(K kernel, dim3 grid, dim3 block, size_t smem, A... args) {
 #define blockIdx (emu::Idx{emu::bid_x})
 #define blockDim (emu::Idx{emu::bdim_x})
 #define __syncthreads() emu::g_barrier->arrive_and_wait()
+namespace emu {
+inline std::atomic<int> g_or[2];
+inline thread_local int or_phase = 0;
+}  // namespace emu
+// barrier + OR-reduction of pred over the workgroup (two alternating slots;
+// lane 0 clears a slot after everyone has read it)
+inline int __syncthreads_or(int pred) {
+  const int ph = emu::or_phase;
+  emu::or_phase ^= 1;
+  if (pred) emu::g_or[ph].store(1);
+  emu::g_barrier->arrive_and_wait();
+  const int r = emu::g_or[ph].load();
+  emu::g_barrier->arrive_and_wait();
+  if (emu::tid_x == 0) emu::g_or[ph].store(0);
+  return r;
+}
 
 template <typename T> inline T min(T a, T b) { return b < a ? b : a; }
 template <typename T> inline T max(T a, T b) { return a < b ? b : a; }
@@ -105,5 +121,8 @@ inline hipError_t hipEventRecord(hipEvent_t, hipStream_t) { return hipSuccess; }
 inline hipError_t hipEventElapsedTime(float* ms, hipEvent_t, hipEvent_t) { *ms = 0.f; return hipSuccess; }
 inline hipError_t hipGetLastError() { return hipSuccess; }
 #define hipLaunchKernelGGL(kernel, grid, block, shmem, stream, ...) emu::launch(kernel, grid, block, shmem, __VA_ARGS__)
+// LDS-DMA: lane l writes 16 bytes at lds_base + 16*l
+#define S2LC_GLDS16(gsrc, lds_base) memcpy((uint8_t*)(lds_base) + 16 * emu::tid_x, (const void*)(gsrc), 16)
+#define S2LC_WAIT_ALL() do { } while (0)
 // dynamic LDS of the emulated workgroup
 #define S2LC_DYNAMIC_LDS(name) uint8_t* name = emu::g_dyn_lds
