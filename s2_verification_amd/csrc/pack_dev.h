@@ -1,0 +1,325 @@
+// pack_dev.h — the packed small-frontier search (included by search.hip after
+// search_dev.h).
+//
+// Most histories of a DST batch have a tiny frontier (C4: at most 1
+// configuration in 93 % of histories, at most 4 in 99.8 %), so a workgroup- or
+// wave-per-history kernel leaves 60+ of 64 lanes idle and is VALU-issue bound
+// (round-1 PROF build: ~38k cycles per round, 64 % of them in a one-lane
+// closure). Here a GROUP of L lanes (L = 16 or 32, a power of two >= K) owns
+// one history, so a wave checks 64/L histories at once, and inside a group
+// lane l owns chain l:
+//   - expand: lane l tries the head of chain l as the next non-identity op
+//     (the candidates of porcupine's checkSingle loop, upstream checker.go),
+//     folding the record hashes (main.go:227-244) only when the tail matches;
+//   - closure: every pass is one head load per lane plus a group min-reduce of
+//     the heads' return events (minret) and required tails (P1 bound); legal
+//     minimal identity ops advance in parallel (rule 1);
+//   - children are consumed one at a time straight from the producing lane
+//     (shuffles), closed by the whole group and deduplicated against the next
+//     frontier (at most F configurations in LDS) by a lane-parallel compare.
+// A history whose frontier outgrows F is flagged S2LC_R_FRONTIER and re-run by
+// search_kernel's HBM-slab passes. Each lane caches the record at its chain's
+// last count in registers, so a chain that did not move costs no load.
+//
+// All control flow that reaches a cross-lane operation is uniform within a
+// group (lanes l >= K take part with a null chain), so ballots and shuffles
+// never read a disabled lane. Groups of one wave diverge freely.
+#pragma once
+
+namespace s2lc {
+namespace {
+
+constexpr int PACK_F = 8;       // frontier capacity per group (configurations)
+constexpr int PACK_BLOCK = 256; // threads per workgroup
+
+template <int L>
+struct __attribute__((aligned(8))) PCfg {
+  uint64_t tail;
+  uint64_t hash;
+  uint32_t tok;
+  uint32_t minret;  // exact minret of the closed configuration
+  uint32_t trace;   // own trace index
+  uint32_t ptrace;  // parent's trace index
+  uint32_t move;    // move that produced it
+  uint32_t _pad;
+  uint16_t cnt[L];
+};
+
+template <int L>
+constexpr size_t pack_group_bytes() { return 2 * PACK_F * sizeof(PCfg<L>); }
+
+template <int L>
+constexpr size_t pack_smem_bytes() { return (PACK_BLOCK / L) * pack_group_bytes<L>(); }
+
+// LDS accesses of one wave execute in program order; this keeps the compiler
+// from reordering them across lanes (a store by lane a, a load by lane b).
+__device__ __forceinline__ void wave_lds_sync() {
+  __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+}
+
+template <int L>
+__device__ __forceinline__ uint32_t gmin_u32(uint32_t v) {
+#pragma unroll
+  for (int o = L / 2; o > 0; o >>= 1) v = min(v, (uint32_t)__shfl_xor((int)v, o, L));
+  return v;
+}
+
+template <int L>
+__device__ __forceinline__ uint64_t gmin_u64(uint64_t v) {
+#pragma unroll
+  for (int o = L / 2; o > 0; o >>= 1) {
+    const uint32_t lo = (uint32_t)__shfl_xor((int)(uint32_t)v, o, L);
+    const uint32_t hi = (uint32_t)__shfl_xor((int)(uint32_t)(v >> 32), o, L);
+    const uint64_t w = ((uint64_t)hi << 32) | lo;
+    v = w < v ? w : v;
+  }
+  return v;
+}
+
+__device__ __forceinline__ uint32_t bcast_u32(uint32_t v, int src) { return (uint32_t)__shfl((int)v, src, 64); }
+__device__ __forceinline__ uint64_t bcast_u64(uint64_t v, int src) {
+  return ((uint64_t)bcast_u32((uint32_t)(v >> 32), src) << 32) | bcast_u32((uint32_t)v, src);
+}
+
+// Per-lane view of chain l of the group's history, with a one-record cache.
+struct ChainLane {
+  const OpRec* __restrict__ base;  // first record of chain l (valid iff on)
+  bool on;                         // l < K
+  uint32_t cc;                     // count of the cached record
+  OpRec r;                         // cached record (null record when !on)
+  __device__ __forceinline__ void reset(const OpRec* b, bool on_) {
+    base = b;
+    on = on_;
+    cc = 0xFFFFFFFFu;
+    r.num_records = 0; r.msn = 0; r.out_tail = 0; r.out_hash = 0;
+    r.sufmin = REQ_NONE; r.call_ev = EV_INF; r.ret_ev = EV_INF;
+    r.hash_off = 0; r.hash_cnt = 0; r.batch_tok = 0; r.set_tok = 0;
+    r.flags = OPF_SENTINEL;
+  }
+  __device__ __forceinline__ void at(uint32_t c) {
+    if (on && c != cc) {
+      r = load_rec(base + c);
+      cc = c;
+    }
+  }
+};
+
+// Group closure of one configuration (state s, lane count cnt) under minimal,
+// legal identity ops + P1/P2/P4; returns CL_* and the exact minret.
+template <int L>
+__device__ __forceinline__ int pack_closure(ChainLane& ch, uint32_t& cnt, const State& s, uint32_t hflags,
+                                            uint64_t gmask, uint32_t& minret_out) {
+  const bool nowrap = hflags & H_NOWRAP;
+  const bool p2 = hflags & H_P2OK;
+  for (;;) {
+    ch.at(cnt);
+    const OpRec& r = ch.r;
+    const uint32_t minret = gmin_u32<L>(r.ret_ev);
+    const uint64_t bound = gmin_u64<L>(r.sufmin);
+    const uint32_t f = r.flags;
+    const bool minimal_e = (f & OPF_CLS_E) && r.call_ev < minret;
+    bool legal = false, dead = false;
+    if (minimal_e) {
+      legal = true;
+      if ((f & OPF_KIND_MASK) != 0) {
+        const bool hash_bad = (f & OPF_HAS_HASH) && s.hash != r.out_hash;
+        const bool tail_bad = !(f & OPF_FAIL) && s.tail != r.out_tail;
+        legal = !hash_bad && !tail_bad;
+        // P2: a minimal successful read at this tail with another hash can never pass
+        dead = p2 && hash_bad && !(f & OPF_FAIL) && r.out_tail == s.tail;
+      }
+    }
+    minret_out = minret;
+    if ((__ballot(dead) & gmask) || (nowrap && s.tail > bound)) return CL_DEAD;
+    if (!(__ballot(legal) & gmask)) {
+      if (minret == EV_INF) return CL_COMPLETE;
+      return bound == REQ_NONE ? CL_P4 : CL_ALIVE;
+    }
+    cnt += legal ? 1u : 0u;
+  }
+}
+
+template <int L>
+__global__ __launch_bounds__(PACK_BLOCK) void pack_kernel(Params p) {
+  using C = PCfg<L>;
+  S2LC_DYNAMIC_LDS(smem);
+  const int lane = (int)(threadIdx.x & 63);
+  const int gl = lane & (L - 1);           // lane within the group = chain index
+  const int gbase = lane & ~(L - 1);       // first wave lane of the group
+  const uint64_t gmask = (L == 64 ? ~0ull : ((1ull << L) - 1)) << gbase;
+  C* const fr = reinterpret_cast<C*>(smem + (threadIdx.x / L) * pack_group_bytes<L>());
+
+  uint32_t tbase = 0, tleft = 0;  // group's trace chunk (uniform)
+  for (;;) {
+    uint32_t hi = 0;
+    if (gl == 0) hi = atomicAdd(p.counter, 1u);
+    hi = bcast_u32(hi, gbase);
+    if (hi >= p.n_hist) break;
+    const uint32_t h = p.order[hi];
+    const HistDesc hd = p.hist[h];
+    const int K = hd.K;
+    const bool on = gl < K;
+    const uint32_t cs = on ? p.chain_start[hd.cs_base + gl] : 0u;
+    ChainLane ch;
+    ch.reset(p.recs + cs, on);
+    bool witness_ok = p.witness != 0;
+
+    uint32_t verdict = V_ILLEGAL, reason = S2LC_R_SEARCH_EXHAUSTED;
+    uint32_t found_parent = TRACE_NONE, found_move = TRACE_NONE, found_p4 = 0;
+    uint64_t configs = 0, children = 0;
+    uint32_t rounds = 0;
+    int cur = 0;  // frontier parity: fr[cur*F ..] current, fr[(1-cur)*F ..] next
+    uint32_t nf = 0;
+
+    // ---- round 0: the initial configuration (∅, (0, 0, nil)) -------------
+    {
+      uint32_t cnt = 0, mr = 0;
+      const State s0{0, 0, 0};
+      const int cr = pack_closure<L>(ch, cnt, s0, hd.flags, gmask, mr);
+      if (cr == CL_DEAD) {
+        nf = 0;
+      } else if (cr != CL_ALIVE) {
+        verdict = V_OK; reason = 0; found_p4 = cr == CL_P4;
+        nf = 0xFFFFFFFFu;  // done
+      } else {
+        C& c = fr[0];
+        if (gl == 0) {
+          c.tail = 0; c.hash = 0; c.tok = 0; c.minret = mr;
+          c.trace = TRACE_NONE; c.ptrace = TRACE_NONE; c.move = TRACE_NONE;
+        }
+        if (gl < L) c.cnt[gl] = on ? (uint16_t)cnt : 0;
+        nf = 1;
+        configs = 1;
+      }
+      wave_lds_sync();
+    }
+
+    // ---- rounds: each linearizes one durable / indefinite append ----------
+    while (nf != 0 && nf != 0xFFFFFFFFu) {
+      C* const curf = fr + cur * PACK_F;
+      C* const nxt = fr + (1 - cur) * PACK_F;
+      uint32_t nn = 0;
+      bool found = false, overflow = false;
+      for (uint32_t f = 0; f < nf && !found && !overflow; ++f) {
+        const C& pc = curf[f];
+        const State s{pc.tail, pc.hash, pc.tok};
+        const uint32_t pmin = pc.minret;
+        const uint32_t ptrace = pc.trace;
+        const uint32_t pcnt = on ? pc.cnt[gl] : 0u;
+        // expand: lane l tries the head of chain l
+        ch.at(pcnt);
+        const OpRec& r = ch.r;
+        const bool cand = on && !(r.flags & (OPF_SENTINEL | OPF_CLS_E)) && r.call_ev < pmin;
+        bool take_opt = false, take_id = false;
+        State opt = s;
+        if (cand) {
+          const bool g = append_guards_ok(r, s);
+          opt.tail = s.tail + r.num_records;
+          opt.tok = r.set_tok ? r.set_tok : s.tok;
+          if (r.flags & OPF_CLS_D) {
+            take_opt = g && opt.tail == r.out_tail;
+          } else {
+            take_opt = g;
+          }
+          if (take_opt) {
+            uint64_t hsh = s.hash;
+            const uint64_t* __restrict__ hp = p.pool + r.hash_off;
+            for (uint32_t i = 0; i < r.hash_cnt; ++i) hsh = chain_hash(hsh, hp[i]);
+            opt.hash = hsh;
+          }
+          if (r.flags & OPF_CLS_I) take_id = r.ret_ev == pmin && !(g && state_eq(opt, s));
+        }
+        uint64_t mo = __ballot(take_opt) & gmask;
+        uint64_t mi = __ballot(take_id) & gmask;
+        children += __popcll(mo) + __popcll(mi);
+        // consume the children one at a time: close, dedupe, insert
+        while ((mo | mi) && !found && !overflow) {
+          const bool is_id = mo == 0;
+          const uint64_t m = is_id ? mi : mo;
+          const int src = __ffsll((unsigned long long)m) - 1;
+          if (is_id) mi &= mi - 1; else mo &= mo - 1;
+          const int j = src - gbase;
+          State ks;
+          ks.tail = bcast_u64(is_id ? s.tail : opt.tail, src);
+          ks.hash = bcast_u64(is_id ? s.hash : opt.hash, src);
+          ks.tok = bcast_u32(is_id ? s.tok : opt.tok, src);
+          uint32_t cnt = pcnt + (gl == j ? 1u : 0u);
+          uint32_t mr = 0;
+          const int cr = pack_closure<L>(ch, cnt, ks, hd.flags, gmask, mr);
+          const uint32_t mv = is_id ? ((uint32_t)j | MOVE_IDENT) : (uint32_t)j;
+          if (cr == CL_COMPLETE || cr == CL_P4) {
+            found = true;
+            found_parent = ptrace; found_move = mv; found_p4 = cr == CL_P4;
+            break;
+          }
+          if (cr == CL_DEAD) continue;
+          // dedupe against the next frontier
+          bool dup = false;
+          for (uint32_t e = 0; e < nn; ++e) {
+            const C& o = nxt[e];
+            if (o.tail != ks.tail || o.hash != ks.hash || o.tok != ks.tok) continue;
+            const bool ne = on && o.cnt[gl] != (uint16_t)cnt;
+            if (!(__ballot(ne) & gmask)) { dup = true; break; }
+          }
+          if (dup) continue;
+          if (nn == PACK_F) { overflow = true; break; }
+          C& o = nxt[nn];
+          if (gl == 0) {
+            o.tail = ks.tail; o.hash = ks.hash; o.tok = ks.tok; o.minret = mr;
+            o.ptrace = ptrace; o.move = mv;
+          }
+          o.cnt[gl] = on ? (uint16_t)cnt : 0;
+          wave_lds_sync();
+          ++nn;
+        }
+      }
+      if (found) { verdict = V_OK; reason = 0; rounds++; break; }
+      if (overflow) { verdict = V_UNKNOWN; reason = S2LC_R_FRONTIER; break; }
+      rounds++;
+      if (nn == 0) { verdict = V_ILLEGAL; reason = S2LC_R_SEARCH_EXHAUSTED; break; }
+      // trace entries (parent, move) of the surviving configurations
+      uint32_t tb = TRACE_NONE;
+      if (witness_ok) {
+        if (tleft < nn) {
+          unsigned long long b = 0;
+          if (gl == 0) b = atomicAdd(p.trace_head, (unsigned long long)TRACE_CHUNK);
+          b = bcast_u64(b, gbase);
+          if (b + TRACE_CHUNK <= p.trace_cap) { tbase = (uint32_t)b; tleft = TRACE_CHUNK; }
+          else { witness_ok = false; tleft = 0; }
+        }
+        if (witness_ok) { tb = tbase; tbase += nn; tleft -= nn; }
+      }
+      if ((uint32_t)gl < nn) {
+        C& o = nxt[gl];
+        if (tb != TRACE_NONE) {
+          o.trace = tb + gl;
+          p.trace[tb + gl] = TraceEnt{o.ptrace, o.move};
+        } else {
+          o.trace = TRACE_NONE;
+        }
+      }
+      wave_lds_sync();
+      configs += nn;
+      if (p.max_configs && configs > p.max_configs) { verdict = V_UNKNOWN; reason = S2LC_R_BUDGET; break; }
+      cur = 1 - cur;
+      nf = nn;
+    }
+    if (gl == 0) {
+      HistResult& R = p.res[h];
+      R.verdict = verdict;
+      R.reason = reason;
+      R.rounds = rounds;
+      R.configs = configs;
+      R.children = children;
+      R.p4 = found_p4;
+      R.final_parent = (verdict == V_OK && witness_ok) ? found_parent : TRACE_NONE;
+      R.final_move = found_move;
+      R.witness_len = 0;
+      R.has_witness = (verdict == V_OK && witness_ok) ? 2u : 0u;  // resolved by walk_kernel
+    }
+  }
+}
+
+}  // namespace
+}  // namespace s2lc

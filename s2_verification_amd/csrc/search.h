@@ -66,7 +66,9 @@ struct DevBatch {
   uint64_t* pool = nullptr;
   uint32_t* chain_start = nullptr;
   HistDesc* hist = nullptr;
-  uint32_t* order = nullptr;        // LPT processing order
+  uint32_t* order = nullptr;        // LPT processing order: [K<=16 | K<=32 | rest]
+  uint32_t n_pack16 = 0, n_pack32 = 0;
+  std::vector<uint32_t> h_rest;     // histories searched one per workgroup (K > 32)
   HistResult* res = nullptr;
   uint32_t* moves = nullptr;        // witness moves (per history at witness_off)
   uint32_t* counter = nullptr;      // work counters (scheduling)
@@ -92,6 +94,7 @@ struct RunStats {
   uint64_t configs = 0, children = 0, rounds = 0;
   uint64_t algo_bytes = 0;
   uint32_t n_overflow = 0, launches = 0;
+  double pack_ms = 0;
 };
 
 int batch_upload(DevBatch& b, const std::vector<const History*>& hs, std::string& err);

@@ -18,6 +18,7 @@
 // per-workgroup HBM slab (L2-resident at these sizes); chain offsets in LDS.
 #include <hip/hip_runtime.h>
 #include <stdio.h>
+#include <stdlib.h>
 #include <string.h>
 
 #include <algorithm>
@@ -28,6 +29,7 @@
 #include "s2lincheck.h"
 #include "search.h"
 #include "search_dev.h"
+#include "pack_dev.h"
 
 namespace s2lc {
 
@@ -165,7 +167,8 @@ int batch_upload(DevBatch& b, const std::vector<const History*>& hs, std::string
     std::copy(h.pool.begin(), h.pool.end(), pool.begin() + pp);
     pp += h.pool.size();
   }
-  // longest-first processing order (LPT): work ~ ops x chains
+  // longest-first processing order (LPT): work ~ ops x chains; split into the
+  // packed-group lists (K <= 16, K <= 32) and the rest (workgroup per history)
   std::vector<uint32_t> order;
   order.reserve(hs.size());
   for (uint32_t i = 0; i < hs.size(); ++i)
@@ -173,6 +176,19 @@ int batch_upload(DevBatch& b, const std::vector<const History*>& hs, std::string
   std::stable_sort(order.begin(), order.end(), [&](uint32_t x, uint32_t y) {
     return (uint64_t)b.h_hist[x].n_ops * b.h_hist[x].K > (uint64_t)b.h_hist[y].n_ops * b.h_hist[y].K;
   });
+  {
+    std::vector<uint32_t> l16, l32, rest;
+    for (uint32_t i : order) {
+      const uint32_t K = b.h_hist[i].K;
+      (K <= 16 ? l16 : K <= 32 ? l32 : rest).push_back(i);
+    }
+    b.n_pack16 = (uint32_t)l16.size();
+    b.n_pack32 = (uint32_t)l32.size();
+    b.h_rest = rest;
+    order = l16;
+    order.insert(order.end(), l32.begin(), l32.end());
+    order.insert(order.end(), rest.begin(), rest.end());
+  }
   b.moves_cap = moves_total;
   b.n_recs = (uint32_t)recs.size();
   b.n_pool = (uint32_t)pool.size();
@@ -217,7 +233,6 @@ static int ensure(void** p, size_t& cap, size_t need, std::string& err) {
 int batch_run(DevBatch& b, hipStream_t stream, uint64_t max_configs, bool witness, RunStats& st, std::string& err) {
   st = RunStats{};
   auto t0 = std::chrono::steady_clock::now();
-  const uint32_t n_search = (uint32_t)std::count(b.forced.begin(), b.forced.end(), 0u);
   int dev = 0;
   HIPCHK(hipGetDevice(&dev));
   int n_cu = 256;
@@ -246,19 +261,65 @@ int batch_run(DevBatch& b, hipStream_t stream, uint64_t max_configs, bool witnes
   HIPCHK(hipMemsetAsync(b.counter, 0, 16 * sizeof(uint32_t), stream));
   HIPCHK(hipMemsetAsync(b.trace_head, 0, sizeof(unsigned long long), stream));
 
-  // Pass 0: LDS-resident search for every history (small frontier / staging).
+  // Packed passes: one L-lane group per history (K <= 16: L = 16, K <= 32:
+  // L = 32), frontier <= PACK_F. Histories that outgrow that frontier, and
+  // those with K > 32, go on to the workgroup-per-history passes:
+  // Pass 0: LDS-resident search (small frontier / staging).
   // Pass 1: HBM slab, 64 lanes, frontier 1024, for the ones that outgrew LDS.
   // Pass 2: HBM slab, 256 lanes, frontier up to 2^20.
   // Pass 0 sizing: one wave per workgroup; the LDS budget per workgroup is
   // what the kernel's register occupancy allows (16 / 12 workgroups per CU for
   // KMAX 16 / 32), so LDS never limits residency below the register limit.
+  const bool use_pack = getenv("S2LC_NO_PACK") == nullptr;
+  std::vector<uint32_t> todo;  // histories for the workgroup-per-history passes
+  if (use_pack) {
+    for (int li = 0; li < 2; ++li) {
+      const uint32_t n_l = li == 0 ? b.n_pack16 : b.n_pack32;
+      if (n_l == 0) continue;
+      Params pp = prm;
+      pp.order = b.order + (li == 0 ? 0 : b.n_pack16);
+      pp.n_hist = n_l;
+      pp.counter = b.counter + 12 + li;
+      const uint32_t L = li == 0 ? 16 : 32;
+      const size_t smem = li == 0 ? pack_smem_bytes<16>() : pack_smem_bytes<32>();
+      int bpc = 1;
+      if (li == 0) HIPCHK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&bpc, pack_kernel<16>, PACK_BLOCK, smem));
+      else HIPCHK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&bpc, pack_kernel<32>, PACK_BLOCK, smem));
+      const uint32_t groups = PACK_BLOCK / L;
+      const uint32_t grid = std::max<uint32_t>(
+          1, std::min<uint32_t>((n_l + groups - 1) / groups, (uint32_t)n_cu * (uint32_t)std::max(1, bpc)));
+      HIPCHK(hipEventRecord(e0, stream));
+      if (li == 0) hipLaunchKernelGGL(pack_kernel<16>, dim3(grid), dim3(PACK_BLOCK), smem, stream, pp);
+      else hipLaunchKernelGGL(pack_kernel<32>, dim3(grid), dim3(PACK_BLOCK), smem, stream, pp);
+      HIPCHK(hipGetLastError());
+      HIPCHK(hipEventRecord(e1, stream));
+      HIPCHK(hipEventSynchronize(e1));
+      float ms = 0;
+      HIPCHK(hipEventElapsedTime(&ms, e0, e1));
+      st.kernel_ms += ms;
+      st.pack_ms += ms;
+      st.launches++;
+    }
+    if (b.n_pack16 + b.n_pack32) {
+      HIPCHK(hipMemcpyAsync(b.h_res.data(), b.res, b.n_hist * sizeof(HistResult), hipMemcpyDeviceToHost, stream));
+      HIPCHK(hipStreamSynchronize(stream));
+    }
+    for (uint32_t i = 0; i < b.n_hist; ++i)
+      if (!b.forced[i] && b.h_hist[i].K <= 32 && b.h_res[i].verdict == V_UNKNOWN && b.h_res[i].reason == S2LC_R_FRONTIER)
+        todo.push_back(i);
+    st.n_overflow = (uint32_t)todo.size();
+    todo.insert(todo.end(), b.h_rest.begin(), b.h_rest.end());
+  } else {
+    std::vector<uint32_t> all(b.n_pack16 + b.n_pack32 + b.h_rest.size());
+    if (!all.empty()) HIPCHK(hipMemcpy(all.data(), b.order, all.size() * sizeof(uint32_t), hipMemcpyDeviceToHost));
+    todo = all;
+  }
   const uint32_t lds_fcap = 8;
   const uint32_t lds_stage = 32;
   const size_t lds_budget = b.kmax <= 16 ? 10240 : b.kmax <= 32 ? 13312 : 0;
-  std::vector<uint32_t> todo;  // histories for passes >= 1
   uint32_t* d_list = nullptr;
   for (int pass = 0; pass < 3; ++pass) {
-    uint32_t n_pass = pass == 0 ? n_search : (uint32_t)todo.size();
+    uint32_t n_pass = (uint32_t)todo.size();
     if (n_pass == 0) break;
     SearchGeom g;
     if (pass == 0) {
@@ -279,15 +340,11 @@ int batch_run(DevBatch& b, hipStream_t stream, uint64_t max_configs, bool witnes
     }
     if (!g.shared && ensure((void**)&b.slab, b.slab_cap, g.slab_bytes * g.grid, err)) return S2LC_EHIP;
     Params pp = prm;
-    if (pass == 0) {
-      pp.order = b.order;
-    } else {
-      if (d_list) (void)hipFree(d_list);
-      d_list = nullptr;
-      HIPCHK(hipMalloc(&d_list, todo.size() * sizeof(uint32_t)));
-      HIPCHK(hipMemcpyAsync(d_list, todo.data(), todo.size() * sizeof(uint32_t), hipMemcpyHostToDevice, stream));
-      pp.order = d_list;
-    }
+    if (d_list) (void)hipFree(d_list);
+    d_list = nullptr;
+    HIPCHK(hipMalloc(&d_list, todo.size() * sizeof(uint32_t)));
+    HIPCHK(hipMemcpyAsync(d_list, todo.data(), todo.size() * sizeof(uint32_t), hipMemcpyHostToDevice, stream));
+    pp.order = d_list;
     pp.n_hist = n_pass;
     pp.counter = b.counter + 4 * pass;
     pp.slab = b.slab;
@@ -345,7 +402,7 @@ int batch_run(DevBatch& b, hipStream_t stream, uint64_t max_configs, bool witnes
     std::vector<uint32_t> next;
     for (uint32_t i = 0; i < b.n_hist; ++i)
       if (!b.forced[i] && b.h_res[i].verdict == V_UNKNOWN && b.h_res[i].reason == S2LC_R_FRONTIER) next.push_back(i);
-    if (pass == 0) st.n_overflow = (uint32_t)next.size();
+    if (pass == 0) st.n_overflow += (uint32_t)next.size();
     else st.n_overflow2 += (uint32_t)next.size();
     todo.swap(next);
   }
