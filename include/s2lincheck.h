@@ -194,6 +194,14 @@ typedef struct s2lc_batch_stats {
   uint64_t algo_bytes;       /* algorithmic bytes of the main launch */
   uint32_t n_overflow;       /* histories re-run on the wide path */
   uint32_t launches;
+  /* device-wide level search (histories with > 128 chains or a frontier
+   * beyond the per-workgroup passes) */
+  double level_ms;           /* device time of the level search, included in kernel_ms */
+  uint32_t level_histories;
+  uint32_t level_max_frontier;
+  uint64_t level_rounds;
+  uint64_t level_configs;
+  uint64_t level_children;
 } s2lc_batch_stats;
 int s2lc_batch_stats_get(const s2lc_batch* b, s2lc_batch_stats* out);
 

@@ -88,7 +88,10 @@ class c_batch_stats(ctypes.Structure):
     _fields_ = [("kernel_ms", ctypes.c_double), ("total_ms", ctypes.c_double),
                 ("configs_explored", ctypes.c_uint64), ("children_generated", ctypes.c_uint64),
                 ("rounds", ctypes.c_uint64), ("algo_bytes", ctypes.c_uint64),
-                ("n_overflow", ctypes.c_uint32), ("launches", ctypes.c_uint32)]
+                ("n_overflow", ctypes.c_uint32), ("launches", ctypes.c_uint32),
+                ("level_ms", ctypes.c_double), ("level_histories", ctypes.c_uint32),
+                ("level_max_frontier", ctypes.c_uint32), ("level_rounds", ctypes.c_uint64),
+                ("level_configs", ctypes.c_uint64), ("level_children", ctypes.c_uint64)]
 
 
 class c_sim_params(ctypes.Structure):

@@ -323,8 +323,10 @@ int s2lc_batch_results(s2lc_ctx* c, s2lc_batch* b, s2lc_result* out, int with_wi
       if (want_w && r.verdict == V_OK && r.has_witness == 1) {
         const History& H = *B.src[i];
         std::vector<uint32_t> order;
-        const bool ok = rebuild_linearization(H, B.h_moves.data() + r.witness_off, r.witness_len, r.p4 != 0, order) &&
-                        replay_order(H, order.data(), order.size());
+        std::vector<uint8_t> ident;
+        const bool ok =
+            rebuild_linearization(H, B.h_moves.data() + r.witness_off, r.witness_len, r.p4 != 0, order, ident) &&
+            replay_path(H, order.data(), ident.data(), order.size());
         if (!ok) {
           o.reason = S2LC_R_WITNESS_INVALID;
           continue;
@@ -361,6 +363,12 @@ int s2lc_batch_stats_get(const s2lc_batch* b, s2lc_batch_stats* out) {
   out->algo_bytes = b->stats.algo_bytes;
   out->n_overflow = b->stats.n_overflow;
   out->launches = b->stats.launches;
+  out->level_ms = b->stats.level.ms;
+  out->level_histories = b->stats.level.histories;
+  out->level_max_frontier = b->stats.level.max_frontier;
+  out->level_rounds = b->stats.level.rounds;
+  out->level_configs = b->stats.level.configs;
+  out->level_children = b->stats.level.children;
   return 0;
 }
 

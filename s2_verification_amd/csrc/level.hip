@@ -1,0 +1,245 @@
+// level.hip — host driver of the device-wide level-synchronous search of one
+// history (kernels in level_dev.h). Called by batch_run for histories with
+// more than 128 chains and for histories whose frontier outgrew the
+// per-workgroup passes. One round = lv_expand -> lv_close -> lv_insert, then
+// one 64-byte control read-back decides: found (Ok), empty (Illegal), or the
+// next round. A round whose children or staged configurations exceed the
+// device buffers is re-run over halves of its frontier.
+#include <hip/hip_runtime.h>
+#include <string.h>
+
+#include <algorithm>
+#include <string>
+
+#include "s2lincheck.h"
+#include "search.h"
+#include "search_dev.h"
+#include "level_dev.h"
+
+namespace s2lc {
+
+namespace {
+
+#define LVCHK(x)                                                         \
+  do {                                                                   \
+    hipError_t e_ = (x);                                                 \
+    if (e_ != hipSuccess) {                                              \
+      err = std::string(#x) + ": " + hipGetErrorString(e_);              \
+      return S2LC_EHIP;                                                  \
+    }                                                                    \
+  } while (0)
+
+size_t lv_cfg_bytes(uint32_t kmax) { return 48 + 2 * (size_t)kmax; }
+
+template <int KMAX>
+hipError_t lv_launch(int which, uint32_t grid, const LvParams& p, hipStream_t st) {
+  if (which == 0) hipLaunchKernelGGL(lv_expand<KMAX>, dim3(grid), dim3(LV_BLOCK), 0, st, p);
+  else if (which == 1) hipLaunchKernelGGL(lv_close<KMAX>, dim3(grid), dim3(LV_BLOCK), 0, st, p);
+  else hipLaunchKernelGGL(lv_insert<KMAX>, dim3(grid), dim3(LV_BLOCK), 0, st, p);
+  return hipGetLastError();
+}
+
+hipError_t lv_dispatch(uint32_t kmax, int which, uint32_t grid, const LvParams& p, hipStream_t st) {
+  switch (kmax) {
+    case 64: return lv_launch<64>(which, grid, p, st);
+    case 128: return lv_launch<128>(which, grid, p, st);
+    case 256: return lv_launch<256>(which, grid, p, st);
+    default: return lv_launch<512>(which, grid, p, st);
+  }
+}
+
+int lv_ensure(void** p, size_t& cap, size_t need, std::string& err) {
+  if (need <= cap) return 0;
+  if (*p) (void)hipFree(*p);
+  *p = nullptr;
+  cap = 0;
+  LVCHK(hipMalloc(p, need));
+  cap = need;
+  return 0;
+}
+
+}  // namespace
+
+uint32_t level_kmax(uint32_t K) { return K <= 64 ? 64 : K <= 128 ? 128 : K <= 256 ? 256 : 512; }
+
+int level_buffers(DevBatch& b, uint32_t kmax, std::string& err) {
+  LevelBufs& L = b.lv;
+  if (L.kmax >= kmax && L.ctl) return 0;
+  size_t free_b = 0, total_b = 0;
+  LVCHK(hipMemGetInfo(&free_b, &total_b));
+  // a quarter of free HBM (at most 48 GiB): two staging arrays + index
+  // lists + table, and the children array
+  const size_t budget = std::min<size_t>(free_b / 4, 48ull << 30);
+  const size_t cb = lv_cfg_bytes(kmax);
+  uint64_t scap = std::min<uint64_t>(1ull << 24, (uint64_t)(budget * 6 / 10) / (2 * cb + 2 * 4 + 2 * 8));
+  uint64_t ccap = std::min<uint64_t>(1ull << 26, (uint64_t)(budget * 3 / 10) / sizeof(LChild));
+  scap = std::max<uint64_t>(scap, 1024);
+  ccap = std::max<uint64_t>(ccap, 4096);
+  uint64_t ht = 1024;
+  while (ht < 2 * scap) ht <<= 1;
+  if (lv_ensure((void**)&L.child, L.child_bytes, ccap * sizeof(LChild), err)) return S2LC_EHIP;
+  for (int i = 0; i < 2; ++i) {
+    if (lv_ensure((void**)&L.stg[i], L.stg_bytes[i], scap * cb, err)) return S2LC_EHIP;
+    if (lv_ensure((void**)&L.idx[i], L.idx_bytes[i], scap * sizeof(uint32_t), err)) return S2LC_EHIP;
+  }
+  if (lv_ensure((void**)&L.ht, L.ht_bytes, ht * 8, err)) return S2LC_EHIP;
+  if (!L.ctl) LVCHK(hipMalloc(&L.ctl, sizeof(LvCtl)));
+  if (!L.h_ctl) LVCHK(hipHostMalloc(&L.h_ctl, sizeof(LvCtl), hipHostMallocDefault));
+  LVCHK(hipMemset(L.ht, 0xFF, ht * 8));
+  L.kmax = kmax;
+  L.scap = (uint32_t)scap;
+  L.ccap = (uint32_t)ccap;
+  L.ht_mask = (uint32_t)(ht - 1);
+  return 0;
+}
+
+void level_release(DevBatch& b) {
+  LevelBufs& L = b.lv;
+  void* ptrs[] = {L.child, L.stg[0], L.stg[1], L.idx[0], L.idx[1], L.ht, L.ctl};
+  for (void* q : ptrs) if (q) (void)hipFree(q);
+  if (L.h_ctl) (void)hipHostFree(L.h_ctl);
+  L = LevelBufs{};
+}
+
+int level_search(DevBatch& b, uint32_t h, hipStream_t st, uint64_t max_configs, bool witness, LevelStats& ls,
+                 std::string& err) {
+  const HistDesc& hd = b.h_hist[h];
+  const uint32_t K = hd.K;
+  const uint32_t kmax = level_kmax(K);
+  if (level_buffers(b, kmax, err)) return S2LC_EHIP;
+  LevelBufs& L = b.lv;
+  LvCtl* hc = reinterpret_cast<LvCtl*>(L.h_ctl);
+  int dev = 0;
+  LVCHK(hipGetDevice(&dev));
+  int n_cu = 256;
+  (void)hipDeviceGetAttribute(&n_cu, hipDeviceAttributeMultiprocessorCount, dev);
+  const uint32_t max_grid = (uint32_t)n_cu * 8;
+
+  // trace entries continue after what earlier passes / histories used
+  unsigned long long tb0 = 0;
+  if (witness && b.trace) {
+    LVCHK(hipMemcpyAsync(&tb0, b.trace_head, sizeof tb0, hipMemcpyDeviceToHost, st));
+    LVCHK(hipStreamSynchronize(st));
+  }
+  bool wit = witness && b.trace != nullptr;
+
+  LvParams p;
+  memset(&p, 0, sizeof p);
+  p.recs = b.recs; p.pool = b.pool; p.cs = b.chain_start + hd.cs_base; p.K = K; p.hflags = hd.flags;
+  p.child = reinterpret_cast<LChild*>(L.child); p.ccap = L.ccap; p.scap = L.scap; p.ht = L.ht; p.ht_mask = L.ht_mask;
+  p.trace = b.trace; p.ctl = reinterpret_cast<LvCtl*>(L.ctl);
+
+  hipEvent_t e0, e1;
+  LVCHK(hipEventCreate(&e0));
+  LVCHK(hipEventCreate(&e1));
+  LVCHK(hipEventRecord(e0, st));
+
+  // round 0: the initial configuration as the only child, closed + inserted
+  memset(hc, 0, sizeof(LvCtl));
+  hc->nchild = 1;
+  const LChild c0{0, 0, 0, LV_NONE, LV_NONE, 0};
+  LVCHK(hipMemcpyAsync(L.child, &c0, sizeof c0, hipMemcpyHostToDevice, st));
+  LVCHK(hipMemcpyAsync(L.ctl, hc, sizeof(LvCtl), hipMemcpyHostToDevice, st));
+  int cur = 0;  // round r stages into stg[cur ^ 1]; its frontier is stg[cur]
+  p.cur = L.stg[cur]; p.cur_idx = L.idx[cur];
+  p.stg = L.stg[cur ^ 1]; p.nxt_idx = L.idx[cur ^ 1];
+  p.tbase = (uint32_t)tb0; p.witness = wit ? 1u : 0u;
+  if (wit && tb0 + 1 > b.trace_cap) { wit = false; p.witness = 0; }
+  LVCHK(lv_dispatch(kmax, 1, 1, p, st));
+  LVCHK(lv_dispatch(kmax, 2, 1, p, st));
+  LVCHK(hipMemcpyAsync(hc, L.ctl, sizeof(LvCtl), hipMemcpyDeviceToHost, st));
+  LVCHK(hipStreamSynchronize(st));
+
+  uint64_t configs = 0, children = 0, tnext = tb0;
+  uint32_t rounds = 0, max_frontier = 0;
+  uint32_t verdict = V_ILLEGAL, reason = S2LC_R_SEARCH_EXHAUSTED;
+  for (;;) {
+    if (hc->found) { verdict = V_OK; reason = 0; break; }
+    const uint32_t nf = hc->nnext;
+    if (nf == 0) { verdict = V_ILLEGAL; reason = S2LC_R_SEARCH_EXHAUSTED; break; }
+    configs += nf;
+    max_frontier = std::max(max_frontier, nf);
+    if (p.witness) tnext += nf;
+    if (max_configs && configs > max_configs) { verdict = V_UNKNOWN; reason = S2LC_R_BUDGET; break; }
+    cur ^= 1;
+    p.cur = L.stg[cur]; p.cur_idx = L.idx[cur];
+    p.stg = L.stg[cur ^ 1]; p.nxt_idx = L.idx[cur ^ 1];
+    p.clear_slots = 1;
+    if (wit && tnext + L.scap > b.trace_cap) wit = false;
+    p.witness = wit ? 1u : 0u;
+    p.tbase = (uint32_t)tnext;
+    ++rounds;
+    // one round, in frontier chunks (normally one)
+    memset(hc, 0, sizeof(LvCtl));
+    uint32_t f0 = 0, chunk = nf, st_lo = 0, nn_lo = 0;
+    bool stop = false;
+    while (f0 < nf) {
+      const uint32_t f1 = (uint32_t)std::min<uint64_t>(nf, (uint64_t)f0 + chunk);
+      hc->nchild = 0; hc->nstage = st_lo; hc->nnext = nn_lo; hc->overflow = 0;
+      LVCHK(hipMemcpyAsync(L.ctl, hc, sizeof(LvCtl), hipMemcpyHostToDevice, st));
+      p.f0 = f0; p.f1 = f1; p.st_lo = st_lo;
+      const uint64_t lanes = (uint64_t)(f1 - f0) * K;
+      const uint32_t g_exp = (uint32_t)std::min<uint64_t>(max_grid, (lanes + LV_BLOCK - 1) / LV_BLOCK);
+      const uint64_t kids_ub = std::min<uint64_t>(2 * lanes, L.ccap);
+      const uint32_t g_cls = (uint32_t)std::min<uint64_t>(max_grid, (kids_ub + 3) / 4);
+      const uint32_t g_ins = (uint32_t)std::min<uint64_t>(max_grid, (std::min<uint64_t>(kids_ub, L.scap) + LV_BLOCK - 1) / LV_BLOCK);
+      LVCHK(lv_dispatch(kmax, 0, std::max<uint32_t>(1, g_exp), p, st));
+      LVCHK(lv_dispatch(kmax, 1, std::max<uint32_t>(1, g_cls), p, st));
+      LVCHK(lv_dispatch(kmax, 2, std::max<uint32_t>(1, g_ins), p, st));
+      LVCHK(hipMemcpyAsync(hc, L.ctl, sizeof(LvCtl), hipMemcpyDeviceToHost, st));
+      LVCHK(hipStreamSynchronize(st));
+      if (hc->found) break;
+      if (hc->overflow) {
+        if (f1 - f0 == 1) { verdict = V_UNKNOWN; reason = S2LC_R_FRONTIER; stop = true; break; }
+        chunk = std::max<uint32_t>(1, (f1 - f0) / 2);
+        ++ls.chunk_retries;
+        continue;
+      }
+      children += std::min(hc->nchild, L.ccap);
+      st_lo = std::min(hc->nstage, L.scap);
+      nn_lo = hc->nnext;
+      f0 = f1;
+    }
+    if (hc->found) children += std::min(hc->nchild, L.ccap);
+    if (stop) break;
+  }
+  LVCHK(hipEventRecord(e1, st));
+  LVCHK(hipEventSynchronize(e1));
+  float ms = 0;
+  LVCHK(hipEventElapsedTime(&ms, e0, e1));
+  LVCHK(hipEventDestroy(e0));
+  LVCHK(hipEventDestroy(e1));
+  // clear the table for the next search (slots of the last frontier; cheap
+  // enough to reset whole when the frontier was large)
+  LVCHK(hipMemsetAsync(L.ht, 0xFF, ((size_t)L.ht_mask + 1) * 8, st));
+
+  HistResult& R = b.h_res[h];
+  const uint32_t woff = R.witness_off;
+  R = HistResult{};
+  R.witness_off = woff;
+  R.verdict = verdict;
+  R.reason = reason;
+  R.rounds = rounds;
+  R.configs = configs;
+  R.children = children;
+  R.p4 = verdict == V_OK ? hc->found_p4 : 0;
+  const bool have_w = verdict == V_OK && wit;
+  R.final_parent = have_w ? hc->found_parent : TRACE_NONE;
+  R.final_move = verdict == V_OK ? hc->found_move : TRACE_NONE;
+  R.has_witness = have_w ? 2u : 0u;
+  LVCHK(hipMemcpyAsync(b.res + h, &R, sizeof R, hipMemcpyHostToDevice, st));
+  if (witness && b.trace) {
+    unsigned long long th = tnext;
+    LVCHK(hipMemcpyAsync(b.trace_head, &th, sizeof th, hipMemcpyHostToDevice, st));
+  }
+  LVCHK(hipStreamSynchronize(st));
+  ls.ms += ms;
+  ls.rounds += rounds;
+  ls.configs += configs;
+  ls.children += children;
+  ls.max_frontier = std::max(ls.max_frontier, max_frontier);
+  ls.histories++;
+  return 0;
+}
+
+}  // namespace s2lc

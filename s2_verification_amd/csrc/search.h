@@ -57,6 +57,24 @@ struct SearchGeom {
   size_t smem_bytes;   // dynamic LDS bytes per workgroup
 };
 
+// Buffers of the device-wide level search (level.hip), reused across histories.
+struct LevelBufs {
+  uint32_t kmax = 0, scap = 0, ccap = 0, ht_mask = 0;
+  void* child = nullptr;
+  uint8_t* stg[2] = {nullptr, nullptr};
+  uint32_t* idx[2] = {nullptr, nullptr};
+  unsigned long long* ht = nullptr;
+  void* ctl = nullptr;
+  void* h_ctl = nullptr;  // pinned host mirror of the control block
+  size_t child_bytes = 0, stg_bytes[2] = {0, 0}, idx_bytes[2] = {0, 0}, ht_bytes = 0;
+};
+
+struct LevelStats {
+  double ms = 0;
+  uint64_t rounds = 0, configs = 0, children = 0;
+  uint32_t max_frontier = 0, histories = 0, chunk_retries = 0;
+};
+
 struct DevBatch {
   int device = 0;
   uint32_t n_hist = 0;
@@ -68,7 +86,9 @@ struct DevBatch {
   HistDesc* hist = nullptr;
   uint32_t* order = nullptr;        // LPT processing order: [K<=16 | K<=32 | rest]
   uint32_t n_pack16 = 0, n_pack32 = 0;
-  std::vector<uint32_t> h_rest;     // histories searched one per workgroup (K > 32)
+  std::vector<uint32_t> h_rest;     // histories searched one per workgroup (32 < K <= 128)
+  std::vector<uint32_t> h_level;    // histories searched by the device-wide level search (K > 128)
+  LevelBufs lv;
   HistResult* res = nullptr;
   uint32_t* moves = nullptr;        // witness moves (per history at witness_off)
   uint32_t* counter = nullptr;      // work counters (scheduling)
@@ -95,6 +115,7 @@ struct RunStats {
   uint64_t algo_bytes = 0;
   uint32_t n_overflow = 0, launches = 0;
   double pack_ms = 0;
+  LevelStats level;
 };
 
 int batch_upload(DevBatch& b, const std::vector<const History*>& hs, std::string& err);
@@ -102,11 +123,27 @@ void batch_release(DevBatch& b);
 int batch_run(DevBatch& b, hipStream_t stream, uint64_t max_configs, bool witness, RunStats& st,
               std::string& err);
 
+constexpr uint32_t LEVEL_KMAX = 512;  // most chains the level search handles
+uint32_t level_kmax(uint32_t K);
+int level_search(DevBatch& b, uint32_t h, hipStream_t st, uint64_t max_configs, bool witness, LevelStats& ls,
+                 std::string& err);
+void level_release(DevBatch& b);
+
 // Host reconstruction of a full linearization (dense op ids) from the device
 // move list; returns false if any move is not a legal successor.
+// ident[i] = 1 when order[i] took its identity outcome (E ops, indefinite
+// appends taken as not applied).
 bool rebuild_linearization(const History& h, const uint32_t* moves, uint32_t n_moves, bool p4,
-                           std::vector<uint32_t>& order);
-// Powerset replay of a linearization through the CPU model (+ real-time check).
+                           std::vector<uint32_t>& order, std::vector<uint8_t>& ident);
+// Every op exactly once, in an order that respects real time.
+bool real_time_ok(const History& h, const uint32_t* order, size_t n);
+// Powerset replay of a linearization through the CPU model (+ real-time
+// check), porcupine's ToModel().Step semantics; false if the state set would
+// exceed 2^16 states.
 bool replay_order(const History& h, const uint32_t* order, size_t n);
+// Single-path replay: real-time check, then every op's claimed outcome must be
+// one of s2Model.Step's successors (main.go:264-335). A path of states is a
+// certificate that the powerset run never empties.
+bool replay_path(const History& h, const uint32_t* order, const uint8_t* ident, size_t n);
 
 }  // namespace s2lc

@@ -129,9 +129,9 @@ int batch_upload(DevBatch& b, const std::vector<const History*>& hs, std::string
     const History& h = *hs[i];
     if (h.status != 0) { err = "history " + std::to_string(i) + ": " + h.error; return h.status; }
     if (h.structural) { b.forced[i] = 1; }
-    if (h.K > 128) { err = "history has more than 128 concurrent chains"; return S2LC_EUNSUPPORTED; }
+    if (h.K > LEVEL_KMAX) { err = "history has more than 512 concurrent chains"; return S2LC_EUNSUPPORTED; }
     if (h.max_chain_len >= 0xFFFF) { err = "chain longer than 65534 ops"; return S2LC_EUNSUPPORTED; }
-    kmax_needed = std::max(kmax_needed, h.K);
+    if (h.K <= 128) kmax_needed = std::max(kmax_needed, h.K);
     HistDesc& d = b.h_hist[i];
     d.rec_base = (uint32_t)n_recs;
     d.cs_base = (uint32_t)n_cs;
@@ -178,9 +178,14 @@ int batch_upload(DevBatch& b, const std::vector<const History*>& hs, std::string
   });
   {
     std::vector<uint32_t> l16, l32, rest;
+    b.h_level.clear();
+    // S2LC_LEVEL_ONLY=1 (tests): every history through the level search
+    const char* lo = getenv("S2LC_LEVEL_ONLY");
+    const bool level_only = lo && lo[0] == '1';
     for (uint32_t i : order) {
       const uint32_t K = b.h_hist[i].K;
-      (K <= 16 ? l16 : K <= 32 ? l32 : rest).push_back(i);
+      if (level_only) b.h_level.push_back(i);
+      else (K <= 16 ? l16 : K <= 32 ? l32 : K <= 128 ? rest : b.h_level).push_back(i);
     }
     b.n_pack16 = (uint32_t)l16.size();
     b.n_pack32 = (uint32_t)l32.size();
@@ -213,6 +218,7 @@ int batch_upload(DevBatch& b, const std::vector<const History*>& hs, std::string
 }
 
 void batch_release(DevBatch& b) {
+  level_release(b);
   void* ptrs[] = {b.recs, b.pool, b.chain_start, b.hist, b.order, b.res, b.moves, b.counter, b.trace, b.trace_head, b.slab};
   for (void* q : ptrs) if (q) (void)hipFree(q);
   b.recs = nullptr; b.pool = nullptr; b.chain_start = nullptr; b.hist = nullptr; b.order = nullptr;
@@ -318,7 +324,7 @@ int batch_run(DevBatch& b, hipStream_t stream, uint64_t max_configs, bool witnes
   const uint32_t lds_stage = 32;
   const size_t lds_budget = b.kmax <= 16 ? 10240 : b.kmax <= 32 ? 13312 : 0;
   uint32_t* d_list = nullptr;
-  for (int pass = 0; pass < 3; ++pass) {
+  for (int pass = 0; pass < 2; ++pass) {
     uint32_t n_pass = (uint32_t)todo.size();
     if (n_pass == 0) break;
     SearchGeom g;
@@ -326,17 +332,9 @@ int batch_run(DevBatch& b, hipStream_t stream, uint64_t max_configs, bool witnes
       g = make_geom(b.kmax, true, 64, lds_fcap, lds_stage, lds_stage, 1, lds_budget);
       const uint32_t per_cu = std::max<uint32_t>(1, std::min<uint32_t>(16, (uint32_t)((160 * 1024) / g.smem_bytes)));
       g.grid = std::max<uint32_t>(1, std::min<uint32_t>(n_pass, (uint32_t)n_cu * per_cu));
-    } else if (pass == 1) {
+    } else {
       g = make_geom(b.kmax, false, 64, 1024, 512, 256, 1, 0);
       g.grid = std::max<uint32_t>(1, std::min<uint32_t>(n_pass, (uint32_t)n_cu * 16));
-    } else {
-      size_t free_b = 0, total_b = 0;
-      HIPCHK(hipMemGetInfo(&free_b, &total_b));
-      uint32_t fcap = 1u << 20;
-      g = make_geom(b.kmax, false, 256, fcap, 32768, 16384, 1, 0);
-      while (g.slab_bytes > free_b / 2 && fcap > 4096) { fcap >>= 1; g = make_geom(b.kmax, false, 256, fcap, 32768, 16384, 1, 0); }
-      g.grid = (uint32_t)std::min<size_t>(n_pass, std::max<size_t>(1, (free_b / 2) / g.slab_bytes));
-      g.grid = std::min<uint32_t>(g.grid, (uint32_t)n_cu);
     }
     if (!g.shared && ensure((void**)&b.slab, b.slab_cap, g.slab_bytes * g.grid, err)) return S2LC_EHIP;
     Params pp = prm;
@@ -407,6 +405,14 @@ int batch_run(DevBatch& b, hipStream_t stream, uint64_t max_configs, bool witnes
     todo.swap(next);
   }
   if (d_list) (void)hipFree(d_list);
+  // Pass 2: the device-wide level search, one history at a time: histories
+  // with more than 128 chains and those whose frontier outgrew pass 1.
+  todo.insert(todo.end(), b.h_level.begin(), b.h_level.end());
+  for (uint32_t h : todo) {
+    const int rc = level_search(b, h, stream, max_configs, witness, st.level, err);
+    if (rc) return rc;
+  }
+  st.kernel_ms += st.level.ms;
   if (witness && b.n_hist) {
     hipLaunchKernelGGL(walk_kernel, dim3((b.n_hist + 255) / 256), dim3(256), 0, stream, b.n_hist, b.res,
                        (const TraceEnt*)b.trace, b.moves);

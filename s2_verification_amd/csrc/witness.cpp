@@ -29,7 +29,7 @@ uint32_t min_ret(const History& h, const HostCfg& c) {
 }
 
 // Same closure as the device (search.hip), recording the ops it linearizes.
-void close(const History& h, HostCfg& c, std::vector<uint32_t>& order) {
+void close(const History& h, HostCfg& c, std::vector<uint32_t>& order, std::vector<uint8_t>& ident) {
   for (;;) {
     const uint32_t mr = min_ret(h, c);
     if (mr == EV_INF) return;
@@ -39,6 +39,7 @@ void close(const History& h, HostCfg& c, std::vector<uint32_t>& order) {
         const OpRec& r = head(h, c, q);
         if (!(r.flags & OPF_CLS_E) || r.call_ev >= mr || !ident_legal(r, c.s)) break;
         order.push_back(h.rec_op[h.chain_start[q] + c.cnt[q]]);
+        ident.push_back(1);
         c.cnt[q]++;
         changed = true;
       }
@@ -50,15 +51,16 @@ void close(const History& h, HostCfg& c, std::vector<uint32_t>& order) {
 }  // namespace
 
 bool rebuild_linearization(const History& h, const uint32_t* moves, uint32_t n_moves, bool p4,
-                           std::vector<uint32_t>& order) {
+                           std::vector<uint32_t>& order, std::vector<uint8_t>& ident) {
   order.clear();
+  ident.clear();
   if (h.structural) return false;
   HostCfg c;
   c.cnt.assign(h.K, 0);
-  close(h, c, order);
+  close(h, c, order, ident);
   for (uint32_t m = 0; m < n_moves; ++m) {
     const uint32_t j = moves[m] & 0xFFFFu;
-    const bool ident = moves[m] & MOVE_IDENT;
+    const bool is_id = moves[m] & MOVE_IDENT;
     if (j >= h.K) return false;
     const OpRec& r = head(h, c, j);
     if (r.flags & (OPF_SENTINEL | OPF_CLS_E)) return false;
@@ -66,7 +68,7 @@ bool rebuild_linearization(const History& h, const uint32_t* moves, uint32_t n_m
     State kids[2];
     const int nk = s2_step(r, c.s, h.pool.data(), kids);
     State want = c.s;
-    if (!ident) {
+    if (!is_id) {
       if (!append_guards_ok(r, c.s)) return false;
       want = append_opt(r, c.s, h.pool.data());
     }
@@ -75,8 +77,9 @@ bool rebuild_linearization(const History& h, const uint32_t* moves, uint32_t n_m
     if (!found) return false;
     c.s = want;
     order.push_back(h.rec_op[h.chain_start[j] + c.cnt[j]]);
+    ident.push_back(is_id ? 1 : 0);
     c.cnt[j]++;
-    close(h, c, order);
+    close(h, c, order, ident);
   }
   if (order.size() != h.n_ops) {
     if (!p4) return false;
@@ -86,11 +89,31 @@ bool rebuild_linearization(const History& h, const uint32_t* moves, uint32_t n_m
       for (uint32_t p = h.chain_start[q] + c.cnt[q]; p + 1 < h.chain_start[q + 1]; ++p) rest.push_back(h.rec_op[p]);
     std::sort(rest.begin(), rest.end(), [&](uint32_t a, uint32_t b) { return h.op_ret[a] < h.op_ret[b]; });
     order.insert(order.end(), rest.begin(), rest.end());
+    ident.resize(order.size(), 1);
   }
   return order.size() == h.n_ops;
 }
 
-bool replay_order(const History& h, const uint32_t* order, size_t n) {
+bool replay_path(const History& h, const uint32_t* order, const uint8_t* ident, size_t n) {
+  if (!real_time_ok(h, order, n)) return false;
+  State s{0, 0, 0};
+  for (size_t i = 0; i < n; ++i) {
+    const OpRec r = h.rec_of(order[i]);
+    State kids[2];
+    const int nk = s2_step(r, s, h.pool.data(), kids);
+    // the outcome this linearization claims: the optimistic successor for an
+    // append taken as applied, the unchanged state otherwise
+    const bool applied = !ident[i] && !(r.flags & OPF_CLS_E) && (r.flags & OPF_KIND_MASK) == 0;
+    const State want = applied ? append_opt(r, s, h.pool.data()) : s;
+    bool found = false;
+    for (int k = 0; k < nk; ++k) found |= state_eq(kids[k], want);
+    if (!found) return false;
+    s = want;
+  }
+  return true;
+}
+
+bool real_time_ok(const History& h, const uint32_t* order, size_t n) {
   if (h.structural || n != h.n_ops) return false;
   std::vector<uint8_t> seen(h.n_ops, 0);
   for (size_t i = 0; i < n; ++i) {
@@ -103,6 +126,11 @@ bool replay_order(const History& h, const uint32_t* order, size_t n) {
     if (h.op_call[order[i]] >= later_min_ret) return false;
     later_min_ret = std::min(later_min_ret, h.op_ret[order[i]]);
   }
+  return true;
+}
+
+bool replay_order(const History& h, const uint32_t* order, size_t n) {
+  if (!real_time_ok(h, order, n)) return false;
   // powerset replay (ToModel().Step + merge)
   std::vector<State> set{State{0, 0, 0}}, next;
   for (size_t i = 0; i < n; ++i) {

@@ -3,8 +3,8 @@
 SURVEY.md §8(d): C1 regular 5x100 (seed 1), C2 match-seq-num 10x200 (seed 2),
 C3 fencing 16x500 (seed 3), C4 10k histories of 5-8 clients x 100 ops (seeds
 0..9999, clients = 5 + seed mod 4, workflow = seed mod 3, every 10th seed with
-an injected violation), C5 32x1000 (seed 5, raised indefinite-failure rate) and
-its non-linearizable variant.
+an injected violation), C5 32x1000 (seed 5, client-id cap lifted, 3% indefinite
+appends) and its non-linearizable variant.
 """
 from . import (VIOL_DEFINITE_APPLIED, VIOL_NONE, VIOL_READ_HASH, VIOL_STALE_MSN, VIOL_TAIL, WF_FENCING,
                WF_MATCH_SEQ_NUM, WF_REGULAR, simulate_history, simulate_jsonl)
@@ -15,10 +15,25 @@ CONFIGS = {
     "C1": dict(workflow=WF_REGULAR, num_clients=5, ops_per_client=100, seed=1, **BASE),
     "C2": dict(workflow=WF_MATCH_SEQ_NUM, num_clients=10, ops_per_client=200, seed=2, **BASE),
     "C3": dict(workflow=WF_FENCING, num_clients=16, ops_per_client=500, seed=3, **BASE),
-    "C5": dict(workflow=WF_REGULAR, num_clients=32, ops_per_client=1000, seed=5,
-               **{**BASE, "p_indefinite": 0.002}),
-    "C5bad": dict(workflow=WF_REGULAR, num_clients=32, ops_per_client=1000, seed=5, violation=VIOL_READ_HASH,
-                  **{**BASE, "p_indefinite": 0.002}),
+    # single hard history: the client-id cap is lifted (max_client_ids), so a
+    # client that hits an indefinite failure rotates to a new id and keeps
+    # going (DST-harness style) instead of stopping at id 20 (history.rs:153-169);
+    # with 3% indefinite appends this leaves ~290 pending appends whose
+    # outcome only later reads resolve: K = 319 chains, ~1.6 M unique
+    # configurations, ~175 M children (the CPU reduced search needs minutes,
+    # porcupine's DFS does not finish).
+    "C5": dict(workflow=WF_REGULAR, num_clients=32, ops_per_client=1000, seed=5, max_client_ids=1 << 20,
+               **{**BASE, "p_indefinite": 0.03}),
+    "C5bad": dict(workflow=WF_REGULAR, num_clients=32, ops_per_client=1000, seed=5, max_client_ids=1 << 20,
+                  violation=VIOL_READ_HASH, **{**BASE, "p_indefinite": 0.03}),
+    # mid-size hard histories (level-search parity against the CPU reduced search)
+    "H174": dict(workflow=WF_REGULAR, num_clients=32, ops_per_client=1000, seed=5, max_client_ids=1 << 20,
+                 **{**BASE, "p_indefinite": 0.015}),
+    "H212": dict(workflow=WF_REGULAR, num_clients=32, ops_per_client=1000, seed=6, max_client_ids=1 << 20,
+                 **{**BASE, "p_indefinite": 0.02}),
+    # the round-1 C5 (client-id cap 20: clients stop at their first indefinite failure)
+    "C5capped": dict(workflow=WF_REGULAR, num_clients=32, ops_per_client=1000, seed=5,
+                     **{**BASE, "p_indefinite": 0.002}),
 }
 
 _C4_VIOLS = [VIOL_READ_HASH, VIOL_TAIL, VIOL_DEFINITE_APPLIED, VIOL_STALE_MSN]

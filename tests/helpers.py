@@ -124,3 +124,11 @@ def random_history(rng: random.Random, n_ops: int, n_clients: int = 3, p_perturb
                                    **op["out"]}))
     evs.sort(key=lambda x: (x[0], x[1]))
     return [e for _, _, e in evs]
+
+
+def config_digest(name: str) -> str:
+    """Fingerprint of a workloads.CONFIGS history (its collector JSONL), to
+    detect a changed simulator."""
+    import hashlib
+    from s2_verification_amd import workloads as W
+    return hashlib.sha256(W.config_jsonl(name)).hexdigest()[:32]

@@ -102,27 +102,19 @@ def test_configs_vs_wgl_and_reduced(checker, name):
         assert g.witness is not None and len(g.witness) == h.info()["n_ops"]
 
 
-@pytest.mark.parametrize("name,expect", [("C5", "Ok"), ("C5bad", "Illegal")])
-def test_single_hard_history(checker, name, expect):
-    """C5: 32 clients x 1000 ops. Porcupine's DFS does not finish (exponential
+def test_capped_32_client_history(checker):
+    """32 clients x 1000 ops with the collector's client-id cap (clients stop at
+    their first indefinite failure): porcupine's DFS does not finish (exponential
     backtracking); verdict cross-checked by the CPU reduced search,
-    Ok witnesses replayed through the CPU model; the bad variant differs from the
-    clean one in exactly one ReadSuccess stream hash (Illegal by construction,
-    up to a 2^-64 hash collision)."""
+    the Ok witness replayed through the CPU model. The uncapped hard histories
+    (C5, > 128 chains) are in test_level.py."""
     from s2_verification_amd import workloads as W
-    h = W.config_history(name)
+    h = W.config_history("C5capped")
     ea = orc.from_s2lc_numpy(h.events_numpy())
     r_, st = orc.check_reduced(ea)
     g = checker.check(h)
-    assert g.verdict == r_ == expect, (name, g, r_, st)
-    if expect == "Ok":
-        assert g.witness is not None and len(g.witness) == h.info()["n_ops"]
-    else:
-        good = W.config_history("C5").events()
-        bad = h.events()
-        diff = [i for i, (a, b) in enumerate(zip(good, bad)) if a != b]
-        assert len(good) == len(bad) and len(diff) == 1
-        assert bad[diff[0]].Value.StreamHash != good[diff[0]].Value.StreamHash
+    assert g.verdict == r_ == "Ok", (g, r_, st)
+    assert g.witness is not None and len(g.witness) == h.info()["n_ops"]
 
 
 def test_c4_sample_vs_wgl(checker):
