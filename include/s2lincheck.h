@@ -215,6 +215,55 @@ uint64_t s2lc_fold_record_hashes(uint64_t stream_hash, const uint64_t* record_ha
  * is accepted in order and every op appears exactly once, else -1. */
 int s2lc_replay(const s2lc_history* h, const uint32_t* order, size_t n);
 
+/* Rebuild a full linearization from a witness move list (one u32 per round:
+ * chain | 0x10000 for an indefinite append taken as not applied), re-deriving
+ * the identity ops, and certify it: real-time order + every op's claimed
+ * outcome is a successor under s2Model.Step (main.go:264-335). Writes the
+ * Event.Ids in order into out_ids[cap >= n_ops] when out_ids != NULL.
+ * 0 = valid, -1 = not a valid linearization. */
+int s2lc_witness_from_moves(const s2lc_history* h, const uint32_t* moves, size_t n_moves, int p4,
+                            int64_t* out_ids, size_t cap);
+
+/* ----- distributed search of ONE history (BASELINE config C5) --------------
+ * One rank per GPU; configurations are owned by a hash of their fingerprint.
+ * The library does the device work; the caller owns the exchange (RCCL
+ * all-to-all through torch.distributed in s2_verification_amd.distributed,
+ * or any transport) and the device buffers it exchanges. Per round:
+ *   s2lc_dist_expand  -> counts[w] configurations for each owner rank w, and
+ *                        whether a child completed (Ok anywhere ends the search)
+ *   (exchange counts; send buffer of sum(counts) * config_bytes)
+ *   s2lc_dist_pack    -> owner-major configurations into the send buffer
+ *   (all-to-all(v) of the configurations)
+ *   s2lc_dist_insert  -> dedupe the received configurations (device buffer,
+ *                        kept alive by the caller until the next insert):
+ *                        they are this rank's next frontier; n_next = its size
+ *   an all-reduce of n_next decides Illegal (0 on every rank).
+ * Trace ids: rank << 29 | index into that rank's pool (s2lc_dist_trace). */
+typedef struct s2lc_dist s2lc_dist;
+typedef struct s2lc_dist_info_t {
+  uint64_t config_bytes;   /* bytes per configuration on the wire */
+  uint32_t n_chains;
+  uint32_t round;          /* rounds completed (inserts) */
+  uint32_t frontier;       /* local frontier size */
+  uint32_t found_parent;   /* trace id of the completing child's parent (after expand reported found) */
+  uint32_t found_move;
+  uint32_t found_p4;
+  uint64_t configs;        /* unique configurations owned by this rank so far */
+  uint64_t children;       /* children generated by this rank */
+  uint64_t max_frontier;
+  double device_ms;        /* device time of this rank's kernels */
+  uint64_t trace_len;
+} s2lc_dist_info_t;
+int s2lc_dist_create(s2lc_ctx* ctx, const s2lc_history* h, int rank, int world, s2lc_dist** out);
+void s2lc_dist_free(s2lc_dist* d);
+int s2lc_dist_expand(s2lc_dist* d, uint64_t* counts /* [world] */, int32_t* found);
+int s2lc_dist_pack(s2lc_dist* d, void* send /* device */, const uint64_t* counts /* [world] */);
+int s2lc_dist_insert(s2lc_dist* d, void* recv /* device */, uint64_t n_recv, uint64_t* n_next);
+int s2lc_dist_info(const s2lc_dist* d, s2lc_dist_info_t* out);
+/* Copy this rank's trace pool ({parent id, move} u32 pairs) to host memory;
+ * with out_pairs == NULL only *n is set. */
+int s2lc_dist_trace(s2lc_dist* d, uint32_t* out_pairs, uint64_t cap_entries, uint64_t* n);
+
 /* ----- deterministic S2 simulator (collector workload, history.rs) ---------- */
 enum s2lc_workflow { S2LC_WF_REGULAR = 0, S2LC_WF_MATCH_SEQ_NUM = 1, S2LC_WF_FENCING = 2 };
 enum s2lc_violation {

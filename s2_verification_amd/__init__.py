@@ -109,6 +109,13 @@ def _np_field(t):
     return np.dtype(t)
 
 
+class c_dist_info(ctypes.Structure):
+    _fields_ = [("config_bytes", ctypes.c_uint64), ("n_chains", ctypes.c_uint32), ("round", ctypes.c_uint32),
+                ("frontier", ctypes.c_uint32), ("found_parent", ctypes.c_uint32), ("found_move", ctypes.c_uint32),
+                ("found_p4", ctypes.c_uint32), ("configs", ctypes.c_uint64), ("children", ctypes.c_uint64),
+                ("max_frontier", ctypes.c_uint64), ("device_ms", ctypes.c_double), ("trace_len", ctypes.c_uint64)]
+
+
 # s2lc_event as a numpy structured dtype (bulk export without Python loops)
 EVENT_NP_DTYPE = np.dtype({"names": [f for f, _ in c_event._fields_],
                            "formats": [_np_field(t) for _, t in c_event._fields_],
@@ -150,6 +157,15 @@ SIGNATURES = [
                                            ctypes.POINTER(ctypes.c_size_t)]),
     ("s2lc_simulate_history", ctypes.c_int, [ctypes.POINTER(c_sim_params), ctypes.POINTER(_P)]),
     ("s2lc_free", None, [_P]),
+    ("s2lc_witness_from_moves", ctypes.c_int, [_P, ctypes.POINTER(ctypes.c_uint32), ctypes.c_size_t, ctypes.c_int,
+                                               ctypes.POINTER(ctypes.c_int64), ctypes.c_size_t]),
+    ("s2lc_dist_create", ctypes.c_int, [_P, _P, ctypes.c_int, ctypes.c_int, ctypes.POINTER(_P)]),
+    ("s2lc_dist_free", None, [_P]),
+    ("s2lc_dist_expand", ctypes.c_int, [_P, ctypes.POINTER(ctypes.c_uint64), ctypes.POINTER(ctypes.c_int32)]),
+    ("s2lc_dist_pack", ctypes.c_int, [_P, _P, ctypes.POINTER(ctypes.c_uint64)]),
+    ("s2lc_dist_insert", ctypes.c_int, [_P, _P, ctypes.c_uint64, ctypes.POINTER(ctypes.c_uint64)]),
+    ("s2lc_dist_info", ctypes.c_int, [_P, ctypes.POINTER(c_dist_info)]),
+    ("s2lc_dist_trace", ctypes.c_int, [_P, _P, ctypes.c_uint64, ctypes.POINTER(ctypes.c_uint64)]),
 ]
 
 _lib = None

@@ -424,6 +424,96 @@ int s2lc_replay(const s2lc_history* h, const uint32_t* order, size_t n) {
   return replay_order(h->h, order, n) ? 0 : -1;
 }
 
+int s2lc_witness_from_moves(const s2lc_history* h, const uint32_t* moves, size_t n_moves, int p4, int64_t* out_ids,
+                            size_t cap) {
+  if (!h || (!moves && n_moves)) return S2LC_EINVAL;
+  try {
+    std::vector<uint32_t> order;
+    std::vector<uint8_t> ident;
+    if (!rebuild_linearization(h->h, moves, (uint32_t)n_moves, p4 != 0, order, ident) ||
+        !replay_path(h->h, order.data(), ident.data(), order.size()))
+      return -1;
+    if (out_ids) {
+      if (cap < order.size()) return S2LC_EINVAL;
+      for (size_t k = 0; k < order.size(); ++k) out_ids[k] = h->h.op_ids[order[k]];
+    }
+    return 0;
+  } catch (...) {
+    return S2LC_ENOMEM;
+  }
+}
+
+// ------------------------------------------------------- distributed search --
+struct s2lc_dist {
+  s2lc_ctx* ctx;
+  DistLevel d;
+};
+
+int s2lc_dist_create(s2lc_ctx* c, const s2lc_history* h, int rank, int world, s2lc_dist** out) {
+  if (!c || !h || !out || rank < 0 || world < 1) return S2LC_EINVAL;
+  *out = nullptr;
+  try {
+    if (hipSetDevice(c->device) != hipSuccess) { c->err = "hipSetDevice"; return S2LC_EHIP; }
+    auto* x = new s2lc_dist();
+    x->ctx = c;
+    const int rc = dist_create(x->d, &h->h, (uint32_t)rank, (uint32_t)world, c->err);
+    if (rc) { dist_release(x->d); delete x; return rc; }
+    *out = x;
+    return 0;
+  } catch (const std::bad_alloc&) {
+    c->err = "out of memory";
+    return S2LC_ENOMEM;
+  }
+}
+
+void s2lc_dist_free(s2lc_dist* x) {
+  if (!x) return;
+  (void)hipSetDevice(x->ctx->device);
+  dist_release(x->d);
+  delete x;
+}
+
+int s2lc_dist_expand(s2lc_dist* x, uint64_t* counts, int32_t* found) {
+  if (!x || !counts || !found) return S2LC_EINVAL;
+  int f = 0;
+  const int rc = dist_expand(x->d, counts, &f, x->ctx->err);
+  *found = f;
+  return rc;
+}
+
+int s2lc_dist_pack(s2lc_dist* x, void* send, const uint64_t* counts) {
+  if (!x || !counts || (!send && x->d.nstage)) return S2LC_EINVAL;
+  return dist_pack(x->d, (uint8_t*)send, counts, x->ctx->err);
+}
+
+int s2lc_dist_insert(s2lc_dist* x, void* recv, uint64_t n_recv, uint64_t* n_next) {
+  if (!x || !n_next || (!recv && n_recv)) return S2LC_EINVAL;
+  return dist_insert(x->d, (uint8_t*)recv, n_recv, n_next, x->ctx->err);
+}
+
+int s2lc_dist_info(const s2lc_dist* x, s2lc_dist_info_t* out) {
+  if (!x || !out) return S2LC_EINVAL;
+  const DistLevel& d = x->d;
+  out->config_bytes = d.cb;
+  out->n_chains = d.K;
+  out->round = d.round;
+  out->frontier = d.nf;
+  out->found_parent = d.found_parent;
+  out->found_move = d.found_move;
+  out->found_p4 = d.found_p4;
+  out->configs = d.configs;
+  out->children = d.children;
+  out->max_frontier = d.max_frontier;
+  out->device_ms = d.ms;
+  out->trace_len = d.tnext;
+  return 0;
+}
+
+int s2lc_dist_trace(s2lc_dist* x, uint32_t* out_pairs, uint64_t cap_entries, uint64_t* n) {
+  if (!x || !n) return S2LC_EINVAL;
+  return dist_trace(x->d, out_pairs, cap_entries, n, x->ctx->err);
+}
+
 // ------------------------------------------------------------- simulator ---
 void s2lc_sim_params_default(s2lc_sim_params* p) {
   if (!p) return;

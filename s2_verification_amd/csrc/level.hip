@@ -35,7 +35,9 @@ template <int KMAX>
 hipError_t lv_launch(int which, uint32_t grid, const LvParams& p, hipStream_t st) {
   if (which == 0) hipLaunchKernelGGL(lv_expand<KMAX>, dim3(grid), dim3(LV_BLOCK), 0, st, p);
   else if (which == 1) hipLaunchKernelGGL(lv_close<KMAX>, dim3(grid), dim3(LV_BLOCK), 0, st, p);
-  else hipLaunchKernelGGL(lv_insert<KMAX>, dim3(grid), dim3(LV_BLOCK), 0, st, p);
+  else if (which == 2) hipLaunchKernelGGL(lv_insert<KMAX>, dim3(grid), dim3(LV_BLOCK), 0, st, p);
+  else if (which == 3) hipLaunchKernelGGL(lv_bucket<KMAX>, dim3(grid), dim3(LV_BLOCK), 0, st, p);
+  else hipLaunchKernelGGL(lv_scatter<KMAX>, dim3(grid), dim3(LV_BLOCK), 0, st, p);
   return hipGetLastError();
 }
 
@@ -239,6 +241,193 @@ int level_search(DevBatch& b, uint32_t h, hipStream_t st, uint64_t max_configs, 
   ls.children += children;
   ls.max_frontier = std::max(ls.max_frontier, max_frontier);
   ls.histories++;
+  return 0;
+}
+
+
+// ============================================================================
+// Distributed level search of one history (BASELINE config C5 over several
+// GPUs). Configurations are owned by rank lv_owner(fp). A round
+// on each rank:
+//   dist_expand : expand + close the local frontier (as above) into local
+//                 staging, count the staged configurations per owner rank
+//   (caller)    : all-to-all of the counts, allocate the send buffer
+//   dist_pack   : copy the staged configurations into owner-major buckets
+//   (caller)    : all-to-all(v) of the buckets over RCCL / xGMI
+//   dist_insert : deduplicate what this rank received (it owns all of it) in
+//                 the local table; the winners are its next frontier
+// The received buffer stays the frontier of the next round (the caller keeps
+// it alive). Trace ids are rank << 29 | local pool index, so the parent chain
+// of a witness crosses ranks; the caller gathers the pools at the end.
+// ============================================================================
+
+int dist_create(DistLevel& d, const History* h, uint32_t rank, uint32_t world, std::string& err) {
+  if (world < 1 || world > 8 || rank >= world) { err = "world must be 1..8"; return S2LC_EINVAL; }
+  std::vector<const History*> hs{h};
+  int rc = batch_upload(d.b, hs, err);
+  if (rc) return rc;
+  d.rank = rank;
+  d.world = world;
+  d.K = d.b.h_hist[0].K;
+  d.kmax = level_kmax(d.K);
+  d.cb = lv_cfg_bytes(d.kmax);
+  if (d.b.forced[0]) { err = "history is structurally illegal (unmatched events)"; return S2LC_EINVAL; }
+  if (level_buffers(d.b, d.kmax, err)) return S2LC_EHIP;
+  LVCHK(hipMalloc(&d.own_cnt, 8 * sizeof(uint32_t)));
+  LVCHK(hipMalloc(&d.own_pos, (size_t)d.b.lv.scap * sizeof(uint32_t)));
+  size_t free_b = 0, total_b = 0;
+  LVCHK(hipMemGetInfo(&free_b, &total_b));
+  d.trace_cap = std::min<uint64_t>(1ull << 29, (uint64_t)(free_b / 16) / sizeof(TraceEnt));
+  LVCHK(hipMalloc(&d.trace, d.trace_cap * sizeof(TraceEnt)));
+  LVCHK(hipStreamCreateWithFlags(&d.stream, hipStreamNonBlocking));
+  d.round = 0;
+  return 0;
+}
+
+void dist_release(DistLevel& d) {
+  if (d.own_cnt) (void)hipFree(d.own_cnt);
+  if (d.own_pos) (void)hipFree(d.own_pos);
+  if (d.trace) (void)hipFree(d.trace);
+  if (d.stream) (void)hipStreamDestroy(d.stream);
+  d.own_cnt = nullptr; d.own_pos = nullptr; d.trace = nullptr; d.stream = nullptr;
+  batch_release(d.b);
+}
+
+static LvParams dist_params(DistLevel& d) {
+  LevelBufs& L = d.b.lv;
+  const HistDesc& hd = d.b.h_hist[0];
+  LvParams p;
+  memset(&p, 0, sizeof p);
+  p.recs = d.b.recs; p.pool = d.b.pool; p.cs = d.b.chain_start + hd.cs_base; p.K = d.K; p.hflags = hd.flags;
+  p.child = reinterpret_cast<LChild*>(L.child); p.ccap = L.ccap; p.scap = L.scap;
+  p.ht = L.ht; p.ht_mask = L.ht_mask;
+  p.trace = d.trace; p.ctl = reinterpret_cast<LvCtl*>(L.ctl);
+  p.world = d.world; p.own_cnt = d.own_cnt; p.own_pos = d.own_pos;
+  p.stg = L.stg[0];  // local staging (the closed children of this rank)
+  p.cur = d.cur; p.cur_idx = L.idx[d.cur_sel];
+  p.tgid = d.rank << 29;
+  return p;
+}
+
+int dist_expand(DistLevel& d, uint64_t* counts, int* found, std::string& err) {
+  LevelBufs& L = d.b.lv;
+  LvCtl* hc = reinterpret_cast<LvCtl*>(L.h_ctl);
+  int dev = 0;
+  LVCHK(hipGetDevice(&dev));
+  int n_cu = 256;
+  (void)hipDeviceGetAttribute(&n_cu, hipDeviceAttributeMultiprocessorCount, dev);
+  const uint32_t max_grid = (uint32_t)n_cu * 8;
+  hipStream_t st = d.stream;
+  LvParams p = dist_params(d);
+  hipEvent_t e0, e1;
+  LVCHK(hipEventCreate(&e0));
+  LVCHK(hipEventCreate(&e1));
+  LVCHK(hipEventRecord(e0, st));
+  memset(hc, 0, sizeof(LvCtl));
+  LVCHK(hipMemsetAsync(d.own_cnt, 0, 8 * sizeof(uint32_t), st));
+  if (d.round == 0) {
+    // the initial configuration: closed on rank 0 only
+    if (d.rank == 0) {
+      hc->nchild = 1;
+      const LChild c0{0, 0, 0, LV_NONE, LV_NONE, 0};
+      LVCHK(hipMemcpyAsync(L.child, &c0, sizeof c0, hipMemcpyHostToDevice, st));
+    }
+    LVCHK(hipMemcpyAsync(L.ctl, hc, sizeof(LvCtl), hipMemcpyHostToDevice, st));
+    if (d.rank == 0) LVCHK(lv_dispatch(d.kmax, 1, 1, p, st));
+  } else {
+    LVCHK(hipMemcpyAsync(L.ctl, hc, sizeof(LvCtl), hipMemcpyHostToDevice, st));
+    if (d.nf) {
+      p.f0 = 0; p.f1 = d.nf; p.clear_slots = 1;
+      const uint64_t lanes = (uint64_t)d.nf * d.K;
+      const uint64_t kids_ub = std::min<uint64_t>(2 * lanes, L.ccap);
+      LVCHK(lv_dispatch(d.kmax, 0, (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>(max_grid, (lanes + LV_BLOCK - 1) / LV_BLOCK)), p, st));
+      LVCHK(lv_dispatch(d.kmax, 1, (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>(max_grid, (kids_ub + 3) / 4)), p, st));
+    }
+  }
+  // ownership buckets
+  const uint32_t g_b = max_grid;
+  LVCHK(lv_dispatch(d.kmax, 3, g_b, p, st));
+  uint32_t cnt[8] = {0};
+  LVCHK(hipMemcpyAsync(cnt, d.own_cnt, sizeof cnt, hipMemcpyDeviceToHost, st));
+  LVCHK(hipMemcpyAsync(hc, L.ctl, sizeof(LvCtl), hipMemcpyDeviceToHost, st));
+  LVCHK(hipEventRecord(e1, st));
+  LVCHK(hipStreamSynchronize(st));
+  float ms = 0;
+  LVCHK(hipEventElapsedTime(&ms, e0, e1));
+  (void)hipEventDestroy(e0);
+  (void)hipEventDestroy(e1);
+  d.ms += ms;
+  if (hc->overflow) { err = "distributed round exceeds the device buffers"; return S2LC_ENOMEM; }
+  d.children += std::min(hc->nchild, L.ccap);
+  d.nstage = std::min(hc->nstage, L.scap);
+  for (uint32_t o = 0; o < d.world; ++o) counts[o] = cnt[o];
+  *found = hc->found ? 1 : 0;
+  if (hc->found) { d.found_parent = hc->found_parent; d.found_move = hc->found_move; d.found_p4 = hc->found_p4; }
+  return 0;
+}
+
+int dist_pack(DistLevel& d, uint8_t* send, const uint64_t* counts, std::string& err) {
+  LvParams p = dist_params(d);
+  uint64_t off = 0;
+  for (uint32_t o = 0; o < d.world; ++o) { p.own_off[o] = off; off += counts[o]; }
+  if (off != d.nstage) { err = "bucket counts do not match the staged configurations"; return S2LC_EINVAL; }
+  p.send = send;
+  if (d.nstage) {
+    const uint64_t pieces = (uint64_t)d.nstage * (d.cb / 16);
+    LVCHK(lv_dispatch(d.kmax, 4, (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>(2048, (pieces + LV_BLOCK - 1) / LV_BLOCK)), p, d.stream));
+  }
+  LVCHK(hipStreamSynchronize(d.stream));
+  return 0;
+}
+
+int dist_insert(DistLevel& d, uint8_t* recv, uint64_t n_recv, uint64_t* n_next, std::string& err) {
+  LevelBufs& L = d.b.lv;
+  LvCtl* hc = reinterpret_cast<LvCtl*>(L.h_ctl);
+  if (n_recv > L.scap) { err = "received configurations exceed the frontier capacity"; return S2LC_ENOMEM; }
+  hipStream_t st = d.stream;
+  const int sel = d.cur_sel ^ 1;
+  LvParams p = dist_params(d);
+  p.stg = recv; p.nxt_idx = L.idx[sel]; p.st_lo = 0;
+  p.witness = 1;
+  if (d.tnext + n_recv > d.trace_cap) { err = "trace pool full"; return S2LC_ENOMEM; }
+  p.tbase = (uint32_t)d.tnext;
+  memset(hc, 0, sizeof(LvCtl));
+  hc->nstage = (uint32_t)n_recv;
+  hipEvent_t e0, e1;
+  LVCHK(hipEventCreate(&e0));
+  LVCHK(hipEventCreate(&e1));
+  LVCHK(hipEventRecord(e0, st));
+  LVCHK(hipMemcpyAsync(L.ctl, hc, sizeof(LvCtl), hipMemcpyHostToDevice, st));
+  if (n_recv) {
+    int dev = 0, n_cu = 256;
+    LVCHK(hipGetDevice(&dev));
+    (void)hipDeviceGetAttribute(&n_cu, hipDeviceAttributeMultiprocessorCount, dev);
+    LVCHK(lv_dispatch(d.kmax, 2, (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>((uint64_t)n_cu * 8, (n_recv + LV_BLOCK - 1) / LV_BLOCK)), p, st));
+  }
+  LVCHK(hipMemcpyAsync(hc, L.ctl, sizeof(LvCtl), hipMemcpyDeviceToHost, st));
+  LVCHK(hipEventRecord(e1, st));
+  LVCHK(hipStreamSynchronize(st));
+  float ms = 0;
+  LVCHK(hipEventElapsedTime(&ms, e0, e1));
+  (void)hipEventDestroy(e0);
+  (void)hipEventDestroy(e1);
+  d.ms += ms;
+  d.cur = recv;
+  d.cur_sel = sel;
+  d.nf = hc->nnext;
+  d.tnext += hc->nnext;
+  d.configs += hc->nnext;
+  d.max_frontier = std::max<uint64_t>(d.max_frontier, hc->nnext);
+  d.round++;
+  *n_next = hc->nnext;
+  return 0;
+}
+
+int dist_trace(DistLevel& d, uint32_t* out, uint64_t cap, uint64_t* n, std::string& err) {
+  *n = d.tnext;
+  if (!out) return 0;
+  if (cap < d.tnext) { err = "trace buffer too small"; return S2LC_EINVAL; }
+  if (d.tnext) LVCHK(hipMemcpy(out, d.trace, d.tnext * sizeof(TraceEnt), hipMemcpyDeviceToHost));
   return 0;
 }
 

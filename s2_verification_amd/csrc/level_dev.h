@@ -89,9 +89,16 @@ struct LvParams {
   uint32_t ht_mask;
   uint32_t clear_slots;  // lv_expand clears the table slots of the frontier it expands
   TraceEnt* trace;
-  uint32_t tbase;        // trace index of nxt_idx[0]
+  uint32_t tbase;        // trace index of nxt_idx[0] (in this process's pool)
   uint32_t witness;
+  uint32_t tgid;         // added to pool indices to form trace ids (distributed: rank << 29)
   LvCtl* ctl;
+  // distributed search: ownership buckets of the staged configurations
+  uint32_t world;
+  uint32_t* own_cnt;     // [world] configurations per owner rank
+  uint32_t* own_pos;     // per staged configuration: owner << 27 | position within the owner's bucket
+  uint8_t* send;         // bucketed configurations, owner-major
+  uint64_t own_off[8];   // first configuration of each owner's bucket in send
 };
 
 template <int KMAX>
@@ -368,10 +375,42 @@ __global__ __launch_bounds__(LV_BLOCK) void lv_insert(LvParams p) {
       p.nxt_idx[n] = k;
       c->slot = slot;
       if (p.witness) {
-        c->trace = p.tbase + n;
+        c->trace = p.tgid + p.tbase + n;
         p.trace[p.tbase + n] = TraceEnt{c->ptrace, c->move};
       }
     }
+  }
+}
+
+// ---- distributed: owner of a configuration ---------------------------------
+// Independent of the table slot (low fingerprint bits) and tag (high bits).
+__host__ __device__ __forceinline__ uint32_t lv_owner(uint64_t fp, uint32_t world) {
+  return (uint32_t)(((fp * 0xD6E8FEB86659FD93ull) >> 40) % world);
+}
+
+// one lane per staged configuration: owner bucket and position within it
+template <int KMAX>
+__global__ __launch_bounds__(LV_BLOCK) void lv_bucket(LvParams p) {
+  const uint32_t n = min(p.ctl->nstage, p.scap);
+  for (uint32_t k = blockIdx.x * LV_BLOCK + threadIdx.x; k < n; k += gridDim.x * LV_BLOCK) {
+    const uint32_t o = lv_owner(lv_cfg<KMAX>(p.stg, k)->fp, p.world);
+    const uint32_t pos = atomicAdd(&p.own_cnt[o], 1u);
+    p.own_pos[k] = (o << 27) | pos;
+  }
+}
+
+// one lane per 16-byte piece: copy staged configurations into their owner's bucket
+template <int KMAX>
+__global__ __launch_bounds__(LV_BLOCK) void lv_scatter(LvParams p) {
+  constexpr uint32_t PER = sizeof(LCfg<KMAX>) / 16;
+  const uint32_t n = min(p.ctl->nstage, p.scap);
+  const uint64_t total = (uint64_t)n * PER;
+  for (uint64_t i = (uint64_t)blockIdx.x * LV_BLOCK + threadIdx.x; i < total; i += (uint64_t)gridDim.x * LV_BLOCK) {
+    const uint32_t k = (uint32_t)(i / PER), c = (uint32_t)(i % PER);
+    const uint32_t op = p.own_pos[k];
+    const uint64_t dst = p.own_off[op >> 27] + (op & ((1u << 27) - 1));
+    const uint4* src = reinterpret_cast<const uint4*>(lv_cfg<KMAX>(p.stg, k));
+    reinterpret_cast<uint4*>(p.send + dst * sizeof(LCfg<KMAX>))[c] = src[c];
   }
 }
 

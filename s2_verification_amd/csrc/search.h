@@ -129,6 +129,30 @@ int level_search(DevBatch& b, uint32_t h, hipStream_t st, uint64_t max_configs, 
                  std::string& err);
 void level_release(DevBatch& b);
 
+// One rank's part of the distributed level search of a single history.
+struct DistLevel {
+  DevBatch b;                    // the history (one entry) + level buffers
+  uint32_t rank = 0, world = 1, K = 0, kmax = 0;
+  size_t cb = 0;                 // bytes per configuration on the wire
+  uint32_t* own_cnt = nullptr;
+  uint32_t* own_pos = nullptr;
+  TraceEnt* trace = nullptr;     // this rank's trace pool
+  uint64_t trace_cap = 0, tnext = 0;
+  hipStream_t stream = nullptr;
+  const uint8_t* cur = nullptr;  // current frontier: received buffer (caller-owned)
+  int cur_sel = 0;               // index list of the current frontier: b.lv.idx[cur_sel]
+  uint32_t nf = 0, nstage = 0, round = 0;
+  uint32_t found_parent = TRACE_NONE, found_move = TRACE_NONE, found_p4 = 0;
+  uint64_t configs = 0, children = 0, max_frontier = 0;
+  double ms = 0;
+};
+int dist_create(DistLevel& d, const History* h, uint32_t rank, uint32_t world, std::string& err);
+void dist_release(DistLevel& d);
+int dist_expand(DistLevel& d, uint64_t* counts, int* found, std::string& err);
+int dist_pack(DistLevel& d, uint8_t* send, const uint64_t* counts, std::string& err);
+int dist_insert(DistLevel& d, uint8_t* recv, uint64_t n_recv, uint64_t* n_next, std::string& err);
+int dist_trace(DistLevel& d, uint32_t* out, uint64_t cap, uint64_t* n, std::string& err);
+
 // Host reconstruction of a full linearization (dense op ids) from the device
 // move list; returns false if any move is not a legal successor.
 // ident[i] = 1 when order[i] took its identity outcome (E ops, indefinite

@@ -1,0 +1,234 @@
+"""Distributed search of ONE history across GPUs (BASELINE config C5).
+
+One process per GPU. Configurations are hash-partitioned by fingerprint
+(`lv_owner` in csrc/level_dev.h); each round every rank expands and closes its
+own frontier on its GPU (libs2lincheck: s2lc_dist_expand / s2lc_dist_pack),
+the closed children travel to their owner rank in ONE all-to-all(v) over
+torch.distributed (backend "nccl" = RCCL over xGMI on MI355X), and the owner
+deduplicates them in its HBM table (s2lc_dist_insert). Per round there are two
+collectives: a small all-to-all of (count, found, staged total) triples, which
+also carries termination (Ok anywhere / nothing staged anywhere = Illegal), and
+the payload all-to-all. The gloo backend works too (payload staged through host
+memory), which is how the protocol is tested with several ranks on one GPU.
+
+This replaces porcupine.CheckEventsVerbose (golang/s2-porcupine/main.go:606)
+for a single history too large for one device's search; the verdict is the
+same question and the Ok witness is rebuilt from the ranks' trace pools and
+certified through the CPU model (s2lc_witness_from_moves).
+"""
+import ctypes
+import time
+from dataclasses import dataclass, field
+from typing import List, Optional
+
+import numpy as np
+import torch
+import torch.distributed as dist
+
+from . import History, Ok, Illegal, S2LCError, c_dist_info, lib
+
+_NONE = 0xFFFFFFFF
+_RANK_SHIFT = 29
+
+
+@dataclass
+class DistResult:
+    verdict: str
+    rounds: int
+    configs: int             # unique configurations, all ranks
+    children: int            # children generated, all ranks
+    max_frontier: int        # largest per-rank frontier
+    device_ms: float         # max over ranks of the kernels' device time
+    wall_s: float            # the search loop (all ranks in lockstep)
+    exchanged_bytes: int     # payload bytes this rank sent to other ranks
+    witness: Optional[List[int]] = None
+    witness_valid: Optional[bool] = None
+    per_rank_configs: List[int] = field(default_factory=list)
+
+
+class DistSearch:
+    """One rank's share of the search (an s2lc_dist)."""
+
+    def __init__(self, checker, history: History, rank: int, world: int):
+        self._d = ctypes.c_void_p()
+        rc = lib().s2lc_dist_create(checker._ctx, history._h, rank, world, ctypes.byref(self._d))
+        if rc:
+            raise S2LCError(rc, checker.last_error())
+        self.checker = checker
+        self.rank, self.world = rank, world
+
+    def close(self):
+        if self._d:
+            lib().s2lc_dist_free(self._d)
+            self._d = ctypes.c_void_p()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def _chk(self, rc, what):
+        if rc:
+            raise S2LCError(rc, f"{what}: {self.checker.last_error()}")
+
+    def info(self) -> c_dist_info:
+        i = c_dist_info()
+        self._chk(lib().s2lc_dist_info(self._d, ctypes.byref(i)), "dist_info")
+        return i
+
+    def expand(self):
+        counts = (ctypes.c_uint64 * self.world)()
+        found = ctypes.c_int32(0)
+        self._chk(lib().s2lc_dist_expand(self._d, counts, ctypes.byref(found)), "dist_expand")
+        return list(counts), bool(found.value)
+
+    def pack(self, send: torch.Tensor, counts):
+        c = (ctypes.c_uint64 * self.world)(*counts)
+        self._chk(lib().s2lc_dist_pack(self._d, ctypes.c_void_p(send.data_ptr() if send.numel() else 0), c),
+                  "dist_pack")
+
+    def insert(self, recv: torch.Tensor, n: int) -> int:
+        nn = ctypes.c_uint64(0)
+        self._chk(lib().s2lc_dist_insert(self._d, ctypes.c_void_p(recv.data_ptr() if n else 0), n,
+                                         ctypes.byref(nn)), "dist_insert")
+        return nn.value
+
+    def trace(self) -> np.ndarray:
+        n = ctypes.c_uint64(0)
+        self._chk(lib().s2lc_dist_trace(self._d, None, 0, ctypes.byref(n)), "dist_trace")
+        out = np.zeros((max(1, n.value), 2), dtype=np.uint32)
+        self._chk(lib().s2lc_dist_trace(self._d, ctypes.c_void_p(out.ctypes.data), n.value, ctypes.byref(n)),
+                  "dist_trace")
+        return out[:n.value]
+
+
+class _Exchange:
+    """The two collectives of a round, on CUDA tensors (nccl/RCCL) or staged
+    through host memory (gloo)."""
+
+    def __init__(self, group, device: torch.device):
+        self.group = group
+        self.device = device
+        self.on_gpu = dist.get_backend(group) == "nccl"
+        self.tdev = device if self.on_gpu else torch.device("cpu")
+        self.world = dist.get_world_size(group)
+
+    def counts(self, counts, found: bool, staged: int):
+        """All-to-all of (count for the receiver, found, staged total) triples."""
+        w = self.world
+        send = torch.tensor([[c, int(found), staged] for c in counts], dtype=torch.int64, device=self.tdev)
+        recv = torch.empty((w, 3), dtype=torch.int64, device=self.tdev)
+        dist.all_to_all_single(recv, send, group=self.group)
+        r = recv.cpu().tolist()
+        return [x[0] for x in r], any(x[1] for x in r), sum(x[2] for x in r)
+
+    def payload(self, send: torch.Tensor, in_bytes, out_bytes) -> torch.Tensor:
+        total = int(sum(out_bytes))
+        if self.on_gpu:
+            recv = torch.empty(max(total, 1), dtype=torch.uint8, device=self.device)
+            dist.all_to_all_single(recv[:total] if total else recv[:0], send, out_bytes, in_bytes, group=self.group)
+            torch.cuda.current_stream(self.device).synchronize()  # the library reads recv on its own stream
+            return recv
+        recv_h = torch.empty(total, dtype=torch.uint8)
+        dist.all_to_all_single(recv_h, send.cpu(), out_bytes, in_bytes, group=self.group)
+        recv = recv_h.to(self.device) if total else torch.empty(1, dtype=torch.uint8, device=self.device)
+        torch.cuda.current_stream(self.device).synchronize()
+        return recv
+
+    def gather_small(self, vals: List[int]) -> List[List[int]]:
+        t = torch.tensor(vals, dtype=torch.int64, device=self.tdev)
+        out = [torch.empty_like(t) for _ in range(self.world)]
+        dist.all_gather(out, t, group=self.group)
+        return [o.cpu().tolist() for o in out]
+
+    def gather_traces(self, tr: np.ndarray) -> List[np.ndarray]:
+        n = self.gather_small([len(tr)])
+        m = max(x[0] for x in n)
+        buf = torch.zeros((max(m, 1), 2), dtype=torch.int64, device=self.tdev)
+        if len(tr):
+            buf[:len(tr)] = torch.from_numpy(tr.astype(np.int64)).to(self.tdev)
+        out = [torch.empty_like(buf) for _ in range(self.world)]
+        dist.all_gather(out, buf, group=self.group)
+        return [o[:x[0]].cpu().numpy().astype(np.uint32) for o, x in zip(out, n)]
+
+
+def _walk(traces: List[np.ndarray], parent: int, move: int) -> Optional[List[int]]:
+    """Moves from the root to the completing child (trace ids cross ranks)."""
+    if move == _NONE:
+        return []
+    moves = [move]
+    idx = parent
+    mask = (1 << _RANK_SHIFT) - 1
+    steps = 0
+    while idx != _NONE:
+        r, i = idx >> _RANK_SHIFT, idx & mask
+        if r >= len(traces) or i >= len(traces[r]):
+            return None
+        p, m = int(traces[r][i][0]), int(traces[r][i][1])
+        if m != _NONE:
+            moves.append(m)
+        idx = p
+        steps += 1
+        if steps > (1 << 26):
+            return None
+    moves.reverse()
+    return moves
+
+
+def check_distributed(checker, history: History, group=None, witness: bool = True) -> DistResult:
+    """Check one history with every rank of `group` (default: the world)."""
+    rank = dist.get_rank(group)
+    world = dist.get_world_size(group)
+    device = torch.device("cuda", torch.cuda.current_device())
+    ex = _Exchange(group, device)
+    ds = DistSearch(checker, history, rank, world)
+    cb = ds.info().config_bytes
+    cur = None  # the received buffer holding this rank's frontier (kept alive)
+    verdict = None
+    sent_bytes = 0
+    t0 = time.perf_counter()
+    try:
+        while verdict is None:
+            counts, found = ds.expand()
+            recv_counts, found_any, staged_total = ex.counts(counts, found, sum(counts))
+            if found_any:
+                verdict = Ok
+                break
+            if staged_total == 0:
+                verdict = Illegal
+                break
+            send = torch.empty(max(1, sum(counts) * cb), dtype=torch.uint8, device=device)
+            ds.pack(send, counts)
+            in_b = [c * cb for c in counts]
+            out_b = [c * cb for c in recv_counts]
+            sent_bytes += sum(b for w, b in enumerate(in_b) if w != rank)
+            recv = ex.payload(send[:sum(in_b)], in_b, out_b)
+            ds.insert(recv, sum(recv_counts))
+            cur = recv  # noqa: F841  (frontier storage for the next expand)
+        wall = time.perf_counter() - t0
+        info = ds.info()
+        stats = ex.gather_small([int(found and verdict == Ok), info.found_parent, info.found_move, info.found_p4,
+                                 info.configs, info.children, info.max_frontier, int(info.device_ms * 1e3),
+                                 info.round])
+        res = DistResult(verdict=verdict, rounds=max(s[8] for s in stats),
+                         configs=sum(s[4] for s in stats), children=sum(s[5] for s in stats),
+                         max_frontier=max(s[6] for s in stats), device_ms=max(s[7] for s in stats) / 1e3,
+                         wall_s=wall, exchanged_bytes=sent_bytes, per_rank_configs=[s[4] for s in stats])
+        if verdict == Ok and witness:
+            src = next(s for s in stats if s[0])
+            traces = ex.gather_traces(ds.trace())
+            moves = _walk(traces, src[1], src[2])
+            ok = False
+            ids = None
+            if moves is not None:
+                n_ops = history.info()["n_ops"]
+                mv = (ctypes.c_uint32 * max(1, len(moves)))(*moves)
+                out = (ctypes.c_int64 * max(1, n_ops))()
+                ok = lib().s2lc_witness_from_moves(history._h, mv, len(moves), src[3], out, n_ops) == 0
+                ids = list(out[:n_ops]) if ok else None
+            res.witness, res.witness_valid = ids, ok
+        return res
+    finally:
+        ds.close()
+        del cur

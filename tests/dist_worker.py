@@ -1,0 +1,56 @@
+"""Worker processes for the multi-rank tests (spawned; one per rank)."""
+import os
+import sys
+import traceback
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+for p in (ROOT, os.path.join(ROOT, "oracle"), os.path.join(ROOT, "tests")):
+    if p not in sys.path:
+        sys.path.insert(0, p)
+
+
+def _init(rank, world, port, backend):
+    import torch.distributed as dist
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group(backend, rank=rank, world_size=world)
+    return dist
+
+
+def exchange_worker(rank, world, port, q):
+    """CPU (gloo): the round's small all-to-all and the trace gather."""
+    try:
+        import numpy as np
+        import torch
+        from s2_verification_amd.distributed import _Exchange, _walk
+        dist = _init(rank, world, port, "gloo")
+        ex = _Exchange(None, torch.device("cpu"))
+        counts = [10 * rank + w for w in range(world)]  # rank -> w
+        recv, found_any, staged = ex.counts(counts, rank == world - 1, sum(counts))
+        tr = np.array([[0xFFFFFFFF, 0xFFFFFFFF], [(rank << 29) | 0, rank + 1]], dtype=np.uint32)
+        traces = ex.gather_traces(tr)
+        q.put((rank, recv, found_any, staged, [t.tolist() for t in traces]))
+        dist.destroy_process_group()
+    except Exception:
+        q.put((rank, "error", traceback.format_exc()))
+
+
+def search_worker(rank, world, port, backend, names, q):
+    """GPU: every rank checks the named histories with check_distributed."""
+    try:
+        import torch
+        import s2_verification_amd as s2
+        from s2_verification_amd import workloads as W
+        from s2_verification_amd.distributed import check_distributed
+        torch.cuda.set_device(0 if backend == "gloo" else rank)
+        dist = _init(rank, world, port, backend)
+        checker = s2.Checker(device=torch.cuda.current_device())
+        out = []
+        for name in names:
+            h = W.config_history(name)
+            r = check_distributed(checker, h)
+            out.append((name, r.verdict, r.rounds, r.configs, r.witness_valid,
+                        None if r.witness is None else len(r.witness), h.info()["n_ops"]))
+        q.put((rank, out))
+        dist.destroy_process_group()
+    except Exception:
+        q.put((rank, "error", traceback.format_exc()))

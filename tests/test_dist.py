@@ -1,0 +1,68 @@
+"""Multi-rank tests of the distributed single-history search (s2_verification_amd.distributed).
+
+CPU (gloo, world 2): the per-round small all-to-all (counts, found, staged
+totals) and the trace gather + cross-rank witness walk.
+GPU (one MI355X): world 1 and world 2 with both ranks on the same GPU over
+gloo (host-staged payload): verdicts equal the committed reduced-search
+verdicts, Ok witnesses certified through the CPU model. The RCCL transport
+differs only in where the two all-to-alls run (same calls on CUDA tensors).
+"""
+import multiprocessing as mp
+import random
+
+import pytest
+
+from helpers import golden
+
+
+def _spawn(target, args_per_rank, timeout=600):
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    ps = [ctx.Process(target=target, args=a + (q,)) for a in args_per_rank]
+    for p in ps:
+        p.start()
+    out = [q.get(timeout=timeout) for _ in ps]
+    for p in ps:
+        p.join(timeout=60)
+    for o in out:
+        assert o[1] != "error", o[2]
+    return sorted(out, key=lambda o: o[0])
+
+
+def test_exchange_gloo_world2():
+    import dist_worker
+    port = random.randint(20000, 40000)
+    out = _spawn(dist_worker.exchange_worker, [(r, 2, port) for r in range(2)], timeout=120)
+    for rank, recv, found_any, staged, traces in out:
+        assert recv == [10 * s + rank for s in range(2)]  # what each source sent to me
+        assert found_any is True
+        assert staged == sum(10 * s + w for s in range(2) for w in range(2))
+        assert traces == [[[0xFFFFFFFF, 0xFFFFFFFF], [(s << 29), s + 1]] for s in range(2)]
+
+
+def test_walk_crosses_ranks():
+    import numpy as np
+    from s2_verification_amd.distributed import _walk
+    N = 0xFFFFFFFF
+    t0 = np.array([[N, N], [(1 << 29) | 0, 5]], dtype=np.uint32)       # rank 0: root, then (parent r1#0, move 5)
+    t1 = np.array([[0, 3]], dtype=np.uint32)                          # rank 1: (parent r0#0, move 3)
+    assert _walk([t0, t1], parent=1, move=7) == [3, 5, 7]
+    assert _walk([t0, t1], parent=N, move=N) == []
+    assert _walk([t0, t1], parent=(2 << 29), move=1) is None
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("world", [1, 2])
+def test_distributed_search_one_gpu(world):
+    import dist_worker
+    ref = golden("hard_reduced.json")
+    names = [n for n in ("H174", "C5bad", "H212") if n in ref]
+    port = random.randint(20000, 40000)
+    out = _spawn(dist_worker.search_worker, [(r, world, port, "gloo", names) for r in range(world)])
+    for rank, res in out:
+        for name, verdict, rounds, configs, wvalid, wlen, n_ops in res:
+            assert verdict == ref[name]["verdict"], (rank, name, verdict)
+            if verdict == "Ok":
+                assert wvalid and wlen == n_ops, (rank, name, wvalid, wlen)
+    # every rank agrees
+    assert len({tuple(r) for _, res in out for r in res}) == len(names)
