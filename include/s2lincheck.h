@@ -202,6 +202,12 @@ typedef struct s2lc_batch_stats {
   uint64_t level_rounds;
   uint64_t level_configs;
   uint64_t level_children;
+  /* the dominant kernel of small-history batches: pack_kernel<16> (one 16-lane
+   * group per history with <= 16 chains) */
+  double pack16_ms;          /* its launch, HIP events on the ctx stream */
+  uint64_t pack16_algo_bytes;/* algorithmic bytes of the histories it settled */
+  uint32_t pack16_histories;
+  uint32_t _pad1;
 } s2lc_batch_stats;
 int s2lc_batch_stats_get(const s2lc_batch* b, s2lc_batch_stats* out);
 

@@ -1,11 +1,12 @@
-"""Summarise rocprofv3 PMC passes for the search kernel into profiles/pmc_c4.json.
+"""Summarise rocprofv3 PMC passes for one kernel into profiles/pmc_c4.json.
 
-Usage: python profiles/pmc_summary.py <fetch_dir> <write_dir> <out.json>
+Usage: python profiles/pmc_summary.py <fetch_dir> <write_dir> <out.json> [kernel]
+(kernel: a substring of the kernel name, default "pack_kernel<16>")
 
 HBM bytes per launch = (2 * FETCH_SIZE + WRITE_SIZE) * 1024, following
 MI355X_MICROARCH.md §HBM: FETCH_SIZE (KiB) counts 64 B per 128-B request for
 wide coalesced reads on gfx950, so it is doubled; WRITE_SIZE is taken as is.
-Both are averaged over the search_kernel dispatches of the run.
+Both are averaged over the dispatches of that kernel in the run.
 """
 import csv
 import glob
@@ -15,12 +16,12 @@ import sys
 from collections import defaultdict
 
 
-def per_dispatch(d, counter):
+def per_dispatch(d, counter, kernel):
     vals = defaultdict(float)
     for path in glob.glob(os.path.join(d, "**", "*counter_collection.csv"), recursive=True):
         with open(path) as f:
             for row in csv.DictReader(f):
-                if "search_kernel" not in row.get("Kernel_Name", ""):
+                if kernel not in row.get("Kernel_Name", ""):
                     continue
                 if row.get("Counter_Name") != counter:
                     continue
@@ -30,14 +31,15 @@ def per_dispatch(d, counter):
 
 def main():
     fetch_dir, write_dir, out = sys.argv[1:4]
-    fetch = per_dispatch(fetch_dir, "FETCH_SIZE")
-    write = per_dispatch(write_dir, "WRITE_SIZE")
+    kernel = sys.argv[4] if len(sys.argv) > 4 else "pack_kernel<16>"
+    fetch = per_dispatch(fetch_dir, "FETCH_SIZE", kernel)
+    write = per_dispatch(write_dir, "WRITE_SIZE", kernel)
     if not fetch or not write:
-        raise SystemExit(f"no search_kernel counters found (fetch={len(fetch)}, write={len(write)})")
+        raise SystemExit(f"no {kernel} counters found (fetch={len(fetch)}, write={len(write)})")
     f = sum(fetch) / len(fetch)
     w = sum(write) / len(write)
     res = {
-        "kernel": "search_kernel",
+        "kernel": kernel,
         "dispatches": {"fetch_pass": len(fetch), "write_pass": len(write)},
         "FETCH_SIZE_KiB": f, "WRITE_SIZE_KiB": w,
         "hbm_bytes_per_launch": int((2 * f + w) * 1024),

@@ -369,6 +369,9 @@ int s2lc_batch_stats_get(const s2lc_batch* b, s2lc_batch_stats* out) {
   out->level_rounds = b->stats.level.rounds;
   out->level_configs = b->stats.level.configs;
   out->level_children = b->stats.level.children;
+  out->pack16_ms = b->stats.pack16_ms;
+  out->pack16_algo_bytes = b->stats.pack16_algo_bytes;
+  out->pack16_histories = b->stats.pack16_histories;
   return 0;
 }
 

@@ -86,6 +86,8 @@ struct DevBatch {
   HistDesc* hist = nullptr;
   uint32_t* order = nullptr;        // LPT processing order: [K<=16 | K<=32 | rest]
   uint32_t n_pack16 = 0, n_pack32 = 0;
+  std::vector<uint8_t> in_pack16;   // per history: in the pack_kernel<16> list
+  std::vector<uint64_t> h_in_bytes; // per history: input SoA bytes (48 per op + 8 per record hash)
   std::vector<uint32_t> h_rest;     // histories searched one per workgroup (32 < K <= 128)
   std::vector<uint32_t> h_level;    // histories searched by the device-wide level search (K > 128)
   LevelBufs lv;
@@ -115,6 +117,9 @@ struct RunStats {
   uint64_t algo_bytes = 0;
   uint32_t n_overflow = 0, launches = 0;
   double pack_ms = 0;
+  double pack16_ms = 0;              // pack_kernel<16> launch (HIP events)
+  uint64_t pack16_algo_bytes = 0;    // algorithmic bytes of the histories it settled
+  uint32_t pack16_histories = 0;
   LevelStats level;
 };
 

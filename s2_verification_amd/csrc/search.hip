@@ -125,6 +125,7 @@ int batch_upload(DevBatch& b, const std::vector<const History*>& hs, std::string
   uint64_t moves_total = 0;
   b.h_hist.resize(hs.size());
   b.h_moves_off.resize(hs.size());
+  b.h_in_bytes.assign(hs.size(), 0);
   for (size_t i = 0; i < hs.size(); ++i) {
     const History& h = *hs[i];
     if (h.status != 0) { err = "history " + std::to_string(i) + ": " + h.error; return h.status; }
@@ -143,8 +144,10 @@ int batch_upload(DevBatch& b, const std::vector<const History*>& hs, std::string
     n_pool += h.pool.size();
     b.h_moves_off[i] = (uint32_t)moves_total;
     moves_total += h.n_ops + 1;
-    b.algo_bytes_inputs += 48ull * h.n_ops;
-    for (const OpRec& r : h.recs) b.algo_bytes_inputs += 8ull * r.hash_cnt;
+    uint64_t in_bytes = 48ull * h.n_ops;
+    for (const OpRec& r : h.recs) in_bytes += 8ull * r.hash_cnt;
+    b.h_in_bytes[i] = in_bytes;
+    b.algo_bytes_inputs += in_bytes;
   }
   if (n_recs >= 0xFFFFFFFFull || n_pool >= 0xFFFFFFFFull || moves_total >= 0xFFFFFFFFull) {
     err = "batch too large for 32-bit indices";
@@ -188,6 +191,8 @@ int batch_upload(DevBatch& b, const std::vector<const History*>& hs, std::string
       else (K <= 16 ? l16 : K <= 32 ? l32 : K <= 128 ? rest : b.h_level).push_back(i);
     }
     b.n_pack16 = (uint32_t)l16.size();
+    b.in_pack16.assign(hs.size(), 0);
+    for (uint32_t i : l16) b.in_pack16[i] = 1;
     b.n_pack32 = (uint32_t)l32.size();
     b.h_rest = rest;
     order = l16;
@@ -277,6 +282,10 @@ int batch_run(DevBatch& b, hipStream_t stream, uint64_t max_configs, bool witnes
   // what the kernel's register occupancy allows (16 / 12 workgroups per CU for
   // KMAX 16 / 32), so LDS never limits residency below the register limit.
   const bool use_pack = getenv("S2LC_NO_PACK") == nullptr;
+  // histories settled by pack_kernel<16> (roofline accounting of that kernel)
+  std::vector<uint8_t> pack16_done(b.n_hist, 0);
+  if (use_pack)
+    for (uint32_t i = 0; i < b.n_hist; ++i) pack16_done[i] = b.in_pack16[i];
   std::vector<uint32_t> todo;  // histories for the workgroup-per-history passes
   if (use_pack) {
     for (int li = 0; li < 2; ++li) {
@@ -304,6 +313,7 @@ int batch_run(DevBatch& b, hipStream_t stream, uint64_t max_configs, bool witnes
       HIPCHK(hipEventElapsedTime(&ms, e0, e1));
       st.kernel_ms += ms;
       st.pack_ms += ms;
+      if (li == 0) st.pack16_ms = ms;
       st.launches++;
     }
     if (b.n_pack16 + b.n_pack32) {
@@ -314,6 +324,7 @@ int batch_run(DevBatch& b, hipStream_t stream, uint64_t max_configs, bool witnes
       if (!b.forced[i] && b.h_hist[i].K <= 32 && b.h_res[i].verdict == V_UNKNOWN && b.h_res[i].reason == S2LC_R_FRONTIER)
         todo.push_back(i);
     st.n_overflow = (uint32_t)todo.size();
+    for (uint32_t i : todo) pack16_done[i] = 0;
     todo.insert(todo.end(), b.h_rest.begin(), b.h_rest.end());
   } else {
     std::vector<uint32_t> all(b.n_pack16 + b.n_pack32 + b.h_rest.size());
@@ -436,6 +447,11 @@ int batch_run(DevBatch& b, hipStream_t stream, uint64_t max_configs, bool witnes
     st.rounds += r.rounds;
     const uint64_t S = 8 * ((2 * (uint64_t)b.h_hist[i].K + 20 + 7) / 8);
     st.algo_bytes += 2 * S * r.configs + 8 * r.children;
+    if (pack16_done[i]) {
+      // pack_kernel<16> alone: its histories' search bytes + their input SoA
+      st.pack16_algo_bytes += 2 * S * r.configs + 8 * r.children + b.h_in_bytes[i];
+      st.pack16_histories++;
+    }
   }
   st.algo_bytes += b.algo_bytes_inputs;
   st.total_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
