@@ -194,7 +194,7 @@ __global__ __launch_bounds__(LV_BLOCK) void lv_expand(LvParams p) {
         if (r.flags & OPF_CLS_D) take_opt = g && opt.tail == r.out_tail;
         else take_opt = g;
         if (take_opt || (r.flags & OPF_CLS_I)) {
-          if (g) opt.hash = fold_hashes(s.hash, p.pool + r.hash_off, r.hash_cnt);
+          if (g) opt.hash = fold_hashes_blk(s.hash, p.pool + r.hash_off, r.hash_cnt);
         }
         if (r.flags & OPF_CLS_I) take_id = r.ret_ev == pmin && !(g && state_eq(opt, s));
         nk = (uint32_t)take_opt + (uint32_t)take_id;

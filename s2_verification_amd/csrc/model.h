@@ -74,6 +74,21 @@ __host__ __device__ inline uint64_t fold_hashes(uint64_t h, const uint64_t* rs, 
   return h;
 }
 
+// Device fold with the record-hash loads issued 8 at a time: the fold is a
+// dependent chain of multiplies, but its loads are independent, and a loop that
+// loads inside the chain pays one memory latency per record.
+__device__ inline uint64_t fold_hashes_blk(uint64_t h, const uint64_t* __restrict__ rs, uint32_t n) {
+  for (uint32_t b = 0; b < n; b += 8) {
+    uint64_t v[8];
+#pragma unroll
+    for (int q = 0; q < 8; ++q) v[q] = b + q < n ? rs[b + q] : 0;
+#pragma unroll
+    for (int q = 0; q < 8; ++q)
+      if (b + q < n) h = chain_hash(h, v[q]);
+  }
+  return h;
+}
+
 __host__ __device__ inline bool state_eq(const State& a, const State& b) {
   return a.tail == b.tail && a.hash == b.hash && a.tok == b.tok;
 }

@@ -58,19 +58,39 @@ __device__ __forceinline__ void wave_lds_sync() {
   __builtin_amdgcn_wave_barrier();
 }
 
+// Group min-reductions. A 16-lane group is one DPP row: quad_perm [1,0,3,2],
+// quad_perm [2,3,0,1], row_ror:4, row_ror:8 leave the row minimum in every
+// lane with VALU data-parallel moves (no LDS round trip, unlike ds_bpermute,
+// which __shfl_xor compiles to). A 32-lane group adds one bpermute (lane ^ 16).
+template <int CTRL>
+__device__ __forceinline__ uint32_t dpp_u32(uint32_t v) {
+  return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, CTRL, 0xF, 0xF, false);
+}
+template <int CTRL>
+__device__ __forceinline__ uint64_t dpp_min_u64(uint64_t v) {
+  const uint64_t w = ((uint64_t)dpp_u32<CTRL>((uint32_t)(v >> 32)) << 32) | dpp_u32<CTRL>((uint32_t)v);
+  return w < v ? w : v;
+}
+
 template <int L>
 __device__ __forceinline__ uint32_t gmin_u32(uint32_t v) {
-#pragma unroll
-  for (int o = L / 2; o > 0; o >>= 1) v = min(v, (uint32_t)__shfl_xor((int)v, o, L));
+  v = min(v, dpp_u32<0xB1>(v));
+  v = min(v, dpp_u32<0x4E>(v));
+  v = min(v, dpp_u32<0x124>(v));
+  v = min(v, dpp_u32<0x128>(v));
+  if (L == 32) v = min(v, (uint32_t)__shfl_xor((int)v, 16, 64));
   return v;
 }
 
 template <int L>
 __device__ __forceinline__ uint64_t gmin_u64(uint64_t v) {
-#pragma unroll
-  for (int o = L / 2; o > 0; o >>= 1) {
-    const uint32_t lo = (uint32_t)__shfl_xor((int)(uint32_t)v, o, L);
-    const uint32_t hi = (uint32_t)__shfl_xor((int)(uint32_t)(v >> 32), o, L);
+  v = dpp_min_u64<0xB1>(v);
+  v = dpp_min_u64<0x4E>(v);
+  v = dpp_min_u64<0x124>(v);
+  v = dpp_min_u64<0x128>(v);
+  if (L == 32) {
+    const uint32_t lo = (uint32_t)__shfl_xor((int)(uint32_t)v, 16, 64);
+    const uint32_t hi = (uint32_t)__shfl_xor((int)(uint32_t)(v >> 32), 16, 64);
     const uint64_t w = ((uint64_t)hi << 32) | lo;
     v = w < v ? w : v;
   }
@@ -82,15 +102,25 @@ __device__ __forceinline__ uint64_t bcast_u64(uint64_t v, int src) {
   return ((uint64_t)bcast_u32((uint32_t)(v >> 32), src) << 32) | bcast_u32((uint32_t)v, src);
 }
 
-// Per-lane view of chain l of the group's history, with a one-record cache.
+// Per-lane view of chain l of the group's history with a register window of
+// PACK_W consecutive records. A closure that advances a chain by several
+// identity ops, and the next rounds' expansions, read them from registers: a
+// window refill issues PACK_W independent loads (one memory latency) where a
+// one-record cache paid one dependent latency per advanced op.
+constexpr int PACK_W = 4;
 struct ChainLane {
   const OpRec* __restrict__ base;  // first record of chain l (valid iff on)
   bool on;                         // l < K
-  uint32_t cc;                     // count of the cached record
-  OpRec r;                         // cached record (null record when !on)
-  __device__ __forceinline__ void reset(const OpRec* b, bool on_) {
+  uint32_t len;                    // records of chain l, its sentinel included
+  uint32_t w0;                     // count of the window's first record
+  uint32_t cc;                     // count of r
+  uint4 wa[4], wb[4], wc[4], wd[4];  // window: records at counts w0 .. w0+3
+  OpRec r;                         // record at count cc (null record when !on)
+  __device__ __forceinline__ void reset(const OpRec* b, bool on_, uint32_t len_) {
     base = b;
     on = on_;
+    len = len_;
+    w0 = 0xFFFF0000u;
     cc = 0xFFFFFFFFu;
     r.num_records = 0; r.msn = 0; r.out_tail = 0; r.out_hash = 0;
     r.sufmin = REQ_NONE; r.call_ev = EV_INF; r.ret_ev = EV_INF;
@@ -98,17 +128,41 @@ struct ChainLane {
     r.flags = OPF_SENTINEL;
   }
   __device__ __forceinline__ void at(uint32_t c) {
-    if (on && c != cc) {
-      r = load_rec(base + c);
-      cc = c;
+    if (!on || c == cc) return;
+    uint32_t o = c - w0;
+    if (o >= (uint32_t)PACK_W) {
+      // clamp to the chain: a record past its sentinel is never selected
+      const OpRec* q = base + c;
+      const uint32_t last = len - 1 - c;  // c < len always (sentinel included)
+      const uint4* qa = reinterpret_cast<const uint4*>(q);
+      const uint4* qb = reinterpret_cast<const uint4*>(q + min(1u, last));
+      const uint4* qc = reinterpret_cast<const uint4*>(q + min(2u, last));
+      const uint4* qd = reinterpret_cast<const uint4*>(q + min(3u, last));
+#pragma unroll
+      for (int k = 0; k < 4; ++k) { wa[k] = qa[k]; wb[k] = qb[k]; wc[k] = qc[k]; wd[k] = qd[k]; }
+      w0 = c;
+      o = 0;
     }
+    // select dword-wise in registers (a struct-typed select goes through scratch)
+    uint4 sel[4];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      const uint4 A = wa[k], B = wb[k], C = wc[k], D = wd[k];
+      sel[k].x = o == 0 ? A.x : o == 1 ? B.x : o == 2 ? C.x : D.x;
+      sel[k].y = o == 0 ? A.y : o == 1 ? B.y : o == 2 ? C.y : D.y;
+      sel[k].z = o == 0 ? A.z : o == 1 ? B.z : o == 2 ? C.z : D.z;
+      sel[k].w = o == 0 ? A.w : o == 1 ? B.w : o == 2 ? C.w : D.w;
+    }
+    __builtin_memcpy(&r, sel, sizeof(OpRec));
+    cc = c;
   }
 };
 
 // Group closure of one configuration (state s, lane count cnt) under minimal,
 // legal identity ops + P1/P2/P4; returns CL_* and the exact minret.
 template <int L>
-__device__ __forceinline__ int pack_closure(ChainLane& ch, uint32_t& cnt, const State& s, uint32_t hflags,
+__device__ __forceinline__ int pack_closure(ChainLane& ch, const uint64_t* __restrict__ pool, uint32_t& cnt,
+                                            const State& s, uint32_t hflags,
                                             uint64_t gmask, uint32_t& minret_out) {
   const bool nowrap = hflags & H_NOWRAP;
   const bool p2 = hflags & H_P2OK;
@@ -140,8 +194,23 @@ __device__ __forceinline__ int pack_closure(ChainLane& ch, uint32_t& cnt, const 
   }
 }
 
+// S2LC_PROF: per-phase cycle counts of the pack kernel (lane 0 of each group),
+// summed into g_prof[10..15]: expand, closure, dedupe+insert, rounds, closure
+// passes, children.
+#ifdef S2LC_PROF
+#define PK_T0() pk_t = clock64()
+#define PK_LAP(i) do { const unsigned long long t_ = clock64(); pk_acc[i] += t_ - pk_t; pk_t = t_; } while (0)
+#else
+#define PK_T0() do { } while (0)
+#define PK_LAP(i) do { } while (0)
+#endif
+
 template <int L>
 __global__ __launch_bounds__(PACK_BLOCK) void pack_kernel(Params p) {
+#ifdef S2LC_PROF
+  unsigned long long pk_acc[6] = {0, 0, 0, 0, 0, 0};
+  unsigned long long pk_t = 0;
+#endif
   using C = PCfg<L>;
   S2LC_DYNAMIC_LDS(smem);
   const int lane = (int)(threadIdx.x & 63);
@@ -161,8 +230,9 @@ __global__ __launch_bounds__(PACK_BLOCK) void pack_kernel(Params p) {
     const int K = hd.K;
     const bool on = gl < K;
     const uint32_t cs = on ? p.chain_start[hd.cs_base + gl] : 0u;
+    const uint32_t ce = on ? p.chain_start[hd.cs_base + gl + 1] : 0u;
     ChainLane ch;
-    ch.reset(p.recs + cs, on);
+    ch.reset(p.recs + cs, on, ce - cs);
     bool witness_ok = p.witness != 0;
 
     uint32_t verdict = V_ILLEGAL, reason = S2LC_R_SEARCH_EXHAUSTED;
@@ -176,7 +246,7 @@ __global__ __launch_bounds__(PACK_BLOCK) void pack_kernel(Params p) {
     {
       uint32_t cnt = 0, mr = 0;
       const State s0{0, 0, 0};
-      const int cr = pack_closure<L>(ch, cnt, s0, hd.flags, gmask, mr);
+      const int cr = pack_closure<L>(ch, p.pool, cnt, s0, hd.flags, gmask, mr);
       if (cr == CL_DEAD) {
         nf = 0;
       } else if (cr != CL_ALIVE) {
@@ -207,6 +277,7 @@ __global__ __launch_bounds__(PACK_BLOCK) void pack_kernel(Params p) {
         const uint32_t pmin = pc.minret;
         const uint32_t ptrace = pc.trace;
         const uint32_t pcnt = on ? pc.cnt[gl] : 0u;
+        PK_T0();
         // expand: lane l tries the head of chain l
         ch.at(pcnt);
         const OpRec& r = ch.r;
@@ -223,13 +294,11 @@ __global__ __launch_bounds__(PACK_BLOCK) void pack_kernel(Params p) {
             take_opt = g;
           }
           if (take_opt) {
-            uint64_t hsh = s.hash;
-            const uint64_t* __restrict__ hp = p.pool + r.hash_off;
-            for (uint32_t i = 0; i < r.hash_cnt; ++i) hsh = chain_hash(hsh, hp[i]);
-            opt.hash = hsh;
+            opt.hash = fold_hashes_blk(s.hash, p.pool + r.hash_off, r.hash_cnt);
           }
           if (r.flags & OPF_CLS_I) take_id = r.ret_ev == pmin && !(g && state_eq(opt, s));
         }
+        PK_LAP(0);
         uint64_t mo = __ballot(take_opt) & gmask;
         uint64_t mi = __ballot(take_id) & gmask;
         children += __popcll(mo) + __popcll(mi);
@@ -246,7 +315,9 @@ __global__ __launch_bounds__(PACK_BLOCK) void pack_kernel(Params p) {
           ks.tok = bcast_u32(is_id ? s.tok : opt.tok, src);
           uint32_t cnt = pcnt + (gl == j ? 1u : 0u);
           uint32_t mr = 0;
-          const int cr = pack_closure<L>(ch, cnt, ks, hd.flags, gmask, mr);
+          PK_LAP(2);
+          const int cr = pack_closure<L>(ch, p.pool, cnt, ks, hd.flags, gmask, mr);
+          PK_LAP(1);
           const uint32_t mv = is_id ? ((uint32_t)j | MOVE_IDENT) : (uint32_t)j;
           if (cr == CL_COMPLETE || cr == CL_P4) {
             found = true;
@@ -274,6 +345,7 @@ __global__ __launch_bounds__(PACK_BLOCK) void pack_kernel(Params p) {
           ++nn;
         }
       }
+      PK_LAP(2);
       if (found) { verdict = V_OK; reason = 0; rounds++; break; }
       if (overflow) { verdict = V_UNKNOWN; reason = S2LC_R_FRONTIER; break; }
       rounds++;
@@ -305,6 +377,13 @@ __global__ __launch_bounds__(PACK_BLOCK) void pack_kernel(Params p) {
       cur = 1 - cur;
       nf = nn;
     }
+#ifdef S2LC_PROF
+    if (gl == 0) {
+      for (int i_ = 0; i_ < 3; ++i_) { atomicAdd(&g_prof[10 + i_], pk_acc[i_]); pk_acc[i_] = 0; }
+      atomicAdd(&g_prof[13], (unsigned long long)rounds);
+      atomicAdd(&g_prof[15], (unsigned long long)children);
+    }
+#endif
     if (gl == 0) {
       HistResult& R = p.res[h];
       R.verdict = verdict;

@@ -288,6 +288,12 @@ int batch_run(DevBatch& b, hipStream_t stream, uint64_t max_configs, bool witnes
     for (uint32_t i = 0; i < b.n_hist; ++i) pack16_done[i] = b.in_pack16[i];
   std::vector<uint32_t> todo;  // histories for the workgroup-per-history passes
   if (use_pack) {
+#ifdef S2LC_PROF
+    {
+      unsigned long long z[16] = {0};
+      HIPCHK(hipMemcpyToSymbol(HIP_SYMBOL(g_prof), z, sizeof z));
+    }
+#endif
     for (int li = 0; li < 2; ++li) {
       const uint32_t n_l = li == 0 ? b.n_pack16 : b.n_pack32;
       if (n_l == 0) continue;
@@ -316,6 +322,15 @@ int batch_run(DevBatch& b, hipStream_t stream, uint64_t max_configs, bool witnes
       if (li == 0) st.pack16_ms = ms;
       st.launches++;
     }
+#ifdef S2LC_PROF
+    {
+      unsigned long long gp[16];
+      HIPCHK(hipMemcpyFromSymbol(gp, HIP_SYMBOL(g_prof), sizeof gp));
+      const double rd = gp[13] ? (double)gp[13] : 1.0;
+      fprintf(stderr, "[s2lc prof] pack: rounds %llu children %llu | cycles/round expand %.0f closure %.0f dedupe+rest %.0f\n",
+              gp[13], gp[15], gp[10] / rd, gp[11] / rd, gp[12] / rd);
+    }
+#endif
     if (b.n_pack16 + b.n_pack32) {
       HIPCHK(hipMemcpyAsync(b.h_res.data(), b.res, b.n_hist * sizeof(HistResult), hipMemcpyDeviceToHost, stream));
       HIPCHK(hipStreamSynchronize(stream));

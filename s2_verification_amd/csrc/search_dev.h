@@ -499,7 +499,11 @@ __global__ __launch_bounds__(BT) void search_kernel(Params p) {
             const bool g = append_guards_ok(r, s);
             State opt{0, 0, 0};
             if (!GUARD((uint64_t)r.hash_off + r.hash_cnt <= p.n_pool, r.hash_off, r.hash_cnt)) continue;
-            if (g) opt = append_opt(r, s, p.pool);
+            if (g) {
+              opt.tail = s.tail + r.num_records;
+              opt.hash = fold_hashes_blk(s.hash, p.pool + r.hash_off, r.hash_cnt);
+              opt.tok = r.set_tok ? r.set_tok : s.tok;
+            }
             // children as two named slots (a runtime-indexed array would go to scratch)
             bool take_opt, take_id;
             if (r.flags & OPF_CLS_D) {
