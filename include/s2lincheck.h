@@ -266,6 +266,21 @@ int s2lc_dist_expand(s2lc_dist* d, uint64_t* counts /* [world] */, int32_t* foun
 int s2lc_dist_pack(s2lc_dist* d, void* send /* device */, const uint64_t* counts /* [world] */);
 int s2lc_dist_insert(s2lc_dist* d, void* recv /* device */, uint64_t n_recv, uint64_t* n_next);
 int s2lc_dist_info(const s2lc_dist* d, s2lc_dist_info_t* out);
+/* Narrow frontiers run REPLICATED: every rank runs the same round on the whole
+ * frontier with no exchange (the configuration set, and so every decision, is
+ * identical on all ranks); the driver switches to the partitioned rounds above
+ * when the frontier is wide and back when it is narrow again.
+ *   s2lc_dist_local_round   one replicated round (round 0 included);
+ *                           n_next = frontier size, found = a child completed
+ *   s2lc_dist_keep_owned    replicated -> partitioned: keep the owned configurations
+ *   s2lc_dist_frontier_pack partitioned -> replicated: this rank's frontier,
+ *                           frontier * config_bytes bytes, into a device buffer
+ *   s2lc_dist_frontier_load the all-gathered frontier (device buffer kept alive
+ *                           by the caller) becomes every rank's frontier */
+int s2lc_dist_local_round(s2lc_dist* d, uint64_t* n_next, int32_t* found);
+int s2lc_dist_keep_owned(s2lc_dist* d, uint64_t* n_kept);
+int s2lc_dist_frontier_pack(s2lc_dist* d, void* buf);
+int s2lc_dist_frontier_load(s2lc_dist* d, void* buf, uint64_t n);
 /* Copy this rank's trace pool ({parent id, move} u32 pairs) to host memory;
  * with out_pairs == NULL only *n is set. */
 int s2lc_dist_trace(s2lc_dist* d, uint32_t* out_pairs, uint64_t cap_entries, uint64_t* n);

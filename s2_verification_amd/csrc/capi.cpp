@@ -494,6 +494,29 @@ int s2lc_dist_insert(s2lc_dist* x, void* recv, uint64_t n_recv, uint64_t* n_next
   return dist_insert(x->d, (uint8_t*)recv, n_recv, n_next, x->ctx->err);
 }
 
+int s2lc_dist_local_round(s2lc_dist* x, uint64_t* n_next, int32_t* found) {
+  if (!x || !n_next || !found) return S2LC_EINVAL;
+  int f = 0;
+  const int rc = dist_local_round(x->d, n_next, &f, x->ctx->err);
+  *found = f;
+  return rc;
+}
+
+int s2lc_dist_keep_owned(s2lc_dist* x, uint64_t* n_kept) {
+  if (!x || !n_kept) return S2LC_EINVAL;
+  return dist_keep_owned(x->d, n_kept, x->ctx->err);
+}
+
+int s2lc_dist_frontier_pack(s2lc_dist* x, void* buf) {
+  if (!x || (!buf && x->d.nf)) return S2LC_EINVAL;
+  return dist_frontier_pack(x->d, (uint8_t*)buf, x->ctx->err);
+}
+
+int s2lc_dist_frontier_load(s2lc_dist* x, void* buf, uint64_t n) {
+  if (!x || (!buf && n)) return S2LC_EINVAL;
+  return dist_frontier_load(x->d, (uint8_t*)buf, n, x->ctx->err);
+}
+
 int s2lc_dist_info(const s2lc_dist* x, s2lc_dist_info_t* out) {
   if (!x || !out) return S2LC_EINVAL;
   const DistLevel& d = x->d;

@@ -37,7 +37,9 @@ hipError_t lv_launch(int which, uint32_t grid, const LvParams& p, hipStream_t st
   else if (which == 1) hipLaunchKernelGGL(lv_close<KMAX>, dim3(grid), dim3(LV_BLOCK), 0, st, p);
   else if (which == 2) hipLaunchKernelGGL(lv_insert<KMAX>, dim3(grid), dim3(LV_BLOCK), 0, st, p);
   else if (which == 3) hipLaunchKernelGGL(lv_bucket<KMAX>, dim3(grid), dim3(LV_BLOCK), 0, st, p);
-  else hipLaunchKernelGGL(lv_scatter<KMAX>, dim3(grid), dim3(LV_BLOCK), 0, st, p);
+  else if (which == 4) hipLaunchKernelGGL(lv_scatter<KMAX>, dim3(grid), dim3(LV_BLOCK), 0, st, p);
+  else if (which == 5) hipLaunchKernelGGL(lv_keep<KMAX>, dim3(grid), dim3(LV_BLOCK), 0, st, p, (uint32_t)(p.tgid >> 29));
+  else hipLaunchKernelGGL(lv_gather_frontier<KMAX>, dim3(grid), dim3(LV_BLOCK), 0, st, p);
   return hipGetLastError();
 }
 
@@ -303,7 +305,9 @@ static LvParams dist_params(DistLevel& d) {
   p.ht = L.ht; p.ht_mask = L.ht_mask;
   p.trace = d.trace; p.ctl = reinterpret_cast<LvCtl*>(L.ctl);
   p.world = d.world; p.own_cnt = d.own_cnt; p.own_pos = d.own_pos;
-  p.stg = L.stg[0];  // local staging (the closed children of this rank)
+  // local staging (the closed children of this rank): the array that does not
+  // hold the current frontier
+  p.stg = d.cur == L.stg[0] ? L.stg[1] : L.stg[0];
   p.cur = d.cur; p.cur_idx = L.idx[d.cur_sel];
   p.tgid = d.rank << 29;
   return p;
@@ -420,6 +424,122 @@ int dist_insert(DistLevel& d, uint8_t* recv, uint64_t n_recv, uint64_t* n_next, 
   d.max_frontier = std::max<uint64_t>(d.max_frontier, hc->nnext);
   d.round++;
   *n_next = hc->nnext;
+  return 0;
+}
+
+// ---- replicated rounds (narrow frontiers): every rank runs the same round on
+// the whole frontier, with no exchange; the set of configurations, and so
+// every decision, is the same on all ranks.
+int dist_local_round(DistLevel& d, uint64_t* n_next, int* found, std::string& err) {
+  LevelBufs& L = d.b.lv;
+  LvCtl* hc = reinterpret_cast<LvCtl*>(L.h_ctl);
+  int dev = 0, n_cu = 256;
+  LVCHK(hipGetDevice(&dev));
+  (void)hipDeviceGetAttribute(&n_cu, hipDeviceAttributeMultiprocessorCount, dev);
+  const uint64_t max_grid = (uint64_t)n_cu * 8;
+  hipStream_t st = d.stream;
+  LvParams p = dist_params(d);
+  p.nxt_idx = L.idx[d.cur_sel ^ 1];
+  p.witness = 1;
+  if (d.tnext + L.scap > d.trace_cap) { err = "trace pool full"; return S2LC_ENOMEM; }
+  p.tbase = (uint32_t)d.tnext;
+  hipEvent_t e0, e1;
+  LVCHK(hipEventCreate(&e0));
+  LVCHK(hipEventCreate(&e1));
+  LVCHK(hipEventRecord(e0, st));
+  memset(hc, 0, sizeof(LvCtl));
+  if (d.round == 0) {
+    hc->nchild = 1;
+    const LChild c0{0, 0, 0, LV_NONE, LV_NONE, 0};
+    LVCHK(hipMemcpyAsync(L.child, &c0, sizeof c0, hipMemcpyHostToDevice, st));
+    LVCHK(hipMemcpyAsync(L.ctl, hc, sizeof(LvCtl), hipMemcpyHostToDevice, st));
+    LVCHK(lv_dispatch(d.kmax, 1, 1, p, st));
+    LVCHK(lv_dispatch(d.kmax, 2, 1, p, st));
+  } else {
+    LVCHK(hipMemcpyAsync(L.ctl, hc, sizeof(LvCtl), hipMemcpyHostToDevice, st));
+    p.f0 = 0; p.f1 = d.nf; p.clear_slots = 1;
+    const uint64_t lanes = (uint64_t)d.nf * d.K;
+    const uint64_t kids_ub = std::min<uint64_t>(2 * lanes, L.ccap);
+    LVCHK(lv_dispatch(d.kmax, 0, (uint32_t)std::max<uint64_t>(1, std::min(max_grid, (lanes + LV_BLOCK - 1) / LV_BLOCK)), p, st));
+    LVCHK(lv_dispatch(d.kmax, 1, (uint32_t)std::max<uint64_t>(1, std::min(max_grid, (kids_ub + 3) / 4)), p, st));
+    LVCHK(lv_dispatch(d.kmax, 2, (uint32_t)std::max<uint64_t>(1, std::min(max_grid, (std::min<uint64_t>(kids_ub, L.scap) + LV_BLOCK - 1) / LV_BLOCK)), p, st));
+  }
+  LVCHK(hipMemcpyAsync(hc, L.ctl, sizeof(LvCtl), hipMemcpyDeviceToHost, st));
+  LVCHK(hipEventRecord(e1, st));
+  LVCHK(hipStreamSynchronize(st));
+  float ms = 0;
+  LVCHK(hipEventElapsedTime(&ms, e0, e1));
+  (void)hipEventDestroy(e0);
+  (void)hipEventDestroy(e1);
+  d.ms += ms;
+  if (hc->overflow && !hc->found) { err = "replicated round exceeds the device buffers"; return S2LC_ENOMEM; }
+  d.children += std::min(hc->nchild, L.ccap);
+  *found = hc->found ? 1 : 0;
+  if (hc->found) {
+    d.found_parent = hc->found_parent; d.found_move = hc->found_move; d.found_p4 = hc->found_p4;
+    *n_next = 0;
+    return 0;
+  }
+  d.cur = p.stg;
+  d.cur_sel ^= 1;
+  d.nf = hc->nnext;
+  d.tnext += hc->nnext;
+  d.configs += hc->nnext;
+  d.max_frontier = std::max<uint64_t>(d.max_frontier, hc->nnext);
+  d.round++;
+  *n_next = hc->nnext;
+  return 0;
+}
+
+// replicated -> partitioned: keep only the frontier configurations this rank owns
+int dist_keep_owned(DistLevel& d, uint64_t* n_kept, std::string& err) {
+  LevelBufs& L = d.b.lv;
+  LvCtl* hc = reinterpret_cast<LvCtl*>(L.h_ctl);
+  hipStream_t st = d.stream;
+  LvParams p = dist_params(d);
+  p.f1 = d.nf;
+  p.nxt_idx = L.idx[d.cur_sel ^ 1];
+  memset(hc, 0, sizeof(LvCtl));
+  LVCHK(hipMemcpyAsync(L.ctl, hc, sizeof(LvCtl), hipMemcpyHostToDevice, st));
+  if (d.nf) LVCHK(lv_dispatch(d.kmax, 5, (uint32_t)std::min<uint64_t>(2048, (d.nf + LV_BLOCK - 1) / LV_BLOCK), p, st));
+  // the table still holds the dropped configurations' slots: reset it
+  LVCHK(hipMemsetAsync(L.ht, 0xFF, ((size_t)L.ht_mask + 1) * 8, st));
+  LVCHK(hipMemcpyAsync(hc, L.ctl, sizeof(LvCtl), hipMemcpyDeviceToHost, st));
+  LVCHK(hipStreamSynchronize(st));
+  d.cur_sel ^= 1;
+  d.nf = hc->nnext;
+  *n_kept = d.nf;
+  return 0;
+}
+
+// partitioned -> replicated, step 1: this rank's frontier, contiguous, into buf
+int dist_frontier_pack(DistLevel& d, uint8_t* buf, std::string& err) {
+  LvParams p = dist_params(d);
+  p.f1 = d.nf;
+  p.send = buf;
+  if (d.nf) {
+    const uint64_t pieces = (uint64_t)d.nf * (d.cb / 16);
+    LVCHK(lv_dispatch(d.kmax, 6, (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>(2048, (pieces + LV_BLOCK - 1) / LV_BLOCK)), p, d.stream));
+  }
+  LVCHK(hipStreamSynchronize(d.stream));
+  return 0;
+}
+
+// partitioned -> replicated, step 2: the gathered frontier of all ranks
+// (caller-owned device buffer, kept alive until the next round) becomes the
+// frontier of every rank
+int dist_frontier_load(DistLevel& d, uint8_t* buf, uint64_t n, std::string& err) {
+  LevelBufs& L = d.b.lv;
+  if (n > L.scap) { err = "gathered frontier exceeds the frontier capacity"; return S2LC_ENOMEM; }
+  hipStream_t st = d.stream;
+  const int sel = d.cur_sel ^ 1;
+  if (n) hipLaunchKernelGGL(lv_iota, dim3((uint32_t)std::min<uint64_t>(1024, (n + 255) / 256)), dim3(256), 0, st, L.idx[sel], (uint32_t)n);
+  LVCHK(hipGetLastError());
+  LVCHK(hipMemsetAsync(L.ht, 0xFF, ((size_t)L.ht_mask + 1) * 8, st));
+  LVCHK(hipStreamSynchronize(st));
+  d.cur = buf;
+  d.cur_sel = sel;
+  d.nf = (uint32_t)n;
   return 0;
 }
 

@@ -414,5 +414,38 @@ __global__ __launch_bounds__(LV_BLOCK) void lv_scatter(LvParams p) {
   }
 }
 
+// keep the frontier configurations this rank owns (replicated -> partitioned)
+template <int KMAX>
+__global__ __launch_bounds__(LV_BLOCK) void lv_keep(LvParams p, uint32_t rank) {
+  const uint32_t nf = p.f1;
+  for (uint32_t b0 = blockIdx.x * LV_BLOCK; b0 < nf; b0 += gridDim.x * LV_BLOCK) {
+    const uint32_t i = b0 + threadIdx.x;
+    uint32_t k = 0;
+    bool mine = false;
+    if (i < nf) {
+      k = p.cur_idx[i];
+      mine = lv_owner(lv_cfg<KMAX>(p.cur, k)->fp, p.world) == rank;
+    }
+    const uint32_t n = wave_alloc(&p.ctl->nnext, mine ? 1u : 0u);
+    if (mine) p.nxt_idx[n] = k;
+  }
+}
+
+// copy the frontier's configurations contiguously into p.send (16 B per lane)
+template <int KMAX>
+__global__ __launch_bounds__(LV_BLOCK) void lv_gather_frontier(LvParams p) {
+  constexpr uint32_t PER = sizeof(LCfg<KMAX>) / 16;
+  const uint64_t total = (uint64_t)p.f1 * PER;
+  for (uint64_t i = (uint64_t)blockIdx.x * LV_BLOCK + threadIdx.x; i < total; i += (uint64_t)gridDim.x * LV_BLOCK) {
+    const uint32_t f = (uint32_t)(i / PER), c = (uint32_t)(i % PER);
+    const uint4* src = reinterpret_cast<const uint4*>(lv_cfg<KMAX>(p.cur, p.cur_idx[f]));
+    reinterpret_cast<uint4*>(p.send + (uint64_t)f * sizeof(LCfg<KMAX>))[c] = src[c];
+  }
+}
+
+__global__ void lv_iota(uint32_t* out, uint32_t n) {
+  for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) out[i] = i;
+}
+
 }  // namespace
 }  // namespace s2lc

@@ -43,7 +43,7 @@ class DistResult:
     exchanged_bytes: int     # payload bytes this rank sent to other ranks
     witness: Optional[List[int]] = None
     witness_valid: Optional[bool] = None
-    per_rank_configs: List[int] = field(default_factory=list)
+    per_rank_configs: List[int] = field(default_factory=list)  # [partitioned rounds]
 
 
 class DistSearch:
@@ -94,6 +94,23 @@ class DistSearch:
                                          ctypes.byref(nn)), "dist_insert")
         return nn.value
 
+    def local_round(self):
+        nn = ctypes.c_uint64(0)
+        found = ctypes.c_int32(0)
+        self._chk(lib().s2lc_dist_local_round(self._d, ctypes.byref(nn), ctypes.byref(found)), "dist_local_round")
+        return nn.value, bool(found.value)
+
+    def keep_owned(self) -> int:
+        n = ctypes.c_uint64(0)
+        self._chk(lib().s2lc_dist_keep_owned(self._d, ctypes.byref(n)), "dist_keep_owned")
+        return n.value
+
+    def frontier_pack(self, buf: torch.Tensor):
+        self._chk(lib().s2lc_dist_frontier_pack(self._d, ctypes.c_void_p(buf.data_ptr())), "dist_frontier_pack")
+
+    def frontier_load(self, buf: torch.Tensor, n: int):
+        self._chk(lib().s2lc_dist_frontier_load(self._d, ctypes.c_void_p(buf.data_ptr()), n), "dist_frontier_load")
+
     def trace(self) -> np.ndarray:
         n = ctypes.c_uint64(0)
         self._chk(lib().s2lc_dist_trace(self._d, None, 0, ctypes.byref(n)), "dist_trace")
@@ -136,6 +153,24 @@ class _Exchange:
         torch.cuda.current_stream(self.device).synchronize()
         return recv
 
+    def sum(self, v: int) -> int:
+        t = torch.tensor([v], dtype=torch.int64, device=self.tdev)
+        dist.all_reduce(t, group=self.group)
+        return int(t.item())
+
+    def gather_frontier(self, mine: torch.Tensor, n_bytes: List[int]) -> torch.Tensor:
+        """All-gather of variable-size byte buffers (every rank's frontier)."""
+        m = max(n_bytes)
+        src = torch.zeros(max(m, 1), dtype=torch.uint8, device=self.tdev)
+        if n_bytes[dist.get_rank(self.group)]:
+            src[:n_bytes[dist.get_rank(self.group)]] = mine[:n_bytes[dist.get_rank(self.group)]].to(self.tdev)
+        out = [torch.empty(max(m, 1), dtype=torch.uint8, device=self.tdev) for _ in range(self.world)]
+        dist.all_gather(out, src, group=self.group)
+        full = torch.cat([out[w][:n_bytes[w]] for w in range(self.world)]) if sum(n_bytes) else out[0][:1]
+        full = full.to(self.device).contiguous()
+        torch.cuda.current_stream(self.device).synchronize()
+        return full
+
     def gather_small(self, vals: List[int]) -> List[List[int]]:
         t = torch.tensor(vals, dtype=torch.int64, device=self.tdev)
         out = [torch.empty_like(t) for _ in range(self.world)]
@@ -176,20 +211,48 @@ def _walk(traces: List[np.ndarray], parent: int, move: int) -> Optional[List[int
     return moves
 
 
-def check_distributed(checker, history: History, group=None, witness: bool = True) -> DistResult:
-    """Check one history with every rank of `group` (default: the world)."""
+def check_distributed(checker, history: History, group=None, witness: bool = True,
+                      wide: int = 4096) -> DistResult:
+    """Check one history with every rank of `group` (default: the world).
+
+    Rounds whose frontier is narrower than `wide` configurations run
+    replicated (every rank the whole round, no exchange); wider rounds run
+    partitioned by owner with one all-to-all per round. wide=0 partitions
+    every round."""
     rank = dist.get_rank(group)
     world = dist.get_world_size(group)
     device = torch.device("cuda", torch.cuda.current_device())
     ex = _Exchange(group, device)
     ds = DistSearch(checker, history, rank, world)
     cb = ds.info().config_bytes
-    cur = None  # the received buffer holding this rank's frontier (kept alive)
+    keep = []  # device buffers holding this rank's frontier (kept alive)
     verdict = None
     sent_bytes = 0
+    found = False
+    rounds = 0
+    configs = 0
+    part_rounds = 0
+    replicated = wide > 0 and world > 1 or world == 1
     t0 = time.perf_counter()
+    first = True  # round 0 closes the initial configuration; rounds counts the ones after it
     try:
         while verdict is None:
+            if not first:
+                rounds += 1
+            first = False
+            if replicated:
+                nn, found = ds.local_round()
+                if found:
+                    verdict = Ok
+                    break
+                if nn == 0:
+                    verdict = Illegal
+                    break
+                configs += nn
+                if world > 1 and nn >= wide:
+                    ds.keep_owned()
+                    replicated = False
+                continue
             counts, found = ds.expand()
             recv_counts, found_any, staged_total = ex.counts(counts, found, sum(counts))
             if found_any:
@@ -204,24 +267,38 @@ def check_distributed(checker, history: History, group=None, witness: bool = Tru
             out_b = [c * cb for c in recv_counts]
             sent_bytes += sum(b for w, b in enumerate(in_b) if w != rank)
             recv = ex.payload(send[:sum(in_b)], in_b, out_b)
-            ds.insert(recv, sum(recv_counts))
-            cur = recv  # noqa: F841  (frontier storage for the next expand)
+            nn = ds.insert(recv, sum(recv_counts))
+            keep = [recv]
+            part_rounds += 1
+            total = ex.sum(nn)
+            configs += total
+            if total == 0:
+                verdict = Illegal
+                break
+            if wide > 0 and total < wide // 4:
+                # narrow again: every rank takes the whole frontier
+                sizes = [x[0] * cb for x in ex.gather_small([nn])]
+                mine = torch.empty(max(1, nn * cb), dtype=torch.uint8, device=device)
+                if nn:
+                    ds.frontier_pack(mine)
+                full = ex.gather_frontier(mine, sizes)
+                ds.frontier_load(full, total)
+                keep = [full]
+                replicated = True
         wall = time.perf_counter() - t0
         info = ds.info()
         stats = ex.gather_small([int(found and verdict == Ok), info.found_parent, info.found_move, info.found_p4,
-                                 info.configs, info.children, info.max_frontier, int(info.device_ms * 1e3),
-                                 info.round])
-        res = DistResult(verdict=verdict, rounds=max(s[8] for s in stats),
-                         configs=sum(s[4] for s in stats), children=sum(s[5] for s in stats),
-                         max_frontier=max(s[6] for s in stats), device_ms=max(s[7] for s in stats) / 1e3,
-                         wall_s=wall, exchanged_bytes=sent_bytes, per_rank_configs=[s[4] for s in stats])
+                                 info.children, info.max_frontier, int(info.device_ms * 1e3)])
+        res = DistResult(verdict=verdict, rounds=rounds, configs=configs, children=sum(s[4] for s in stats),
+                         max_frontier=max(s[5] for s in stats), device_ms=max(s[6] for s in stats) / 1e3,
+                         wall_s=wall, exchanged_bytes=sent_bytes, per_rank_configs=[part_rounds])
         if verdict == Ok and witness:
             src = next(s for s in stats if s[0])
             traces = ex.gather_traces(ds.trace())
             moves = _walk(traces, src[1], src[2])
             ok = False
             ids = None
-            if moves is not None:
+            if moves is not None and len(moves) == rounds:
                 n_ops = history.info()["n_ops"]
                 mv = (ctypes.c_uint32 * max(1, len(moves)))(*moves)
                 out = (ctypes.c_int64 * max(1, n_ops))()
@@ -231,4 +308,4 @@ def check_distributed(checker, history: History, group=None, witness: bool = Tru
         return res
     finally:
         ds.close()
-        del cur
+        del keep
