@@ -125,6 +125,12 @@ typedef struct s2lc_result {
   uint32_t _pad;
   int64_t* witness;           /* Event.Id of each op in linearization order; library-owned */
   double device_ms;           /* device time of the search launch(es) */
+  /* Illegal: the linearized prefix of a configuration of the deepest round the
+   * search reached (what porcupine's LinearizationInfo partial linearizations
+   * show, main.go:607-611), certified like a witness; library-owned */
+  int64_t* partial;
+  uint32_t partial_len;
+  uint32_t _pad2;
 } s2lc_result;
 
 #define S2LC_R_NONE 0
@@ -229,6 +235,13 @@ int s2lc_replay(const s2lc_history* h, const uint32_t* order, size_t n);
  * 0 = valid, -1 = not a valid linearization. */
 int s2lc_witness_from_moves(const s2lc_history* h, const uint32_t* moves, size_t n_moves, int p4,
                             int64_t* out_ids, size_t cap);
+
+/* porcupine.Visualize(model, info, file) (main.go:608-631): write an HTML page
+ * for a checked history — each client's ops on the event axis, labelled with
+ * DescribeOperation (main.go:341-426), and the witness (Ok) or the deepest
+ * certified prefix (Illegal) with the powerset state after each op
+ * (DescribeState). r is the s2lc_check result for h. */
+int s2lc_visualize(const s2lc_history* h, const s2lc_result* r, const char* path);
 
 /* ----- distributed search of ONE history (BASELINE config C5) --------------
  * One rank per GPU; configurations are owned by a hash of their fingerprint.

@@ -75,7 +75,8 @@ class c_result(ctypes.Structure):
     _fields_ = [("verdict", ctypes.c_int32), ("reason", ctypes.c_int32), ("configs_explored", ctypes.c_uint64),
                 ("rounds", ctypes.c_uint32), ("n_ops", ctypes.c_uint32), ("witness_len", ctypes.c_uint32),
                 ("_pad", ctypes.c_uint32), ("witness", ctypes.POINTER(ctypes.c_int64)),
-                ("device_ms", ctypes.c_double)]
+                ("device_ms", ctypes.c_double), ("partial", ctypes.POINTER(ctypes.c_int64)),
+                ("partial_len", ctypes.c_uint32), ("_pad2", ctypes.c_uint32)]
 
 
 class c_history_info(ctypes.Structure):
@@ -159,6 +160,7 @@ SIGNATURES = [
                                            ctypes.POINTER(ctypes.c_size_t)]),
     ("s2lc_simulate_history", ctypes.c_int, [ctypes.POINTER(c_sim_params), ctypes.POINTER(_P)]),
     ("s2lc_free", None, [_P]),
+    ("s2lc_visualize", ctypes.c_int, [_P, ctypes.POINTER(c_result), ctypes.c_char_p]),
     ("s2lc_witness_from_moves", ctypes.c_int, [_P, ctypes.POINTER(ctypes.c_uint32), ctypes.c_size_t, ctypes.c_int,
                                                ctypes.POINTER(ctypes.c_int64), ctypes.c_size_t]),
     ("s2lc_dist_create", ctypes.c_int, [_P, _P, ctypes.c_int, ctypes.c_int, ctypes.POINTER(_P)]),
@@ -381,12 +383,14 @@ class CheckResult:
     n_ops: int
     witness: Optional[List[int]]
     device_ms: float
+    partial: Optional[List[int]] = None  # Illegal: deepest certified linearized prefix (Event.Ids)
 
 
 def _convert(r: c_result) -> CheckResult:
     w = [r.witness[k] for k in range(r.witness_len)] if r.witness else None
+    pa = [r.partial[k] for k in range(r.partial_len)] if r.partial else None
     return CheckResult(_VERDICT[r.verdict], REASONS.get(r.reason, str(r.reason)), r.configs_explored,
-                       r.rounds, r.n_ops, w, r.device_ms)
+                       r.rounds, r.n_ops, w, r.device_ms, pa)
 
 
 class Batch:

@@ -19,9 +19,6 @@ int simulate(const s2lc_sim_params& p, History* h, std::string* jsonl);
 
 using namespace s2lc;
 
-struct s2lc_history {
-  History h;
-};
 
 struct s2lc_ctx {
   int device = 0;
@@ -325,7 +322,7 @@ int s2lc_batch_results(s2lc_ctx* c, s2lc_batch* b, s2lc_result* out, int with_wi
         std::vector<uint32_t> order;
         std::vector<uint8_t> ident;
         const bool ok =
-            rebuild_linearization(H, B.h_moves.data() + r.witness_off, r.witness_len, r.p4 != 0, order, ident) &&
+            rebuild_linearization(H, B.h_moves.data() + r.witness_off, r.witness_len, r.p4 != 0, order, ident, false) &&
             replay_path(H, order.data(), ident.data(), order.size());
         if (!ok) {
           o.reason = S2LC_R_WITNESS_INVALID;
@@ -335,6 +332,18 @@ int s2lc_batch_results(s2lc_ctx* c, s2lc_batch* b, s2lc_result* out, int with_wi
         if (!o.witness) { c->err = "out of memory"; return S2LC_ENOMEM; }
         for (size_t k = 0; k < order.size(); ++k) o.witness[k] = H.op_ids[order[k]];
         o.witness_len = (uint32_t)order.size();
+      }
+      if (want_w && r.verdict == V_ILLEGAL && r.has_witness == 1) {
+        const History& H = *B.src[i];
+        std::vector<uint32_t> order;
+        std::vector<uint8_t> ident;
+        if (rebuild_linearization(H, B.h_moves.data() + r.witness_off, r.witness_len, false, order, ident, true) &&
+            replay_prefix(H, order.data(), ident.data(), order.size())) {
+          o.partial = (int64_t*)malloc(sizeof(int64_t) * (order.size() ? order.size() : 1));
+          if (!o.partial) { c->err = "out of memory"; return S2LC_ENOMEM; }
+          for (size_t k = 0; k < order.size(); ++k) o.partial[k] = H.op_ids[order[k]];
+          o.partial_len = (uint32_t)order.size();
+        }
       }
     }
     return 0;
@@ -395,6 +404,9 @@ void s2lc_result_free(s2lc_result* r) {
   free(r->witness);
   r->witness = nullptr;
   r->witness_len = 0;
+  free(r->partial);
+  r->partial = nullptr;
+  r->partial_len = 0;
 }
 
 // ----------------------------------------------------------------- model ---
@@ -433,7 +445,7 @@ int s2lc_witness_from_moves(const s2lc_history* h, const uint32_t* moves, size_t
   try {
     std::vector<uint32_t> order;
     std::vector<uint8_t> ident;
-    if (!rebuild_linearization(h->h, moves, (uint32_t)n_moves, p4 != 0, order, ident) ||
+    if (!rebuild_linearization(h->h, moves, (uint32_t)n_moves, p4 != 0, order, ident, false) ||
         !replay_path(h->h, order.data(), ident.data(), order.size()))
       return -1;
     if (out_ids) {

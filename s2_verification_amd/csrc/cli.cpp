@@ -6,9 +6,14 @@
 #include <stdio.h>
 #include <stdlib.h>
 #include <string.h>
+#include <sys/stat.h>
 #include <time.h>
+#include <unistd.h>
+
+#include <errno.h>
 
 #include <string>
+#include <vector>
 
 #include "s2lincheck.h"
 
@@ -103,6 +108,30 @@ int main(int argc, char** argv) {
     s2lc_destroy(ctx);
     s2lc_history_free(h);
     return 1;
+  }
+  // main.go:608-631: ./porcupine-outputs/<input base>-<random>.html (stdin-*.html)
+  if (mkdir("./porcupine-outputs", 0755) != 0 && errno != EEXIST)
+    slog("ERROR", "failed to create visualizations directory", ",\"err\":" + jstr(strerror(errno)));
+  {
+    std::string base = "stdin";
+    if (strcmp(file, "-") != 0) {
+      base = file;
+      const size_t sl = base.find_last_of('/');
+      if (sl != std::string::npos) base = base.substr(sl + 1);
+      const size_t dot = base.find_last_of('.');
+      if (dot != std::string::npos && dot > 0) base = base.substr(0, dot);
+    }
+    std::string tmpl = "porcupine-outputs/" + base + "-XXXXXX.html";
+    std::vector<char> path(tmpl.begin(), tmpl.end());
+    path.push_back(0);
+    const int fd = mkstemps(path.data(), 5);
+    if (fd < 0) {
+      slog("ERROR", "failed to create temp file", ",\"err\":" + jstr(strerror(errno)));
+    } else {
+      close(fd);
+      if (s2lc_visualize(h, &r, path.data()) != 0) slog("ERROR", "failed to visualize", ",\"err\":\"write\"");
+      slog("INFO", "wrote visualization", ",\"file\":" + jstr(path.data()));
+    }
   }
   const bool ok = r.verdict == S2LC_OK;
   if (ok) {

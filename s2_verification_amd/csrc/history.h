@@ -67,3 +67,8 @@ int load_jsonl(const uint8_t* buf, size_t len, History& h, std::string& err);
 // Deterministic simulator (collector workload, history.rs + collect-history.rs).
 struct SimParams;
 }  // namespace s2lc
+
+// The opaque C-ABI handle (include/s2lincheck.h) is a History.
+struct s2lc_history {
+  s2lc::History h;
+};

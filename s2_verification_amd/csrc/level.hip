@@ -157,10 +157,22 @@ int level_search(DevBatch& b, uint32_t h, hipStream_t st, uint64_t max_configs, 
   uint64_t configs = 0, children = 0, tnext = tb0;
   uint32_t rounds = 0, max_frontier = 0;
   uint32_t verdict = V_ILLEGAL, reason = S2LC_R_SEARCH_EXHAUSTED;
+  uint32_t deep_trace = TRACE_NONE, deep_len = 0;
   for (;;) {
     if (hc->found) { verdict = V_OK; reason = 0; break; }
     const uint32_t nf = hc->nnext;
-    if (nf == 0) { verdict = V_ILLEGAL; reason = S2LC_R_SEARCH_EXHAUSTED; break; }
+    if (nf == 0) {
+      verdict = V_ILLEGAL; reason = S2LC_R_SEARCH_EXHAUSTED;
+      if (rounds > 0 && p.witness) {
+        // a configuration of the deepest non-empty round (the input of the last one)
+        uint32_t k = 0;
+        LVCHK(hipMemcpy(&k, L.idx[cur], sizeof k, hipMemcpyDeviceToHost));
+        LVCHK(hipMemcpy(&deep_trace, L.stg[cur] + (size_t)k * lv_cfg_bytes(kmax) + 40, sizeof deep_trace,
+                        hipMemcpyDeviceToHost));  // LCfg::trace
+        deep_len = rounds - 1;
+      }
+      break;
+    }
     configs += nf;
     max_frontier = std::max(max_frontier, nf);
     if (p.witness) tnext += nf;
@@ -230,7 +242,9 @@ int level_search(DevBatch& b, uint32_t h, hipStream_t st, uint64_t max_configs, 
   const bool have_w = verdict == V_OK && wit;
   R.final_parent = have_w ? hc->found_parent : TRACE_NONE;
   R.final_move = verdict == V_OK ? hc->found_move : TRACE_NONE;
-  R.has_witness = have_w ? 2u : 0u;
+  R.deep_trace = deep_trace;
+  R.deep_len = deep_len;
+  R.has_witness = (have_w || deep_trace != TRACE_NONE) ? 2u : 0u;
   LVCHK(hipMemcpyAsync(b.res + h, &R, sizeof R, hipMemcpyHostToDevice, st));
   if (witness && b.trace) {
     unsigned long long th = tnext;

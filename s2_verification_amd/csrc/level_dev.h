@@ -43,6 +43,7 @@ struct __attribute__((aligned(16))) LCfg {
   uint32_t slot;    // table slot (cleared when this configuration is expanded)
   uint16_t cnt[KMAX];
 };
+static_assert(offsetof(LCfg<64>, trace) == 40, "LCfg::trace offset (read by the host)");
 
 // A raw child: successor state of frontier configuration `parent` (staging
 // index) after the op at the head of chain move & 0xFFFF.

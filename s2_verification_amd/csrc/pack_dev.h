@@ -237,6 +237,7 @@ __global__ __launch_bounds__(PACK_BLOCK) void pack_kernel(Params p) {
 
     uint32_t verdict = V_ILLEGAL, reason = S2LC_R_SEARCH_EXHAUSTED;
     uint32_t found_parent = TRACE_NONE, found_move = TRACE_NONE, found_p4 = 0;
+    uint32_t deep_trace = TRACE_NONE, deep_len = 0;
     uint64_t configs = 0, children = 0;
     uint32_t rounds = 0;
     int cur = 0;  // frontier parity: fr[cur*F ..] current, fr[(1-cur)*F ..] next
@@ -349,7 +350,12 @@ __global__ __launch_bounds__(PACK_BLOCK) void pack_kernel(Params p) {
       if (found) { verdict = V_OK; reason = 0; rounds++; break; }
       if (overflow) { verdict = V_UNKNOWN; reason = S2LC_R_FRONTIER; break; }
       rounds++;
-      if (nn == 0) { verdict = V_ILLEGAL; reason = S2LC_R_SEARCH_EXHAUSTED; break; }
+      if (nn == 0) {
+        verdict = V_ILLEGAL; reason = S2LC_R_SEARCH_EXHAUSTED;
+        deep_trace = curf[0].trace;  // a configuration of the deepest non-empty round
+        deep_len = rounds - 1;
+        break;
+      }
       // trace entries (parent, move) of the surviving configurations
       uint32_t tb = TRACE_NONE;
       if (witness_ok) {
@@ -395,7 +401,9 @@ __global__ __launch_bounds__(PACK_BLOCK) void pack_kernel(Params p) {
       R.final_parent = (verdict == V_OK && witness_ok) ? found_parent : TRACE_NONE;
       R.final_move = found_move;
       R.witness_len = 0;
-      R.has_witness = (verdict == V_OK && witness_ok) ? 2u : 0u;  // resolved by walk_kernel
+      R.deep_trace = (verdict == V_ILLEGAL && witness_ok) ? deep_trace : TRACE_NONE;
+      R.deep_len = deep_len;
+      R.has_witness = ((verdict == V_OK || R.deep_trace != TRACE_NONE) && witness_ok) ? 2u : 0u;  // resolved by walk_kernel
     }
   }
 }

@@ -39,8 +39,11 @@ struct HistResult {
   uint32_t witness_off;   // into the witness move buffer
   uint32_t witness_len;   // moves written (rounds on the path)
   uint32_t has_witness;   // 0 none, 1 moves valid, 2 pending (set by search, resolved by walk)
+  uint32_t deep_trace;    // Illegal: trace index of a configuration of the deepest non-empty round
+  uint32_t deep_len;      // Illegal: its depth (moves on its path); the walk writes them as a partial
   uint32_t _pad;
 };
+static_assert(sizeof(HistResult) == 64, "HistResult is 64 bytes");
 
 struct SearchGeom {
   bool shared;         // arrays in LDS (true) or in a per-workgroup HBM slab
@@ -166,8 +169,12 @@ int dist_frontier_load(DistLevel& d, uint8_t* buf, uint64_t n, std::string& err)
 // move list; returns false if any move is not a legal successor.
 // ident[i] = 1 when order[i] took its identity outcome (E ops, indefinite
 // appends taken as not applied).
+// partial = true: a prefix (the path to a non-final configuration) is accepted.
 bool rebuild_linearization(const History& h, const uint32_t* moves, uint32_t n_moves, bool p4,
-                           std::vector<uint32_t>& order, std::vector<uint8_t>& ident);
+                           std::vector<uint32_t>& order, std::vector<uint8_t>& ident, bool partial);
+// A linearized prefix: distinct ops, real-time order within it, closed under
+// real-time predecessors, and every claimed outcome a Step successor.
+bool replay_prefix(const History& h, const uint32_t* order, const uint8_t* ident, size_t n);
 // Every op exactly once, in an order that respects real time.
 bool real_time_ok(const History& h, const uint32_t* order, size_t n);
 // Powerset replay of a linearization through the CPU model (+ real-time

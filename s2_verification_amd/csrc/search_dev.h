@@ -464,8 +464,15 @@ __global__ __launch_bounds__(BT) void search_kernel(Params p) {
     uint64_t configs = 0;
     uint32_t rounds = 0;
     uint32_t verdict = V_ILLEGAL, reason = S2LC_R_SEARCH_EXHAUSTED;
+    uint32_t deep_trace = TRACE_NONE, deep_len = 0;
     for (bool init = true;; init = false) {
-      if (!init && ncur == 0) { verdict = V_ILLEGAL; reason = S2LC_R_SEARCH_EXHAUSTED; break; }
+      if (!init && ncur == 0) {
+        verdict = V_ILLEGAL; reason = S2LC_R_SEARCH_EXHAUSTED;
+        // nxt holds the previous (deepest non-empty) frontier after the swap
+        deep_trace = rounds > 0 ? nxt[0].trace : TRACE_NONE;
+        deep_len = rounds > 0 ? rounds - 1 : 0;
+        break;
+      }
       if (tid == 0) S.nnext = 0;
       if (SHARED && W) window_refill<KMAX, BT>(S, win, recs, cur, ncur, K, W, init);
       const uint32_t total = init ? 1u : ncur * (uint32_t)K;
@@ -664,7 +671,9 @@ __global__ __launch_bounds__(BT) void search_kernel(Params p) {
       R.final_parent = (verdict == V_OK && S.witness_ok) ? S.found_parent : TRACE_NONE;
       R.final_move = S.found_move;
       R.witness_len = 0;
-      R.has_witness = (verdict == V_OK && S.witness_ok) ? 2u : 0u;  // resolved by walk_kernel
+      R.deep_trace = (verdict == V_ILLEGAL && S.witness_ok) ? deep_trace : TRACE_NONE;
+      R.deep_len = deep_len;
+      R.has_witness = ((verdict == V_OK || R.deep_trace != TRACE_NONE) && S.witness_ok) ? 2u : 0u;  // resolved by walk_kernel
       PROF_ADD(8, rounds);
     }
     __syncthreads();
@@ -674,26 +683,32 @@ __global__ __launch_bounds__(BT) void search_kernel(Params p) {
 }
 
 // Witness extraction: one lane per history walks the parent chain backwards
-// and writes the move list in order.
+// and writes the move list in order. Ok: the completing move after the path
+// to its parent. Illegal: the path to a configuration of the deepest
+// non-empty round (the partial linearization the visualization shows).
 __global__ void walk_kernel(uint32_t n, HistResult* res, const TraceEnt* trace, uint32_t* moves) {
   const uint32_t h = blockIdx.x * blockDim.x + threadIdx.x;
   if (h >= n) return;
   HistResult r = res[h];
-  if (r.verdict != V_OK || r.has_witness != 2u) return;
-  const uint32_t len = (r.final_move == TRACE_NONE) ? 0u : r.rounds;
+  if (r.has_witness != 2u) return;
   uint32_t* out = moves + r.witness_off;
-  bool ok = true;
-  if (len) {
-    out[len - 1] = r.final_move;
-    uint32_t idx = r.final_parent;
-    uint32_t pos = len - 1;
-    while (pos > 0 && idx != TRACE_NONE) {
-      const TraceEnt e = trace[idx];
-      out[--pos] = e.move;
-      idx = e.parent;
-    }
-    ok = (pos == 0);
+  uint32_t len, pos, idx;
+  if (r.verdict == V_OK) {
+    len = (r.final_move == TRACE_NONE) ? 0u : r.rounds;
+    if (len) out[len - 1] = r.final_move;
+    pos = len ? len - 1 : 0;
+    idx = r.final_parent;
+  } else {
+    len = r.deep_len;
+    pos = len;
+    idx = r.deep_trace;
   }
+  while (pos > 0 && idx != TRACE_NONE) {
+    const TraceEnt e = trace[idx];
+    out[--pos] = e.move;
+    idx = e.parent;
+  }
+  const bool ok = pos == 0;
   res[h].witness_len = ok ? len : 0u;
   res[h].has_witness = ok ? 1u : 0u;
 }

@@ -51,7 +51,7 @@ void close(const History& h, HostCfg& c, std::vector<uint32_t>& order, std::vect
 }  // namespace
 
 bool rebuild_linearization(const History& h, const uint32_t* moves, uint32_t n_moves, bool p4,
-                           std::vector<uint32_t>& order, std::vector<uint8_t>& ident) {
+                           std::vector<uint32_t>& order, std::vector<uint8_t>& ident, bool partial) {
   order.clear();
   ident.clear();
   if (h.structural) return false;
@@ -81,6 +81,7 @@ bool rebuild_linearization(const History& h, const uint32_t* moves, uint32_t n_m
     c.cnt[j]++;
     close(h, c, order, ident);
   }
+  if (partial) return true;
   if (order.size() != h.n_ops) {
     if (!p4) return false;
     // P4 completion: nothing left constrains the state; finish in return order.
@@ -94,8 +95,7 @@ bool rebuild_linearization(const History& h, const uint32_t* moves, uint32_t n_m
   return order.size() == h.n_ops;
 }
 
-bool replay_path(const History& h, const uint32_t* order, const uint8_t* ident, size_t n) {
-  if (!real_time_ok(h, order, n)) return false;
+static bool replay_states(const History& h, const uint32_t* order, const uint8_t* ident, size_t n) {
   State s{0, 0, 0};
   for (size_t i = 0; i < n; ++i) {
     const OpRec r = h.rec_of(order[i]);
@@ -111,6 +111,30 @@ bool replay_path(const History& h, const uint32_t* order, const uint8_t* ident, 
     s = want;
   }
   return true;
+}
+
+bool replay_path(const History& h, const uint32_t* order, const uint8_t* ident, size_t n) {
+  return real_time_ok(h, order, n) && replay_states(h, order, ident, n);
+}
+
+bool replay_prefix(const History& h, const uint32_t* order, const uint8_t* ident, size_t n) {
+  if (h.structural || n > h.n_ops) return false;
+  std::vector<uint8_t> in(h.n_ops, 0);
+  uint32_t max_call = 0;
+  for (size_t i = 0; i < n; ++i) {
+    if (order[i] >= h.n_ops || in[order[i]]) return false;
+    in[order[i]] = 1;
+    max_call = std::max(max_call, h.op_call[order[i]]);
+  }
+  // closed under real-time predecessors: nothing outside returned before an op inside was called
+  for (uint32_t d = 0; d < h.n_ops; ++d)
+    if (!in[d] && h.op_ret[d] < max_call) return false;
+  uint32_t later_min_ret = EV_INF;
+  for (size_t i = n; i-- > 0;) {
+    if (h.op_call[order[i]] >= later_min_ret) return false;
+    later_min_ret = std::min(later_min_ret, h.op_ret[order[i]]);
+  }
+  return replay_states(h, order, ident, n);
 }
 
 bool real_time_ok(const History& h, const uint32_t* order, size_t n) {

@@ -127,20 +127,45 @@ def test_c4_sample_vs_wgl(checker):
     assert all(r.witness is not None for r in res if r.verdict == s2.Ok)
 
 
-def test_cli_verdicts_and_exit_codes():
+def test_cli_verdicts_and_exit_codes(tmp_path):
     import json
     import subprocess
     for c in golden("reference_cases.json")["cases"]:
         if not c.get("jsonl_file"):
             continue
         p = subprocess.run([s2.CLI_PATH, "-file=" + os.path.join(GOLDEN, c["jsonl_file"])], capture_output=True,
-                           text=True, timeout=120)
-        line = json.loads(p.stderr.strip().splitlines()[-1])
+                           text=True, timeout=120, cwd=tmp_path)
+        lines = [json.loads(x) for x in p.stderr.strip().splitlines()]
+        line = lines[-1]
+        # main.go:608-631: the visualization is written before the verdict line
+        viz = [x for x in lines if x["msg"] == "wrote visualization"]
+        assert len(viz) == 1 and viz[0]["file"].startswith("porcupine-outputs/" + c["jsonl_file"][:-6] + "-")
+        html = (tmp_path / viz[0]["file"]).read_text()
+        assert ("<h2>Ok</h2>" if c["expected"] == "Ok" else "<h2>Illegal</h2>") in html
+        assert "append(len[" in html
         if c["expected"] == "Ok":
             assert p.returncode == 0 and line["msg"] == "passed: is linearizable", (c["name"], p.stderr)
         else:
             assert p.returncode == 1 and line["msg"] == "failed: is NOT linearizable" and line["res"] == "Illegal"
     # stdin
     with open(os.path.join(GOLDEN, "ref_BasicNoConcurrency.jsonl"), "rb") as f:
-        p = subprocess.run([s2.CLI_PATH, "-file", "-"], stdin=f, capture_output=True, timeout=120)
+        p = subprocess.run([s2.CLI_PATH, "-file", "-"], stdin=f, capture_output=True, timeout=120, cwd=tmp_path)
     assert p.returncode == 0
+    assert list((tmp_path / "porcupine-outputs").glob("stdin-*.html"))
+
+
+def test_illegal_partial_prefix(checker):
+    """Illegal verdicts carry the deepest certified linearized prefix (the
+    visualization's partial linearization); it is a real-time-closed prefix
+    whose claimed outcomes replay through the CPU model (checked in the library)."""
+    from s2_verification_amd import workloads as W
+    hs = [h for h in W.c4_histories(200) if True]
+    res = checker.check_batch(hs)
+    bad = [(h, r) for h, r in zip(hs, res) if r.verdict == s2.Illegal]
+    assert bad
+    with_partial = [(h, r) for h, r in bad if r.partial is not None]
+    assert len(with_partial) >= len(bad) // 2
+    for h, r in with_partial:
+        ids = [e.Id for e in h.events()]
+        assert len(set(r.partial)) == len(r.partial) and set(r.partial) <= set(ids)
+        assert len(r.partial) < h.info()["n_ops"]
