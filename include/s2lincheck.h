@@ -154,6 +154,12 @@ const char* s2lc_version(void);
  * message into err. */
 int s2lc_load_jsonl(const char* path_or_dash, const uint8_t* buf, size_t len,
                     s2lc_history** out, char* err, size_t errlen);
+/* Decode n JSONL histories (DST seeds, C4) from memory, one worker thread per
+ * core (n_threads <= 0) or n_threads: eventsFromReader per buffer, histories
+ * being independent. All or nothing: on the first (lowest-index) failure every
+ * out[i] is NULL, *err_index names the buffer and err its decode error. */
+int s2lc_load_jsonl_many(const uint8_t* const* bufs, const size_t* lens, size_t n, int n_threads,
+                         s2lc_history** out, size_t* err_index, char* err, size_t errlen);
 /* Build a history from porcupine-style events; all buffers are copied. */
 int s2lc_history_from_events(const s2lc_event* events, size_t n_events,
                              s2lc_history** out, char* err, size_t errlen);

@@ -11,7 +11,7 @@ TAG=${1:-run}
 OUT=gpurun_out/$TAG
 mkdir -p "$OUT"
 export TMPDIR=/tmp
-SHORT="--no-cpu-baseline --no-c5 --no-small --steps 3 --warmup 1"
+SHORT="--no-cpu-baseline --no-c5 --no-small --no-e2e --steps 3 --warmup 1"
 timeout -k 10 300 python3 bench.py > "$OUT/bench.json" 2> "$OUT/bench.err"
 timeout -k 10 200 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/stats" -o c4 -- \
   python3 bench.py $SHORT > "$OUT/stats_bench.json" 2> "$OUT/stats.err"

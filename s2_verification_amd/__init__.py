@@ -160,6 +160,9 @@ SIGNATURES = [
                                            ctypes.POINTER(ctypes.c_size_t)]),
     ("s2lc_simulate_history", ctypes.c_int, [ctypes.POINTER(c_sim_params), ctypes.POINTER(_P)]),
     ("s2lc_free", None, [_P]),
+    ("s2lc_load_jsonl_many", ctypes.c_int, [ctypes.POINTER(ctypes.c_void_p), ctypes.POINTER(ctypes.c_size_t),
+                                            ctypes.c_size_t, ctypes.c_int, ctypes.POINTER(_P),
+                                            ctypes.POINTER(ctypes.c_size_t), ctypes.c_char_p, ctypes.c_size_t]),
     ("s2lc_visualize", ctypes.c_int, [_P, ctypes.POINTER(c_result), ctypes.c_char_p]),
     ("s2lc_witness_from_moves", ctypes.c_int, [_P, ctypes.POINTER(ctypes.c_uint32), ctypes.c_size_t, ctypes.c_int,
                                                ctypes.POINTER(ctypes.c_int64), ctypes.c_size_t]),
@@ -363,6 +366,21 @@ class History:
     def replay(self, order: Sequence[int]) -> bool:
         arr = (ctypes.c_uint32 * len(order))(*order)
         return lib().s2lc_replay(self._h, arr, len(order)) == 0
+
+
+def load_many(blobs: Sequence[bytes], threads: int = 0) -> List[History]:
+    """Decode many JSONL histories in parallel (s2lc_load_jsonl_many)."""
+    n = len(blobs)
+    keep = [ctypes.create_string_buffer(b, len(b)) for b in blobs]
+    bufs = (ctypes.c_void_p * max(1, n))(*[ctypes.cast(k, ctypes.c_void_p) for k in keep])
+    lens = (ctypes.c_size_t * max(1, n))(*[len(b) for b in blobs])
+    out = (ctypes.c_void_p * max(1, n))()
+    bad = ctypes.c_size_t(0)
+    err = ctypes.create_string_buffer(1024)
+    rc = lib().s2lc_load_jsonl_many(bufs, lens, n, threads, out, ctypes.byref(bad), err, 1024)
+    if rc:
+        raise S2LCError(rc, err.value.decode(errors="replace"))
+    return [History(out[i]) for i in range(n)]
 
 
 def events_from_reader(data) -> History:

@@ -6,7 +6,9 @@
 #include <string.h>
 
 #include <new>
+#include <atomic>
 #include <string>
+#include <thread>
 #include <vector>
 
 #include "history.h"
@@ -134,6 +136,60 @@ int s2lc_load_jsonl(const char* path, const uint8_t* buf, size_t len, s2lc_histo
     set_err(err, errlen, "internal error");
     return S2LC_EINVAL;
   }
+}
+
+int s2lc_load_jsonl_many(const uint8_t* const* bufs, const size_t* lens, size_t n, int n_threads,
+                         s2lc_history** out, size_t* err_index, char* err, size_t errlen) {
+  if (!out || (n && (!bufs || !lens))) return S2LC_EINVAL;
+  for (size_t i = 0; i < n; ++i) out[i] = nullptr;
+  if (n_threads <= 0) n_threads = (int)std::max(1u, std::thread::hardware_concurrency());
+  n_threads = (int)std::min<size_t>((size_t)n_threads, std::max<size_t>(n, 1));
+  std::atomic<size_t> next{0};
+  std::atomic<size_t> first_bad{SIZE_MAX};
+  std::vector<int> rcs(n, 0);
+  std::vector<std::string> errs(n);
+  auto work = [&]() {
+    for (;;) {
+      const size_t i = next.fetch_add(1);
+      if (i >= n) return;
+      try {
+        s2lc_history* h = new s2lc_history();
+        int rc = load_jsonl(bufs[i], lens[i], h->h, errs[i]);
+        if (!rc) {
+          rc = h->h.finalize();
+          if (rc) errs[i] = h->h.error;
+        }
+        if (rc) {
+          delete h;
+          rcs[i] = rc;
+          size_t cur = first_bad.load();
+          while (i < cur && !first_bad.compare_exchange_weak(cur, i)) {}
+        } else {
+          out[i] = h;
+        }
+      } catch (...) {
+        rcs[i] = S2LC_ENOMEM;
+        errs[i] = "out of memory";
+        size_t cur = first_bad.load();
+        while (i < cur && !first_bad.compare_exchange_weak(cur, i)) {}
+      }
+    }
+  };
+  std::vector<std::thread> ts;
+  for (int t = 1; t < n_threads; ++t) ts.emplace_back(work);
+  work();
+  for (auto& t : ts) t.join();
+  const size_t bad = first_bad.load();
+  if (bad != SIZE_MAX) {
+    for (size_t i = 0; i < n; ++i) {
+      delete out[i];
+      out[i] = nullptr;
+    }
+    if (err_index) *err_index = bad;
+    set_err(err, errlen, "history " + std::to_string(bad) + ": " + errs[bad]);
+    return rcs[bad];
+  }
+  return 0;
 }
 
 int s2lc_history_from_events(const s2lc_event* ev, size_t n, s2lc_history** out, char* err, size_t errlen) {

@@ -150,3 +150,27 @@ def test_simulator_jsonl_roundtrip():
         # serde field order (history.rs:133-138)
         first = json.loads(data.split(b"\n")[0])
         assert list(first.keys()) == ["event", "client_id", "op_id"]
+
+
+def test_load_many_parallel_equals_sequential():
+    """s2lc_load_jsonl_many (threads) decodes each buffer exactly like s2lc_load_jsonl."""
+    import s2_verification_amd as s2
+    from s2_verification_amd import workloads as W
+    blobs = [s2.simulate_jsonl(**W.c4_params(seed)) for seed in range(40)]
+    many = s2.load_many(blobs, threads=4)
+    for b, h in zip(blobs, many):
+        one = s2.events_from_reader(b)
+        assert h.info() == one.info()
+        assert h.events() == one.events()
+
+
+def test_load_many_reports_first_bad_buffer():
+    import pytest
+    import s2_verification_amd as s2
+    from s2_verification_amd import workloads as W
+    blobs = [s2.simulate_jsonl(**W.c4_params(seed)) for seed in range(6)]
+    blobs[4] = b'{"event":{"Start":"Read"},"client_id":1'
+    blobs[2] = blobs[2] + b"not json\n"
+    with pytest.raises(s2.S2LCError) as e:
+        s2.load_many(blobs, threads=3)
+    assert "history 2:" in str(e.value)
