@@ -20,3 +20,6 @@ timeout -s KILL 120 rocprofv3 --pmc FETCH_SIZE --output-format csv -d "$OUT/pmc_
 timeout -s KILL 120 rocprofv3 --pmc WRITE_SIZE --output-format csv -d "$OUT/pmc_write" -o c4 -- \
   python3 bench.py $SHORT > "$OUT/pmc_write_bench.json" 2> "$OUT/pmc_write.err"
 python3 profiles/pmc_summary.py "$OUT/pmc_fetch" "$OUT/pmc_write" "$OUT/pmc_c4.json" "pack_kernel<16>"
+# 4. the level search on the single hard history (C5)      -> gpurun_out/<tag>/c5stats/
+timeout -k 10 200 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/c5stats" -o c5 -- \
+  python3 tools/c5run.py C5 > "$OUT/c5run.log" 2> "$OUT/c5stats.err"

@@ -371,7 +371,7 @@ class History:
 def load_many(blobs: Sequence[bytes], threads: int = 0) -> List[History]:
     """Decode many JSONL histories in parallel (s2lc_load_jsonl_many)."""
     n = len(blobs)
-    keep = [ctypes.create_string_buffer(b, len(b)) for b in blobs]
+    keep = [ctypes.c_char_p(bytes(b)) for b in blobs]  # points into the bytes objects (no copy for bytes)
     bufs = (ctypes.c_void_p * max(1, n))(*[ctypes.cast(k, ctypes.c_void_p) for k in keep])
     lens = (ctypes.c_size_t * max(1, n))(*[len(b) for b in blobs])
     out = (ctypes.c_void_p * max(1, n))()

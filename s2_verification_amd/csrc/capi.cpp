@@ -363,45 +363,64 @@ int s2lc_batch_results(s2lc_ctx* c, s2lc_batch* b, s2lc_result* out, int with_wi
         return S2LC_EHIP;
       }
     }
-    for (uint32_t i = 0; i < B.n_hist; ++i) {
-      const HistResult& r = B.h_res[i];
-      s2lc_result& o = out[i];
-      memset(&o, 0, sizeof o);
-      o.verdict = (int32_t)r.verdict;
-      o.reason = (int32_t)r.reason;
-      o.configs_explored = r.configs;
-      o.rounds = r.rounds;
-      o.n_ops = B.src[i]->n_ops;
-      o.device_ms = b->stats.kernel_ms;
-      if (want_w && r.verdict == V_OK && r.has_witness == 1) {
+    // Witness rebuild + CPU-model certification is independent per history:
+    // spread over worker threads (S2LC_THREADS, default min(16, cores)).
+    std::atomic<uint32_t> next{0};
+    std::atomic<int> oom{0};
+    auto work = [&]() {
+      for (;;) {
+        const uint32_t i = next.fetch_add(1);
+        if (i >= B.n_hist) return;
+        const HistResult& r = B.h_res[i];
+        s2lc_result& o = out[i];
+        memset(&o, 0, sizeof o);
+        o.verdict = (int32_t)r.verdict;
+        o.reason = (int32_t)r.reason;
+        o.configs_explored = r.configs;
+        o.rounds = r.rounds;
+        o.n_ops = B.src[i]->n_ops;
+        o.device_ms = b->stats.kernel_ms;
+        if (!want_w || r.has_witness != 1 || (r.verdict != V_OK && r.verdict != V_ILLEGAL)) continue;
         const History& H = *B.src[i];
         std::vector<uint32_t> order;
         std::vector<uint8_t> ident;
-        const bool ok =
-            rebuild_linearization(H, B.h_moves.data() + r.witness_off, r.witness_len, r.p4 != 0, order, ident, false) &&
-            replay_path(H, order.data(), ident.data(), order.size());
-        if (!ok) {
-          o.reason = S2LC_R_WITNESS_INVALID;
-          continue;
+        try {
+          if (r.verdict == V_OK) {
+            const bool ok = rebuild_linearization(H, B.h_moves.data() + r.witness_off, r.witness_len, r.p4 != 0, order,
+                                                  ident, false) &&
+                            replay_path(H, order.data(), ident.data(), order.size());
+            if (!ok) {
+              o.reason = S2LC_R_WITNESS_INVALID;
+              continue;
+            }
+            o.witness = (int64_t*)malloc(sizeof(int64_t) * (order.size() ? order.size() : 1));
+            if (!o.witness) { oom = 1; continue; }
+            for (size_t k = 0; k < order.size(); ++k) o.witness[k] = H.op_ids[order[k]];
+            o.witness_len = (uint32_t)order.size();
+          } else if (rebuild_linearization(H, B.h_moves.data() + r.witness_off, r.witness_len, false, order, ident,
+                                           true) &&
+                     replay_prefix(H, order.data(), ident.data(), order.size())) {
+            o.partial = (int64_t*)malloc(sizeof(int64_t) * (order.size() ? order.size() : 1));
+            if (!o.partial) { oom = 1; continue; }
+            for (size_t k = 0; k < order.size(); ++k) o.partial[k] = H.op_ids[order[k]];
+            o.partial_len = (uint32_t)order.size();
+          }
+        } catch (...) {
+          oom = 1;
         }
-        o.witness = (int64_t*)malloc(sizeof(int64_t) * (order.size() ? order.size() : 1));
-        if (!o.witness) { c->err = "out of memory"; return S2LC_ENOMEM; }
-        for (size_t k = 0; k < order.size(); ++k) o.witness[k] = H.op_ids[order[k]];
-        o.witness_len = (uint32_t)order.size();
       }
-      if (want_w && r.verdict == V_ILLEGAL && r.has_witness == 1) {
-        const History& H = *B.src[i];
-        std::vector<uint32_t> order;
-        std::vector<uint8_t> ident;
-        if (rebuild_linearization(H, B.h_moves.data() + r.witness_off, r.witness_len, false, order, ident, true) &&
-            replay_prefix(H, order.data(), ident.data(), order.size())) {
-          o.partial = (int64_t*)malloc(sizeof(int64_t) * (order.size() ? order.size() : 1));
-          if (!o.partial) { c->err = "out of memory"; return S2LC_ENOMEM; }
-          for (size_t k = 0; k < order.size(); ++k) o.partial[k] = H.op_ids[order[k]];
-          o.partial_len = (uint32_t)order.size();
-        }
-      }
+    };
+    int n_threads = 1;
+    if (want_w) {
+      const char* e = getenv("S2LC_THREADS");
+      n_threads = e ? atoi(e) : (int)std::min(16u, std::max(1u, std::thread::hardware_concurrency()));
+      n_threads = std::max(1, std::min<int>(n_threads, (int)(B.n_hist / 64 + 1)));
     }
+    std::vector<std::thread> ts;
+    for (int t = 1; t < n_threads; ++t) ts.emplace_back(work);
+    work();
+    for (auto& t : ts) t.join();
+    if (oom) { c->err = "out of memory"; return S2LC_ENOMEM; }
     return 0;
   } catch (const std::bad_alloc&) {
     c->err = "out of memory";
