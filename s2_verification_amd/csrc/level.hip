@@ -87,7 +87,7 @@ int level_buffers(DevBatch& b, uint32_t kmax, std::string& err) {
     if (lv_ensure((void**)&L.idx[i], L.idx_bytes[i], scap * sizeof(uint32_t), err)) return S2LC_EHIP;
   }
   if (lv_ensure((void**)&L.ht, L.ht_bytes, ht * 8, err)) return S2LC_EHIP;
-  if (!L.ctl) LVCHK(hipMalloc(&L.ctl, sizeof(LvCtl)));
+  if (!L.ctl) LVCHK(hipMalloc(&L.ctl, 2 * sizeof(LvCtl)));  // double buffered by round
   if (!L.h_ctl) LVCHK(hipHostMalloc(&L.h_ctl, sizeof(LvCtl), hipHostMallocDefault));
   LVCHK(hipMemset(L.ht, 0xFF, ht * 8));
   L.kmax = kmax;
@@ -126,6 +126,10 @@ int level_search(DevBatch& b, uint32_t h, hipStream_t st, uint64_t max_configs, 
     LVCHK(hipStreamSynchronize(st));
   }
   bool wit = witness && b.trace != nullptr;
+
+  LvCtl* d_hc = nullptr;  // device view of the host-mapped control mirror
+  LVCHK(hipHostGetDevicePointer((void**)&d_hc, hc, 0));
+  LVCHK(hipMemsetAsync(L.ctl, 0, 2 * sizeof(LvCtl), st));
 
   LvParams p;
   memset(&p, 0, sizeof p);
@@ -185,14 +189,24 @@ int level_search(DevBatch& b, uint32_t h, hipStream_t st, uint64_t max_configs, 
     p.witness = wit ? 1u : 0u;
     p.tbase = (uint32_t)tnext;
     ++rounds;
-    // one round, in frontier chunks (normally one)
-    memset(hc, 0, sizeof(LvCtl));
+    // one round, in frontier chunks (normally one). Round r uses control
+    // block r & 1, which round r-1's lv_expand zeroed, and lv_insert publishes
+    // it to the host-mapped mirror hc: the single-chunk round needs no copies.
+    LvCtl* const ctl_r = reinterpret_cast<LvCtl*>(L.ctl) + (rounds & 1);
+    p.ctl = ctl_r;
+    p.ctl_next = reinterpret_cast<LvCtl*>(L.ctl) + ((rounds + 1) & 1);
+    p.publish = d_hc;
     uint32_t f0 = 0, chunk = nf, st_lo = 0, nn_lo = 0;
     bool stop = false;
+    bool first = true;
     while (f0 < nf) {
       const uint32_t f1 = (uint32_t)std::min<uint64_t>(nf, (uint64_t)f0 + chunk);
-      hc->nchild = 0; hc->nstage = st_lo; hc->nnext = nn_lo; hc->overflow = 0;
-      LVCHK(hipMemcpyAsync(L.ctl, hc, sizeof(LvCtl), hipMemcpyHostToDevice, st));
+      if (!first) {
+        memset(hc, 0, sizeof(LvCtl));
+        hc->nchild = 0; hc->nstage = st_lo; hc->nnext = nn_lo; hc->overflow = 0;
+        LVCHK(hipMemcpyAsync(ctl_r, hc, sizeof(LvCtl), hipMemcpyHostToDevice, st));
+      }
+      first = false;
       p.f0 = f0; p.f1 = f1; p.st_lo = st_lo;
       const uint64_t lanes = (uint64_t)(f1 - f0) * K;
       const uint32_t g_exp = (uint32_t)std::min<uint64_t>(max_grid, (lanes + LV_BLOCK - 1) / LV_BLOCK);
@@ -202,8 +216,7 @@ int level_search(DevBatch& b, uint32_t h, hipStream_t st, uint64_t max_configs, 
       LVCHK(lv_dispatch(kmax, 0, std::max<uint32_t>(1, g_exp), p, st));
       LVCHK(lv_dispatch(kmax, 1, std::max<uint32_t>(1, g_cls), p, st));
       LVCHK(lv_dispatch(kmax, 2, std::max<uint32_t>(1, g_ins), p, st));
-      LVCHK(hipMemcpyAsync(hc, L.ctl, sizeof(LvCtl), hipMemcpyDeviceToHost, st));
-      LVCHK(hipStreamSynchronize(st));
+      LVCHK(hipStreamSynchronize(st));  // hc was published by lv_insert's last block
       if (hc->found) break;
       if (hc->overflow) {
         if (f1 - f0 == 1) { verdict = V_UNKNOWN; reason = S2LC_R_FRONTIER; stop = true; break; }

@@ -65,7 +65,8 @@ struct LvCtl {
   uint32_t overflow;  // 1: children over capacity, 2: staging over capacity
   uint32_t found_parent, found_move, found_p4;
   unsigned long long children;  // running total
-  uint32_t _pad[6];
+  uint32_t done_blocks;         // lv_insert blocks finished (the last one publishes)
+  uint32_t _pad[5];
 };
 
 struct LvParams {
@@ -89,6 +90,8 @@ struct LvParams {
   unsigned long long* ht;
   uint32_t ht_mask;
   uint32_t clear_slots;  // lv_expand clears the table slots of the frontier it expands
+  LvCtl* ctl_next;       // lv_expand zeroes the next round's control block (double buffer)
+  LvCtl* publish;        // host-mapped mirror lv_insert's last block copies the control block to
   TraceEnt* trace;
   uint32_t tbase;        // trace index of nxt_idx[0] (in this process's pool)
   uint32_t witness;
@@ -165,6 +168,8 @@ __device__ __forceinline__ uint64_t lv_state_term(uint64_t tail, uint64_t hash, 
 // ---- expand: one lane per (frontier position, chain) ----------------------
 template <int KMAX>
 __global__ __launch_bounds__(LV_BLOCK) void lv_expand(LvParams p) {
+  if (p.ctl_next && blockIdx.x == 0 && threadIdx.x < sizeof(LvCtl) / 4)
+    reinterpret_cast<uint32_t*>(p.ctl_next)[threadIdx.x] = 0;
   const uint32_t K = p.K;
   const uint64_t total = (uint64_t)(p.f1 - p.f0) * K;
   const uint64_t stride = (uint64_t)gridDim.x * LV_BLOCK;
@@ -350,8 +355,7 @@ __device__ __forceinline__ bool lv_eq(const LCfg<KMAX>* a, const LCfg<KMAX>* b, 
 // ---- insert: one lane per staged configuration -----------------------------
 template <int KMAX>
 __global__ __launch_bounds__(LV_BLOCK) void lv_insert(LvParams p) {
-  if (p.ctl->overflow) return;
-  const uint32_t hi = min(p.ctl->nstage, p.scap);
+  const uint32_t hi = p.ctl->overflow ? 0u : min(p.ctl->nstage, p.scap);
   const uint32_t stride = gridDim.x * LV_BLOCK;
   for (uint32_t b0 = p.st_lo + blockIdx.x * LV_BLOCK; b0 < hi; b0 += stride) {
     const uint32_t k = b0 + threadIdx.x;
@@ -379,6 +383,23 @@ __global__ __launch_bounds__(LV_BLOCK) void lv_insert(LvParams p) {
         c->trace = p.tgid + p.tbase + n;
         p.trace[p.tbase + n] = TraceEnt{c->ptrace, c->move};
       }
+    }
+  }
+  // the last block to finish copies the control block to the host-mapped
+  // mirror: the host then needs no copy, only the stream sync
+  if (p.publish) {
+    __syncthreads();
+    __shared__ uint32_t s_last;
+    if (threadIdx.x == 0) {
+      __threadfence();
+      s_last = atomicAdd(&p.ctl->done_blocks, 1u) == gridDim.x - 1;
+    }
+    __syncthreads();
+    if (s_last && threadIdx.x < sizeof(LvCtl) / 4) {
+      __threadfence();
+      const uint32_t v = atomicAdd(reinterpret_cast<uint32_t*>(p.ctl) + threadIdx.x, 0u);
+      reinterpret_cast<volatile uint32_t*>(p.publish)[threadIdx.x] = v;
+      __threadfence_system();
     }
   }
 }
