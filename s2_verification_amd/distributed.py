@@ -232,7 +232,7 @@ def check_distributed(checker, history: History, group=None, witness: bool = Tru
     rounds = 0
     configs = 0
     part_rounds = 0
-    replicated = wide > 0 and world > 1 or world == 1
+    replicated = wide > 0  # wide = 0: every round partitioned (also on one rank: a self-exchange)
     t0 = time.perf_counter()
     first = True  # round 0 closes the initial configuration; rounds counts the ones after it
     try:
