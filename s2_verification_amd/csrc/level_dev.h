@@ -252,27 +252,35 @@ __global__ __launch_bounds__(LV_BLOCK) void lv_close(LvParams p) {
     }
     int res;
     uint32_t minret;
+    // Head fields of the owned chains, kept in registers across passes: a pass
+    // reloads only the chains the previous pass advanced (the first pass loads
+    // every head), so the closure's L2 traffic is one head per chain plus one
+    // per advanced op instead of one per chain per pass.
+    uint32_t callv[NQ], flv[NQ], retv[NQ];
+    uint64_t otl[NQ], ohs[NQ], smv[NQ];
+    uint32_t need = (1u << NQ) - 1u;
     for (;;) {
       uint32_t mr = EV_INF;
       uint64_t bd = REQ_NONE;
-      uint32_t callv[NQ], flv[NQ];
-      uint64_t otl[NQ], ohs[NQ];
 #pragma unroll
       for (int q = 0; q < NQ; ++q) {
         const uint32_t j = (uint32_t)lane + 64u * q;
         if (j < K) {
-          const OpRec* r = p.recs + csj[q] + cnt[q];
-          const uint4 obs = ld16(r, 16);
-          const uint4 mid = ld16(r, 32);
-          flv[q] = r->flags;
-          otl[q] = (uint64_t)obs.x | ((uint64_t)obs.y << 32);
-          ohs[q] = (uint64_t)obs.z | ((uint64_t)obs.w << 32);
-          callv[q] = mid.z;
-          mr = min(mr, mid.w);
-          const uint64_t sm = (uint64_t)mid.x | ((uint64_t)mid.y << 32);
-          bd = sm < bd ? sm : bd;
+          if ((need >> q) & 1u) {
+            const OpRec* r = p.recs + csj[q] + cnt[q];
+            const uint4 obs = ld16(r, 16);
+            const uint4 mid = ld16(r, 32);
+            flv[q] = r->flags;
+            otl[q] = (uint64_t)obs.x | ((uint64_t)obs.y << 32);
+            ohs[q] = (uint64_t)obs.z | ((uint64_t)obs.w << 32);
+            callv[q] = mid.z;
+            retv[q] = mid.w;
+            smv[q] = (uint64_t)mid.x | ((uint64_t)mid.y << 32);
+          }
+          mr = min(mr, retv[q]);
+          bd = smv[q] < bd ? smv[q] : bd;
         } else {
-          flv[q] = OPF_SENTINEL; otl[q] = 0; ohs[q] = 0; callv[q] = EV_INF;
+          flv[q] = OPF_SENTINEL; otl[q] = 0; ohs[q] = 0; callv[q] = EV_INF; retv[q] = EV_INF; smv[q] = REQ_NONE;
         }
       }
       minret = wave_min_u32(mr);
@@ -300,6 +308,7 @@ __global__ __launch_bounds__(LV_BLOCK) void lv_close(LvParams p) {
       }
 #pragma unroll
       for (int q = 0; q < NQ; ++q) cnt[q] += (adv >> q) & 1u;
+      need = adv;
     }
     if (res == CL_DEAD) continue;
     const uint32_t ptrace = pc ? pc->trace : TRACE_NONE;

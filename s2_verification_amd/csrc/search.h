@@ -105,6 +105,7 @@ struct DevBatch {
   // host mirrors
   std::vector<HistDesc> h_hist;
   std::vector<HistResult> h_res;
+  bool h_res_pinned = false;          // h_res page-locked (hipHostRegister) for the per-run read-back
   std::vector<uint32_t> h_moves_off;  // witness_off per history
   uint64_t moves_cap = 0;
   std::vector<uint32_t> h_moves;

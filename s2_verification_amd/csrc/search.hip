@@ -216,14 +216,20 @@ int batch_upload(DevBatch& b, const std::vector<const History*>& hs, std::string
   HIPCHK(hipMemcpy(b.chain_start, cs.data(), cs.size() * sizeof(uint32_t), hipMemcpyHostToDevice));
   if (!hs.empty()) HIPCHK(hipMemcpy(b.hist, b.h_hist.data(), hs.size() * sizeof(HistDesc), hipMemcpyHostToDevice));
   if (!order.empty()) HIPCHK(hipMemcpy(b.order, order.data(), order.size() * sizeof(uint32_t), hipMemcpyHostToDevice));
+  if (b.h_res_pinned) { (void)hipHostUnregister(b.h_res.data()); b.h_res_pinned = false; }
   b.h_res.assign(hs.size(), HistResult{});
   for (size_t i = 0; i < hs.size(); ++i) b.h_res[i].witness_off = b.h_moves_off[i];
+  // every run reads the results back: page-lock them so that copy is a direct DMA
+  if (!hs.empty() && hipHostRegister(b.h_res.data(), hs.size() * sizeof(HistResult), hipHostRegisterDefault) == hipSuccess)
+    b.h_res_pinned = true;
+  (void)hipGetLastError();  // a failed registration only costs the staged copy
   if (!hs.empty()) HIPCHK(hipMemcpy(b.res, b.h_res.data(), hs.size() * sizeof(HistResult), hipMemcpyHostToDevice));
   return 0;
 }
 
 void batch_release(DevBatch& b) {
   level_release(b);
+  if (b.h_res_pinned) { (void)hipHostUnregister(b.h_res.data()); b.h_res_pinned = false; }
   void* ptrs[] = {b.recs, b.pool, b.chain_start, b.hist, b.order, b.res, b.moves, b.counter, b.trace, b.trace_head, b.slab};
   for (void* q : ptrs) if (q) (void)hipFree(q);
   b.recs = nullptr; b.pool = nullptr; b.chain_start = nullptr; b.hist = nullptr; b.order = nullptr;
@@ -294,6 +300,12 @@ int batch_run(DevBatch& b, hipStream_t stream, uint64_t max_configs, bool witnes
       HIPCHK(hipMemcpyToSymbol(HIP_SYMBOL(g_prof), z, sizeof z));
     }
 #endif
+    // Both packed launches, then (witness on) the walk of the histories they
+    // settled, then one results read-back: a batch that needs no other pass
+    // (all of C4) costs a single host sync per run.
+    hipEvent_t pe[4];
+    for (hipEvent_t& e : pe) HIPCHK(hipEventCreate(&e));
+    bool launched[2] = {false, false};
     for (int li = 0; li < 2; ++li) {
       const uint32_t n_l = li == 0 ? b.n_pack16 : b.n_pack32;
       if (n_l == 0) continue;
@@ -309,19 +321,32 @@ int batch_run(DevBatch& b, hipStream_t stream, uint64_t max_configs, bool witnes
       const uint32_t groups = PACK_BLOCK / L;
       const uint32_t grid = std::max<uint32_t>(
           1, std::min<uint32_t>((n_l + groups - 1) / groups, (uint32_t)n_cu * (uint32_t)std::max(1, bpc)));
-      HIPCHK(hipEventRecord(e0, stream));
+      HIPCHK(hipEventRecord(pe[2 * li], stream));
       if (li == 0) hipLaunchKernelGGL(pack_kernel<16>, dim3(grid), dim3(PACK_BLOCK), smem, stream, pp);
       else hipLaunchKernelGGL(pack_kernel<32>, dim3(grid), dim3(PACK_BLOCK), smem, stream, pp);
       HIPCHK(hipGetLastError());
-      HIPCHK(hipEventRecord(e1, stream));
-      HIPCHK(hipEventSynchronize(e1));
+      HIPCHK(hipEventRecord(pe[2 * li + 1], stream));
+      launched[li] = true;
+      st.launches++;
+    }
+    if (b.n_pack16 + b.n_pack32) {
+      if (witness) {
+        hipLaunchKernelGGL(walk_kernel, dim3((b.n_hist + 255) / 256), dim3(256), 0, stream, b.n_hist, b.res,
+                           (const TraceEnt*)b.trace, b.moves);
+        HIPCHK(hipGetLastError());
+      }
+      HIPCHK(hipMemcpyAsync(b.h_res.data(), b.res, b.n_hist * sizeof(HistResult), hipMemcpyDeviceToHost, stream));
+      HIPCHK(hipStreamSynchronize(stream));
+    }
+    for (int li = 0; li < 2; ++li) {
+      if (!launched[li]) continue;
       float ms = 0;
-      HIPCHK(hipEventElapsedTime(&ms, e0, e1));
+      HIPCHK(hipEventElapsedTime(&ms, pe[2 * li], pe[2 * li + 1]));
       st.kernel_ms += ms;
       st.pack_ms += ms;
       if (li == 0) st.pack16_ms = ms;
-      st.launches++;
     }
+    for (hipEvent_t e : pe) (void)hipEventDestroy(e);
 #ifdef S2LC_PROF
     {
       unsigned long long gp[16];
@@ -331,10 +356,6 @@ int batch_run(DevBatch& b, hipStream_t stream, uint64_t max_configs, bool witnes
               gp[13], gp[15], gp[10] / rd, gp[11] / rd, gp[12] / rd);
     }
 #endif
-    if (b.n_pack16 + b.n_pack32) {
-      HIPCHK(hipMemcpyAsync(b.h_res.data(), b.res, b.n_hist * sizeof(HistResult), hipMemcpyDeviceToHost, stream));
-      HIPCHK(hipStreamSynchronize(stream));
-    }
     for (uint32_t i = 0; i < b.n_hist; ++i)
       if (!b.forced[i] && b.h_hist[i].K <= 32 && b.h_res[i].verdict == V_UNKNOWN && b.h_res[i].reason == S2LC_R_FRONTIER)
         todo.push_back(i);
@@ -350,9 +371,11 @@ int batch_run(DevBatch& b, hipStream_t stream, uint64_t max_configs, bool witnes
   const uint32_t lds_stage = 32;
   const size_t lds_budget = b.kmax <= 16 ? 10240 : b.kmax <= 32 ? 13312 : 0;
   uint32_t* d_list = nullptr;
+  int n_passes_run = 0;
   for (int pass = 0; pass < 2; ++pass) {
     uint32_t n_pass = (uint32_t)todo.size();
     if (n_pass == 0) break;
+    ++n_passes_run;
     SearchGeom g;
     if (pass == 0) {
       g = make_geom(b.kmax, true, 64, lds_fcap, lds_stage, lds_stage, 1, lds_budget);
@@ -439,7 +462,10 @@ int batch_run(DevBatch& b, hipStream_t stream, uint64_t max_configs, bool witnes
     if (rc) return rc;
   }
   st.kernel_ms += st.level.ms;
-  if (witness && b.n_hist) {
+  // the packed histories were walked with the packed launches; walk again only
+  // for what the other passes settled (walk_kernel skips walked histories)
+  const bool other_work = !use_pack || n_passes_run > 0 || !todo.empty();
+  if (witness && b.n_hist && other_work) {
     hipLaunchKernelGGL(walk_kernel, dim3((b.n_hist + 255) / 256), dim3(256), 0, stream, b.n_hist, b.res,
                        (const TraceEnt*)b.trace, b.moves);
     HIPCHK(hipGetLastError());
