@@ -38,7 +38,7 @@
 extern "C" {
 #endif
 
-#define S2LC_ABI_VERSION 1
+#define S2LC_ABI_VERSION 2
 
 /* CheckResult (porcupine: Ok / Illegal / Unknown). Unknown only when a
  * timeout or configuration budget was set and hit (the reference CLI passes
@@ -53,7 +53,10 @@ enum s2lc_status {
   S2LC_ENODEV = -4,       /* no usable HIP device */
   S2LC_EHIP = -5,         /* HIP runtime error */
   S2LC_EUNSUPPORTED = -6, /* history outside the supported envelope */
-  S2LC_ENOMEM = -7
+  S2LC_ENOMEM = -7,
+  S2LC_EWITNESS = -8      /* an Ok witness failed CPU-model certification: a checker bug.
+                             The results are still written; the affected histories carry
+                             verdict Unknown, reason S2LC_R_WITNESS_INVALID. */
 };
 
 /* StreamInput.InputType, main.go:207-208 */
@@ -102,8 +105,30 @@ typedef struct s2lc_history s2lc_history;
 typedef struct s2lc_ctx s2lc_ctx;
 typedef struct s2lc_batch s2lc_batch;
 
-/* Context options. Zero-initialise, set struct_size = sizeof(s2lc_opts). */
-#define S2LC_F_NO_WITNESS 0x1u   /* do not record the witness trace */
+/* Context options. Zero-initialise, set struct_size = sizeof(s2lc_opts).
+ * A caller built against the first layout (up to `stream`) still works: the
+ * fields after it then keep their zero defaults. */
+#define S2LC_F_NO_WITNESS 0x1u     /* do not record the witness trace */
+#define S2LC_F_ROUND_COUNTS 0x2u   /* record every round's unique-configuration count
+                                      (s2lc_batch_round_counts; search-parity tests) */
+
+/* Search engine routing (tests / diagnostics). AUTO picks per history:
+ * packed lane groups (K <= 32), one workgroup per history (K <= 128), the
+ * device-wide level search (K > 128, or a frontier beyond a workgroup). */
+enum s2lc_engine {
+  S2LC_ENGINE_AUTO = 0,
+  S2LC_ENGINE_WORKGROUP = 1,     /* skip the packed kernels: workgroup passes (LDS, then HBM slab) */
+  S2LC_ENGINE_WORKGROUP_HBM = 2, /* skip the packed kernels and the LDS pass: HBM-slab pass only */
+  S2LC_ENGINE_LEVEL = 3          /* every history through the device-wide level search */
+};
+
+/* Verdict-exact search reductions that can be switched off for
+ * ablation tests; the E-closure is the search's definition and stays on. */
+#define S2LC_RED_P1 0x1u     /* tail lower bound of pending observers */
+#define S2LC_RED_P2 0x2u     /* minimal read at the current tail with another hash */
+#define S2LC_RED_P4 0x4u     /* nothing left constrains the state: complete */
+#define S2LC_RED_IDEFER 0x8u /* indefinite append's identity outcome deferred to minret */
+
 typedef struct s2lc_opts {
   uint32_t struct_size;
   int32_t device;          /* HIP device ordinal; -1 = current device */
@@ -112,6 +137,19 @@ typedef struct s2lc_opts {
   uint64_t max_configs;    /* per-history budget of unique configurations; 0 = unlimited
                               (the search always terminates: it is bounded by n rounds) */
   void* stream;            /* hipStream_t to launch on; NULL = context-owned stream */
+  /* ---- since ABI 2 ---- */
+  uint64_t timeout_us;     /* CheckEventsVerbose's timeout (main.go:606) per s2lc_check /
+                              s2lc_check_batch / s2lc_batch_run call: histories not decided
+                              when it expires get Unknown (S2LC_R_TIMEOUT). 0 = none, the
+                              reference CLI's setting: the result is then Ok or Illegal. */
+  uint32_t engine;         /* s2lc_engine */
+  uint32_t reductions_off; /* S2LC_RED_* bits to disable */
+  const int32_t* devices;  /* s2lc_check_batch over several GPUs: HIP ordinals (an ordinal may
+                              repeat: two shards on one GPU); NULL / n_devices 0 = {device}.
+                              Histories are placed longest-processing-time first by
+                              n_ops x chains; verdicts are gathered in input order. */
+  uint32_t n_devices;      /* at most 16 */
+  uint32_t _pad2;
 } s2lc_opts;
 
 /* Result of one history check. */
@@ -139,7 +177,10 @@ typedef struct s2lc_result {
 #define S2LC_R_SEARCH_EXHAUSTED 2 /* no configuration survived */
 #define S2LC_R_BUDGET 3          /* max_configs exceeded (Unknown) */
 #define S2LC_R_FRONTIER 4        /* frontier exceeded device capacity (Unknown) */
-#define S2LC_R_WITNESS_INVALID 5 /* Ok, but the witness failed CPU replay (a bug; never expected) */
+#define S2LC_R_WITNESS_INVALID 5 /* the search found a linearization whose witness failed CPU
+                                    replay (a checker bug; never expected): verdict Unknown and
+                                    the call returns S2LC_EWITNESS */
+#define S2LC_R_TIMEOUT 6         /* s2lc_opts.timeout_us expired before the verdict (Unknown) */
 
 /* ----- context ----------------------------------------------------------- */
 s2lc_ctx* s2lc_create(const s2lc_opts* opts, int* status);
@@ -188,6 +229,10 @@ void s2lc_result_free(s2lc_result* r); /* frees r->witness; r itself is caller s
 
 /* Device-resident batches: upload once, check many times (bench / DST loops). */
 int s2lc_batch_create(s2lc_ctx* ctx, const s2lc_history* const* hs, size_t n, s2lc_batch** out);
+/* Replace the batch's histories with hs[0..n) on the same device buffers
+ * (grown only when hs needs more): a DST loop streams history batches
+ * through one device batch without reallocating. */
+int s2lc_batch_load(s2lc_ctx* ctx, s2lc_batch* b, const s2lc_history* const* hs, size_t n);
 /* s2lc_batch_run + s2lc_batch_results(..., with_witness = 1). */
 int s2lc_batch_check(s2lc_ctx* ctx, s2lc_batch* b, s2lc_result* out /* [n] */);
 /* Device work only: search every history, copy verdicts back. */
@@ -222,6 +267,10 @@ typedef struct s2lc_batch_stats {
   uint32_t _pad1;
 } s2lc_batch_stats;
 int s2lc_batch_stats_get(const s2lc_batch* b, s2lc_batch_stats* out);
+/* With S2LC_F_ROUND_COUNTS: the unique-configuration count of each completed
+ * round of history i's last search, rounds 0 .. *n-1 (round 0 = the closed
+ * initial configuration). With out == NULL only *n is set. */
+int s2lc_batch_round_counts(const s2lc_batch* b, size_t i, uint32_t* out, size_t cap, size_t* n);
 
 /* ----- model (s2Model, main.go:253-340) ------------------------------------ */
 /* Step op op_index (dense id, first-appearance order) of history h from
@@ -229,6 +278,11 @@ int s2lc_batch_stats_get(const s2lc_batch* b, s2lc_batch_stats* out);
 int s2lc_step_cpu(const s2lc_history* h, const s2lc_state* s, uint32_t op_index, s2lc_state out[2]);
 uint64_t s2lc_chain_hash(uint64_t stream_hash, uint64_t record_hash);
 uint64_t s2lc_fold_record_hashes(uint64_t stream_hash, const uint64_t* record_hashes, size_t n);
+/* foldRecordHashes on the GPU, through the same device routine the search
+ * kernels use: out[i] = fold(seeds[i], pool[offs[i] .. offs[i] + cnts[i])).
+ * Host buffers in and out (known-answer tests of the device hash). */
+int s2lc_device_fold(s2lc_ctx* ctx, const uint64_t* seeds, const uint64_t* pool, size_t pool_len,
+                     const uint32_t* offs, const uint32_t* cnts, size_t n, uint64_t* out);
 /* Replay a linearization (op indices) through the CPU model; 0 if every op
  * is accepted in order and every op appears exactly once, else -1. */
 int s2lc_replay(const s2lc_history* h, const uint32_t* order, size_t n);

@@ -78,7 +78,12 @@ int or_check_brute(const or_event* ev, size_t n, or_stats* st);
  * NOT a restatement of the reference; a cross-check where WGL cannot finish.
  * st->cache_inserts = configurations, st->backtracks = rounds,
  * st->max_state_set = widest frontier. */
-int or_check_reduced(const or_event* ev, size_t n, uint64_t max_configs, or_stats* st);
+/* reductions_off: bits of the product's S2LC_RED_* (1 P1 tail bound, 2 P2 hash
+ * at equal tail, 4 P4 nothing constrains, 8 indefinite identity deferral).
+ * rc_out (nullable, rc_cap entries): unique configurations of rounds 0, 1, ...
+ * (st->backtracks = the number of completed rounds). */
+int or_check_reduced(const or_event* ev, size_t n, uint64_t max_configs, uint32_t reductions_off,
+                     uint32_t* rc_out, size_t rc_cap, or_stats* st);
 
 #ifdef __cplusplus
 }

@@ -70,7 +70,8 @@ def lib():
         L.or_check_wgl.argtypes = [ctypes.c_void_p, ctypes.c_size_t, ctypes.c_int, ctypes.c_double,
                                    ctypes.c_uint64, ctypes.POINTER(_Stats)]
         L.or_check_reduced.restype = ctypes.c_int
-        L.or_check_reduced.argtypes = [ctypes.c_void_p, ctypes.c_size_t, ctypes.c_uint64, ctypes.POINTER(_Stats)]
+        L.or_check_reduced.argtypes = [ctypes.c_void_p, ctypes.c_size_t, ctypes.c_uint64, ctypes.c_uint32,
+                                       ctypes.c_void_p, ctypes.c_size_t, ctypes.POINTER(_Stats)]
         L.or_check_brute.restype = ctypes.c_int
         L.or_check_brute.argtypes = [ctypes.c_void_p, ctypes.c_size_t, ctypes.POINTER(_Stats)]
         _lib = L
@@ -165,13 +166,22 @@ def check_brute(events):
     return _NAMES[r], {"steps": st.steps}
 
 
-def check_reduced(events, max_configs=0):
-    """CPU implementation of the GPU's reduced search (cross-check, not the reference)."""
+def check_reduced(events, max_configs=0, reductions_off=0, round_counts=False):
+    """CPU implementation of the GPU's reduced search (cross-check, not the reference).
+
+    reductions_off: the product's RED_* bits; round_counts: also return the
+    unique configurations of each completed round (stats["round_counts"])."""
     ea = _as_array(events)
     st = _Stats()
-    r = lib().or_check_reduced(ea.ptr, len(ea), int(max_configs), ctypes.byref(st))
-    return _NAMES[r], {"configs": st.cache_inserts, "rounds": st.backtracks, "max_frontier": st.max_state_set,
-                       "children": st.steps, "seconds": st.seconds}
+    cap = len(ea) + 2 if round_counts else 0
+    rc = np.zeros(max(cap, 1), dtype=np.uint32)
+    r = lib().or_check_reduced(ea.ptr, len(ea), int(max_configs), int(reductions_off),
+                               rc.ctypes.data if round_counts else None, cap, ctypes.byref(st))
+    out = {"configs": st.cache_inserts, "rounds": st.backtracks, "max_frontier": st.max_state_set,
+           "children": st.steps, "seconds": st.seconds}
+    if round_counts:
+        out["round_counts"] = rc[:st.backtracks].tolist()
+    return _NAMES[r], out
 
 
 # ------------------------------------------------------------------ loader --

@@ -2,7 +2,9 @@
  * reduced.c — TEST INFRASTRUCTURE ONLY. An independent, single-threaded CPU
  * implementation of the *reduced* configuration search that the GPU runs
  * (DESIGN.md §3): rounds of one non-identity op, E-closure, I-identity
- * deferral, P1 tail bound, P4 completion. It is NOT a restatement of the
+ * deferral, P1 tail bound, P2 hash at equal tail, P4 completion, each of
+ * which can be switched off (ablation parity with the GPU engines, which take
+ * the same switches: include/s2lincheck.h S2LC_RED_*). It is NOT a restatement of the
  * reference; the reductions themselves are validated against the WGL
  * restatement (oracle.c, = porcupine checkSingle) and brute force on
  * histories where those finish. This file exists to cross-check the GPU on
@@ -67,7 +69,10 @@ typedef struct rctx {
   int* chain;      /* op indices, chain-major */
   int* cstart;     /* K+1 */
   uint64_t* sufmin;/* per chain position (len+1 per chain incl. sentinel) */
-  int nowrap;
+  int nowrap;      /* P1 on (tails never wrap) */
+  int p2;          /* P2 on (nowrap, no 0-record append with hashes) */
+  int p4;          /* P4 on */
+  int idefer;      /* indefinite identity deferral on */
 } rctx;
 
 static int head(const rctx* c, const uint16_t* cnt, int q) {
@@ -100,7 +105,16 @@ static int r_close(const rctx* c, uint16_t* cnt, const rst* s) {
     if (mr == (size_t)-1) return 2;
     uint64_t b = bound_of(c, cnt);
     if (c->nowrap && s->tail > b) return 1;
-    if (b == ~0ull) return 2;
+    if (c->p4 && b == ~0ull) return 2;
+    if (c->p2) { /* a minimal successful hash-checking read at this very tail with another hash never passes */
+      for (int q = 0; q < c->K; q++) {
+        int h = head(c, cnt, q);
+        if (h < 0) continue;
+        const rop* o = &c->ops[h];
+        if (o->cls != 0 || o->call >= mr || o->in->input_type == 0) continue;
+        if (!o->out->failure && o->out->has_hash && o->out->tail == s->tail && o->out->stream_hash != s->hash) return 1;
+      }
+    }
     int changed = 0;
     for (int q = 0; q < c->K; q++) {
       for (;;) {
@@ -126,7 +140,8 @@ static uint64_t mixr(uint64_t x) {
   return x;
 }
 
-int or_check_reduced(const or_event* ev, size_t n_ev, uint64_t max_configs, or_stats* st) {
+int or_check_reduced(const or_event* ev, size_t n_ev, uint64_t max_configs, uint32_t red_off, uint32_t* rc_out,
+                     size_t rc_cap, or_stats* st) {
   or_stats local;
   memset(&local, 0, sizeof local);
   struct timespec t0, t1;
@@ -158,7 +173,7 @@ int or_check_reduced(const or_event* ev, size_t n_ev, uint64_t max_configs, or_s
     }
   free(ncall); free(nret); free(ids); free(mslot);
   uint64_t total = 0;
-  int nowrap = 1;
+  int nowrap = 1, zero_with_hashes = 0;
   for (int k = 0; k < n; k++) {
     rop* o = &ops[k];
     const or_event* in = o->in;
@@ -166,6 +181,7 @@ int or_check_reduced(const or_event* ev, size_t n_ev, uint64_t max_configs, or_s
     if (in->input_type == 0) {
       if (!in->has_num_records) { free(ops); return OR_PANIC; }
       if (in->num_records > (1ull << 63) - total) nowrap = 0; else total += in->num_records;
+      if (in->num_records == 0 && in->n_hashes > 0) zero_with_hashes = 1;
       o->cls = (ou->failure && ou->definite) ? 0 : (ou->failure ? 2 : 1);
       o->constrain = !ou->failure;
       o->req = ou->tail >= in->num_records ? ou->tail - in->num_records : 0;
@@ -180,7 +196,11 @@ int or_check_reduced(const or_event* ev, size_t n_ev, uint64_t max_configs, or_s
   /* chains: ops are in call order already (first appearance = call) */
   rctx c;
   memset(&c, 0, sizeof c);
-  c.ops = ops; c.n = n; c.nowrap = nowrap;
+  c.ops = ops; c.n = n;
+  c.nowrap = nowrap && !(red_off & 1u);
+  c.p2 = nowrap && !zero_with_hashes && !(red_off & 2u);
+  c.p4 = !(red_off & 4u);
+  c.idefer = !(red_off & 8u);
   int* chain_of = (int*)malloc(sizeof(int) * (size_t)(n + 1));
   size_t* last_ret = (size_t*)malloc(sizeof(size_t) * (size_t)(n + 1));
   int K = 0;
@@ -219,7 +239,8 @@ int or_check_reduced(const or_event* ev, size_t n_ev, uint64_t max_configs, or_s
   rst s0 = {0, 0, 0};
   int r0 = r_close(&c, fcnt, &s0);
   if (r0 == 2) result = OR_OK;
-  else if (r0 == 0) { fst[0] = s0; nf = 1; }
+  else if (r0 == 0) { fst[0] = s0; nf = 1; if (rc_out && rc_cap > 0) rc_out[0] = 1; }
+  size_t round = 0;
   uint16_t* tmp = (uint16_t*)malloc(sizeof(uint16_t) * cw);
   while (result != OR_OK && nf > 0) {
     size_t ncap = 1024, nn = 0;
@@ -242,7 +263,7 @@ int or_check_reduced(const or_event* ev, size_t n_ev, uint64_t max_configs, or_s
         int nk = r_step(o, ps, kids);
         for (int k = 0; k < nk; k++) {
           /* I-op identity child only when the op holds minret */
-          if (o->cls == 2 && rs_eq(&kids[k], ps) && o->ret != mr) {
+          if (c.idefer && o->cls == 2 && rs_eq(&kids[k], ps) && o->ret != mr) {
             /* unless it is also the opt outcome (opt == s) */
             rst opt;
             opt.tail = ps->tail + o->in->num_records;
@@ -297,6 +318,8 @@ int or_check_reduced(const or_event* ev, size_t n_ev, uint64_t max_configs, or_s
     free(set.fp); free(set.idx);
     free(fcnt); free(fst);
     fcnt = ncnt; fst = nst; nf = nn;
+    round++;
+    if (result != OR_OK && rc_out && round < rc_cap) rc_out[round] = (uint32_t)nn;
     local.cache_inserts += nn;
     local.backtracks++; /* rounds */
     if (nn > local.max_state_set) local.max_state_set = nn;

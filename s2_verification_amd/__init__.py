@@ -35,8 +35,15 @@ CallEvent, ReturnEvent = 0, 1
 Ok, Illegal, Unknown = "Ok", "Illegal", "Unknown"
 _VERDICT = {S2LC_OK: Ok, S2LC_ILLEGAL: Illegal, S2LC_UNKNOWN: Unknown}
 STATUS = {0: "SUCCESS", -1: "EINVAL", -2: "EDECODE", -3: "EIO", -4: "ENODEV", -5: "EHIP",
-          -6: "EUNSUPPORTED", -7: "ENOMEM"}
-REASONS = {0: "none", 1: "unmatched", 2: "search_exhausted", 3: "budget", 4: "frontier", 5: "witness_invalid"}
+          -6: "EUNSUPPORTED", -7: "ENOMEM", -8: "EWITNESS"}
+EWITNESS = -8
+REASONS = {0: "none", 1: "unmatched", 2: "search_exhausted", 3: "budget", 4: "frontier", 5: "witness_invalid",
+           6: "timeout"}
+# s2lc_engine: force a search engine (tests / diagnostics)
+ENGINE_AUTO, ENGINE_WORKGROUP, ENGINE_WORKGROUP_HBM, ENGINE_LEVEL = 0, 1, 2, 3
+# S2LC_RED_*: verdict-exact search reductions that can be disabled (ablation tests)
+RED_P1, RED_P2, RED_P4, RED_IDEFER = 0x1, 0x2, 0x4, 0x8
+F_NO_WITNESS, F_ROUND_COUNTS = 0x1, 0x2
 WF_REGULAR, WF_MATCH_SEQ_NUM, WF_FENCING = 0, 1, 2
 VIOL_NONE, VIOL_READ_HASH, VIOL_DEFINITE_APPLIED, VIOL_TAIL, VIOL_STALE_MSN = 0, 1, 2, 3, 4
 
@@ -68,7 +75,10 @@ class c_state(ctypes.Structure):
 
 class c_opts(ctypes.Structure):
     _fields_ = [("struct_size", ctypes.c_uint32), ("device", ctypes.c_int32), ("flags", ctypes.c_uint32),
-                ("_pad", ctypes.c_uint32), ("max_configs", ctypes.c_uint64), ("stream", ctypes.c_void_p)]
+                ("_pad", ctypes.c_uint32), ("max_configs", ctypes.c_uint64), ("stream", ctypes.c_void_p),
+                ("timeout_us", ctypes.c_uint64), ("engine", ctypes.c_uint32), ("reductions_off", ctypes.c_uint32),
+                ("devices", ctypes.POINTER(ctypes.c_int32)), ("n_devices", ctypes.c_uint32),
+                ("_pad2", ctypes.c_uint32)]
 
 
 class c_result(ctypes.Structure):
@@ -147,10 +157,17 @@ SIGNATURES = [
     ("s2lc_result_free", None, [ctypes.POINTER(c_result)]),
     ("s2lc_batch_create", ctypes.c_int, [_P, ctypes.POINTER(_P), ctypes.c_size_t, ctypes.POINTER(_P)]),
     ("s2lc_batch_check", ctypes.c_int, [_P, _P, ctypes.POINTER(c_result)]),
+    ("s2lc_batch_load", ctypes.c_int, [_P, _P, ctypes.POINTER(_P), ctypes.c_size_t]),
     ("s2lc_batch_run", ctypes.c_int, [_P, _P]),
     ("s2lc_batch_results", ctypes.c_int, [_P, _P, ctypes.POINTER(c_result), ctypes.c_int]),
     ("s2lc_batch_free", None, [_P]),
     ("s2lc_batch_stats_get", ctypes.c_int, [_P, ctypes.POINTER(c_batch_stats)]),
+    ("s2lc_batch_round_counts", ctypes.c_int, [_P, ctypes.c_size_t, ctypes.POINTER(ctypes.c_uint32), ctypes.c_size_t,
+                                               ctypes.POINTER(ctypes.c_size_t)]),
+    ("s2lc_device_fold", ctypes.c_int, [_P, ctypes.POINTER(ctypes.c_uint64), ctypes.POINTER(ctypes.c_uint64),
+                                        ctypes.c_size_t, ctypes.POINTER(ctypes.c_uint32),
+                                        ctypes.POINTER(ctypes.c_uint32), ctypes.c_size_t,
+                                        ctypes.POINTER(ctypes.c_uint64)]),
     ("s2lc_step_cpu", ctypes.c_int, [_P, ctypes.POINTER(c_state), ctypes.c_uint32, ctypes.POINTER(c_state)]),
     ("s2lc_chain_hash", ctypes.c_uint64, [ctypes.c_uint64, ctypes.c_uint64]),
     ("s2lc_fold_record_hashes", ctypes.c_uint64, [ctypes.c_uint64, ctypes.POINTER(ctypes.c_uint64), ctypes.c_size_t]),
@@ -404,11 +421,19 @@ class CheckResult:
     partial: Optional[List[int]] = None  # Illegal: deepest certified linearized prefix (Event.Ids)
 
 
-def _convert(r: c_result) -> CheckResult:
-    w = [r.witness[k] for k in range(r.witness_len)] if r.witness else None
-    pa = [r.partial[k] for k in range(r.partial_len)] if r.partial else None
+def _ids(ptr, n, as_numpy):
+    if not ptr:
+        return None
+    a = np.ctypeslib.as_array(ptr, shape=(n,)).copy() if n else np.zeros(0, dtype=np.int64)
+    return a if as_numpy else a.tolist()
+
+
+def _convert(r: c_result, as_numpy: bool = False) -> CheckResult:
+    """c_result -> CheckResult; witness / partial as lists of Event.Ids (numpy
+    int64 arrays with as_numpy, a memcpy instead of one Python int per op)."""
     return CheckResult(_VERDICT[r.verdict], REASONS.get(r.reason, str(r.reason)), r.configs_explored,
-                       r.rounds, r.n_ops, w, r.device_ms, pa)
+                       r.rounds, r.n_ops, _ids(r.witness, r.witness_len, as_numpy), r.device_ms,
+                       _ids(r.partial, r.partial_len, as_numpy))
 
 
 class Batch:
@@ -429,21 +454,43 @@ class Batch:
         if b and _lib is not None:
             _lib.s2lc_batch_free(b)
 
+    def load(self, histories: Sequence[History]):
+        """s2lc_batch_load: replace the histories, reusing the device buffers."""
+        hs = list(histories)
+        arr = (ctypes.c_void_p * max(1, len(hs)))(*[h._h for h in hs])
+        rc = lib().s2lc_batch_load(self.checker._ctx, self._b, arr, len(hs))
+        if rc:
+            raise S2LCError(rc, self.checker.last_error())
+        self.histories = hs
+
     def run(self):
         rc = lib().s2lc_batch_run(self.checker._ctx, self._b)
         if rc:
             raise S2LCError(rc, self.checker.last_error())
 
-    def results(self, with_witness=True) -> List[CheckResult]:
+    def results(self, with_witness=True, as_numpy=False) -> List[CheckResult]:
         n = len(self.histories)
         res = (c_result * max(n, 1))()
         rc = lib().s2lc_batch_results(self.checker._ctx, self._b, res, int(with_witness))
-        if rc:
-            raise S2LCError(rc, self.checker.last_error())
-        out = [_convert(res[i]) for i in range(n)]
+        out = [_convert(res[i], as_numpy) for i in range(n)] if rc in (0, EWITNESS) else None
         for i in range(n):
             lib().s2lc_result_free(ctypes.byref(res[i]))
+        if rc:
+            raise S2LCError(rc, self.checker.last_error())
         return out
+
+    def round_counts(self, i: int) -> List[int]:
+        """Unique configurations of each completed round of history i's last
+        search (the checker needs round_counts=True)."""
+        n = ctypes.c_size_t(0)
+        rc = lib().s2lc_batch_round_counts(self._b, i, None, 0, ctypes.byref(n))
+        if rc:
+            raise S2LCError(rc, "round counts (Checker(round_counts=True) and a run first)")
+        buf = (ctypes.c_uint32 * max(1, n.value))()
+        rc = lib().s2lc_batch_round_counts(self._b, i, buf, n.value, ctypes.byref(n))
+        if rc:
+            raise S2LCError(rc, "round counts")
+        return list(buf[:n.value])
 
     def check(self, with_witness=True) -> List[CheckResult]:
         self.run()
@@ -456,15 +503,29 @@ class Batch:
 
 
 class Checker:
-    """An s2lc_ctx bound to one HIP device (and optionally an existing stream)."""
+    """An s2lc_ctx bound to one HIP device (and optionally an existing stream).
 
-    def __init__(self, device: int = -1, witness: bool = True, max_configs: int = 0, stream: int = 0):
+    timeout: seconds, porcupine's CheckEventsVerbose timeout (0 = none).
+    engine: ENGINE_* to force a search engine; reductions_off: RED_* bits;
+    round_counts: record per-round configuration counts (Batch.round_counts);
+    devices: HIP ordinals for check_batch sharding (LPT placement)."""
+
+    def __init__(self, device: int = -1, witness: bool = True, max_configs: int = 0, stream: int = 0,
+                 timeout: float = 0, engine: int = ENGINE_AUTO, reductions_off: int = 0,
+                 round_counts: bool = False, devices: Optional[Sequence[int]] = None):
         o = c_opts()
         o.struct_size = ctypes.sizeof(c_opts)
         o.device = device
-        o.flags = 0 if witness else 1
+        o.flags = (0 if witness else F_NO_WITNESS) | (F_ROUND_COUNTS if round_counts else 0)
         o.max_configs = max_configs
         o.stream = stream or None
+        o.timeout_us = int(round(timeout * 1e6)) if timeout else 0
+        o.engine = engine
+        o.reductions_off = reductions_off
+        if devices:
+            self._devs = (ctypes.c_int32 * len(devices))(*devices)
+            o.devices = self._devs
+            o.n_devices = len(devices)
         st = ctypes.c_int(0)
         ctx = lib().s2lc_create(ctypes.byref(o), ctypes.byref(st))
         if not ctx:
@@ -480,13 +541,47 @@ class Checker:
         return lib().s2lc_last_error(self._ctx).decode(errors="replace")
 
     def check(self, h: History) -> CheckResult:
+        """s2lc_check: one history through the context's reusable scratch batch."""
         r = c_result()
         rc = lib().s2lc_check(self._ctx, h._h, ctypes.byref(r))
+        out = _convert(r) if rc in (0, EWITNESS) else None
+        lib().s2lc_result_free(ctypes.byref(r))
         if rc:
             raise S2LCError(rc, self.last_error())
-        out = _convert(r)
-        lib().s2lc_result_free(ctypes.byref(r))
         return out
+
+    def check_many(self, hs: Sequence[History], as_numpy: bool = False) -> List[CheckResult]:
+        """s2lc_check_batch: the context's scratch (no allocation once warm),
+        sharded over the context's devices when it has several."""
+        n = len(hs)
+        arr = (ctypes.c_void_p * max(1, n))(*[h._h for h in hs])
+        res = (c_result * max(1, n))()
+        rc = lib().s2lc_check_batch(self._ctx, arr, n, res)
+        out = [_convert(res[i], as_numpy) for i in range(n)] if rc in (0, EWITNESS) else None
+        for i in range(n):
+            lib().s2lc_result_free(ctypes.byref(res[i]))
+        if rc:
+            raise S2LCError(rc, self.last_error())
+        return out
+
+    def device_fold(self, seeds, folds):
+        """foldRecordHashes on the GPU (the search kernels' device routine):
+        [fold(seeds[i], folds[i]) for i]."""
+        n = len(seeds)
+        pool = [x for f in folds for x in f]
+        offs, o = [], 0
+        for f in folds:
+            offs.append(o)
+            o += len(f)
+        sd = (ctypes.c_uint64 * max(1, n))(*seeds)
+        pl = (ctypes.c_uint64 * max(1, len(pool)))(*pool)
+        of = (ctypes.c_uint32 * max(1, n))(*offs)
+        ct = (ctypes.c_uint32 * max(1, n))(*[len(f) for f in folds])
+        out = (ctypes.c_uint64 * max(1, n))()
+        rc = lib().s2lc_device_fold(self._ctx, sd, pl, len(pool), of, ct, n, out)
+        if rc:
+            raise S2LCError(rc, self.last_error())
+        return list(out[:n])
 
     def check_batch(self, hs: Sequence[History]) -> List[CheckResult]:
         return Batch(self, hs).check()
@@ -495,21 +590,22 @@ class Checker:
         return Batch(self, hs)
 
 
-_default_checker = None
+_checkers = {}
 
 
 def check_events_verbose(model, events, timeout: float = 0):
     """porcupine.CheckEventsVerbose(s2Model.ToModel(), events, timeout) on the GPU.
 
     `model` is accepted for signature parity and ignored (the S2 model is built in).
-    Returns (verdict, info) with verdict in {Ok, Illegal, Unknown}; info carries the
+    timeout is in seconds (Go's time.Duration; 0 = none, as at main.go:606):
+    past it the verdict is Unknown. Returns (verdict, info); info carries the
     witness linearization (op ids) for Ok, configs explored and rounds.
     """
-    global _default_checker
-    if _default_checker is None:
-        _default_checker = Checker()
+    key = float(timeout or 0)
+    if key not in _checkers:
+        _checkers[key] = Checker(timeout=key)
     h = events if isinstance(events, History) else History.from_events(events)
-    r = _default_checker.check(h)
+    r = _checkers[key].check(h)
     return r.verdict, r
 
 

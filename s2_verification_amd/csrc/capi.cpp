@@ -5,10 +5,14 @@
 #include <stdlib.h>
 #include <string.h>
 
+#include <algorithm>
+#include <memory>
 #include <new>
+#include <stddef.h>
 #include <atomic>
 #include <string>
 #include <thread>
+#include <stdexcept>
 #include <vector>
 
 #include "history.h"
@@ -22,13 +26,40 @@ int simulate(const s2lc_sim_params& p, History* h, std::string* jsonl);
 using namespace s2lc;
 
 
+// One device shard of a context: its stream and a scratch batch reused by
+// every s2lc_check / s2lc_check_batch (no device allocation per call once the
+// scratch has grown to the working set).
+struct Shard {
+  int device = 0;
+  hipStream_t stream = nullptr;
+  bool own_stream = false;
+  DevBatch scratch;
+  RunStats stats;
+  std::string err;
+};
+
 struct s2lc_ctx {
   int device = 0;
   hipStream_t stream = nullptr;
   bool own_stream = false;
   uint32_t flags = 0;
   uint64_t max_configs = 0;
+  uint64_t timeout_us = 0;
+  uint32_t engine = S2LC_ENGINE_AUTO;
+  uint32_t red_off = 0;
+  std::vector<int> devices;                    // s2lc_check_batch shards (>= 1 entries)
+  std::vector<std::unique_ptr<Shard>> shards;  // created lazily, one per devices entry
   std::string err;
+
+  RunOpts run_opts() const {
+    RunOpts r;
+    r.max_configs = max_configs;
+    r.witness = !(flags & S2LC_F_NO_WITNESS);
+    r.round_counts = (flags & S2LC_F_ROUND_COUNTS) != 0;
+    r.engine = engine;
+    r.timeout_us = timeout_us;
+    return r;
+  }
 };
 
 struct s2lc_batch {
@@ -48,10 +79,9 @@ static void set_err(char* err, size_t errlen, const std::string& msg) {
 
 extern "C" {
 
-const char* s2lc_version(void) { return "s2lincheck 0.1.0 (gfx950)"; }
+const char* s2lc_version(void) { return "s2lincheck 0.2.0 (gfx950, ABI 2)"; }
 
 s2lc_ctx* s2lc_create(const s2lc_opts* opts, int* status) {
-  int st = 0;
   s2lc_ctx* c = nullptr;
   try {
     int n = 0;
@@ -61,18 +91,34 @@ s2lc_ctx* s2lc_create(const s2lc_opts* opts, int* status) {
     }
     c = new s2lc_ctx();
     int dev = -1;
-    if (opts && opts->struct_size >= sizeof(uint32_t) * 2) dev = opts->device;
+    if (opts && opts->struct_size >= offsetof(s2lc_opts, flags)) dev = opts->device;
     if (dev < 0) {
       if (hipGetDevice(&dev) != hipSuccess) dev = 0;
     }
     if (dev >= n) { delete c; if (status) *status = S2LC_ENODEV; return nullptr; }
     if (hipSetDevice(dev) != hipSuccess) { delete c; if (status) *status = S2LC_EHIP; return nullptr; }
     c->device = dev;
-    if (opts && opts->struct_size >= sizeof(s2lc_opts)) {
+    // ABI 1 callers pass the layout up to `stream`; the ABI 2 fields keep their defaults
+    if (opts && opts->struct_size >= offsetof(s2lc_opts, timeout_us)) {
       c->flags = opts->flags;
       c->max_configs = opts->max_configs;
       c->stream = (hipStream_t)opts->stream;
     }
+    if (opts && opts->struct_size >= sizeof(s2lc_opts)) {
+      c->timeout_us = opts->timeout_us;
+      c->engine = opts->engine;
+      c->red_off = opts->reductions_off;
+      if (c->engine > S2LC_ENGINE_LEVEL) { delete c; if (status) *status = S2LC_EINVAL; return nullptr; }
+      if (opts->devices && opts->n_devices) {
+        if (opts->n_devices > 16) { delete c; if (status) *status = S2LC_EINVAL; return nullptr; }
+        for (uint32_t i = 0; i < opts->n_devices; ++i) {
+          const int d = opts->devices[i];
+          if (d < 0 || d >= n) { delete c; if (status) *status = S2LC_ENODEV; return nullptr; }
+          c->devices.push_back(d);
+        }
+      }
+    }
+    if (c->devices.empty()) c->devices.push_back(dev);
     if (!c->stream) {
       if (hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess) {
         delete c;
@@ -86,12 +132,19 @@ s2lc_ctx* s2lc_create(const s2lc_opts* opts, int* status) {
     if (status) *status = S2LC_ENOMEM;
     return nullptr;
   }
-  if (status) *status = st;
+  if (status) *status = 0;
   return c;
 }
 
 void s2lc_destroy(s2lc_ctx* c) {
   if (!c) return;
+  for (auto& sh : c->shards) {
+    if (!sh) continue;
+    (void)hipSetDevice(sh->device);
+    batch_release(sh->scratch);
+    if (sh->own_stream && sh->stream) (void)hipStreamDestroy(sh->stream);
+  }
+  (void)hipSetDevice(c->device);
   if (c->own_stream && c->stream) (void)hipStreamDestroy(c->stream);
   delete c;
 }
@@ -300,6 +353,126 @@ int s2lc_history_info_get(const s2lc_history* h, s2lc_history_info* out) {
 }
 
 // --------------------------------------------------------------- checker ---
+}  // extern "C"
+
+namespace {
+
+// Results of a run (+ witness rebuild and CPU-model certification) into
+// out[0 .. B.n_hist). Every Ok witness must replay through s2Model.Step
+// (main.go:264-335); one that does not is a checker bug: that history becomes
+// Unknown (S2LC_R_WITNESS_INVALID) and the call returns S2LC_EWITNESS.
+int collect_results(DevBatch& B, const RunStats& stats, bool witness_recorded, s2lc_result* out, int with_witness,
+                    std::string& err) {
+  const bool want_w = with_witness && witness_recorded;
+  if (want_w && B.n_hist) {
+    const int rc = batch_fetch_moves(B, err);
+    if (rc) return rc;
+  }
+  // test hook: corrupt every Ok witness before certification (the failure path
+  // of the certificate must be loud; tests/test_gpu.py)
+  const char* fault = getenv("S2LC_FAULT_WITNESS");
+  const bool corrupt = fault && fault[0] == '1';
+  std::atomic<uint32_t> next{0};
+  std::atomic<int> oom{0}, invalid{0};
+  auto work = [&]() {
+    std::vector<uint32_t> order, mv;
+    std::vector<uint8_t> ident;
+    for (;;) {
+      const uint32_t i = next.fetch_add(1);
+      if (i >= B.n_hist) return;
+      const HistResult& r = B.h_res[i];
+      s2lc_result& o = out[i];
+      memset(&o, 0, sizeof o);
+      o.verdict = (int32_t)r.verdict;
+      o.reason = (int32_t)r.reason;
+      o.configs_explored = r.configs;
+      o.rounds = r.rounds;
+      o.n_ops = B.src[i]->n_ops;
+      o.device_ms = stats.kernel_ms;
+      if (!want_w || r.has_witness != 1 || (r.verdict != V_OK && r.verdict != V_ILLEGAL)) continue;
+      const History& H = *B.src[i];
+      const uint32_t* moves = B.h_moves + r.witness_off;
+      try {
+        if (corrupt && r.verdict == V_OK) {
+          mv.assign(moves, moves + r.witness_len);
+          if (mv.empty()) mv.push_back(0xFFFFu); else mv[0] = 0xFFFFu;  // no such chain
+          moves = mv.data();
+        }
+        const uint32_t n_moves = corrupt && r.verdict == V_OK ? (uint32_t)mv.size() : r.witness_len;
+        if (r.verdict == V_OK) {
+          const bool ok = rebuild_linearization(H, moves, n_moves, r.p4 != 0, order, ident, false) &&
+                          replay_path(H, order.data(), ident.data(), order.size());
+          if (!ok) {
+            o.verdict = S2LC_UNKNOWN;
+            o.reason = S2LC_R_WITNESS_INVALID;
+            invalid = 1;
+            continue;
+          }
+          o.witness = (int64_t*)malloc(sizeof(int64_t) * (order.size() ? order.size() : 1));
+          if (!o.witness) { oom = 1; continue; }
+          for (size_t k = 0; k < order.size(); ++k) o.witness[k] = H.op_ids[order[k]];
+          o.witness_len = (uint32_t)order.size();
+        } else if (rebuild_linearization(H, moves, n_moves, false, order, ident, true) &&
+                   replay_prefix(H, order.data(), ident.data(), order.size())) {
+          o.partial = (int64_t*)malloc(sizeof(int64_t) * (order.size() ? order.size() : 1));
+          if (!o.partial) { oom = 1; continue; }
+          for (size_t k = 0; k < order.size(); ++k) o.partial[k] = H.op_ids[order[k]];
+          o.partial_len = (uint32_t)order.size();
+        }
+      } catch (...) {
+        oom = 1;
+      }
+    }
+  };
+  // Witness rebuild + certification is independent per history: worker
+  // threads (S2LC_THREADS, default min(16, cores)).
+  int n_threads = 1;
+  if (want_w) {
+    const char* e = getenv("S2LC_THREADS");
+    n_threads = e ? atoi(e) : (int)std::min(16u, std::max(1u, std::thread::hardware_concurrency()));
+    n_threads = std::max(1, std::min<int>(n_threads, (int)(B.n_hist / 64 + 1)));
+  }
+  std::vector<std::thread> ts;
+  for (int t = 1; t < n_threads; ++t) ts.emplace_back(work);
+  work();
+  for (auto& t : ts) t.join();
+  if (oom) { err = "out of memory"; return S2LC_ENOMEM; }
+  if (invalid) { err = "an Ok witness failed CPU-model certification (checker bug)"; return S2LC_EWITNESS; }
+  return 0;
+}
+
+Shard& shard_of(s2lc_ctx* c, size_t k) {
+  if (c->shards.size() < c->devices.size()) c->shards.resize(c->devices.size());
+  if (!c->shards[k]) {
+    auto sh = std::make_unique<Shard>();
+    sh->device = c->devices[k];
+    sh->scratch.device = sh->device;
+    if (k == 0 && sh->device == c->device) {
+      sh->stream = c->stream;  // the context's (or caller's) stream
+    } else {
+      if (hipSetDevice(sh->device) != hipSuccess || hipStreamCreateWithFlags(&sh->stream, hipStreamNonBlocking) != hipSuccess)
+        throw std::runtime_error("stream");
+      sh->own_stream = true;
+    }
+    c->shards[k] = std::move(sh);
+  }
+  return *c->shards[k];
+}
+
+// upload + run + results of `hs` on one shard, into out[0 .. hs.size())
+int shard_check(s2lc_ctx* c, Shard& sh, const std::vector<const History*>& hs, s2lc_result* out) {
+  if (hipSetDevice(sh.device) != hipSuccess) { sh.err = "hipSetDevice failed"; return S2LC_EHIP; }
+  const RunOpts ro = c->run_opts();
+  int rc = batch_upload(sh.scratch, hs, c->red_off, sh.err);
+  if (!rc) rc = batch_run(sh.scratch, sh.stream, ro, sh.stats, sh.err);
+  if (!rc) rc = collect_results(sh.scratch, sh.stats, ro.witness, out, 1, sh.err);
+  return rc;
+}
+
+}  // namespace
+
+extern "C" {
+
 int s2lc_batch_create(s2lc_ctx* c, const s2lc_history* const* hs, size_t n, s2lc_batch** out) {
   if (!c || !out || (!hs && n)) return S2LC_EINVAL;
   *out = nullptr;
@@ -313,10 +486,30 @@ int s2lc_batch_create(s2lc_ctx* c, const s2lc_history* const* hs, size_t n, s2lc
       v[i] = &hs[i]->h;
     }
     std::string e;
-    int rc = batch_upload(b->b, v, e);
+    int rc = batch_upload(b->b, v, c->red_off, e);
     if (rc) { c->err = e; batch_release(b->b); delete b; return rc; }
     *out = b;
     return 0;
+  } catch (const std::bad_alloc&) {
+    c->err = "out of memory";
+    return S2LC_ENOMEM;
+  } catch (...) {
+    c->err = "internal error";
+    return S2LC_EINVAL;
+  }
+}
+
+int s2lc_batch_load(s2lc_ctx* c, s2lc_batch* b, const s2lc_history* const* hs, size_t n) {
+  if (!c || !b || (!hs && n)) return S2LC_EINVAL;
+  try {
+    if (hipSetDevice(b->b.device) != hipSuccess) { c->err = "hipSetDevice failed"; return S2LC_EHIP; }
+    std::vector<const History*> v(n);
+    for (size_t i = 0; i < n; ++i) {
+      if (!hs[i]) { c->err = "null history"; return S2LC_EINVAL; }
+      v[i] = &hs[i]->h;
+    }
+    b->ran = false;
+    return batch_upload(b->b, v, c->red_off, c->err);
   } catch (const std::bad_alloc&) {
     c->err = "out of memory";
     return S2LC_ENOMEM;
@@ -336,13 +529,13 @@ void s2lc_batch_free(s2lc_batch* b) {
 int s2lc_batch_run(s2lc_ctx* c, s2lc_batch* b) {
   if (!c || !b) return S2LC_EINVAL;
   try {
-    if (hipSetDevice(c->device) != hipSuccess) { c->err = "hipSetDevice failed"; return S2LC_EHIP; }
-    const bool witness = !(c->flags & S2LC_F_NO_WITNESS);
+    if (hipSetDevice(b->b.device) != hipSuccess) { c->err = "hipSetDevice failed"; return S2LC_EHIP; }
+    const RunOpts ro = c->run_opts();
     std::string e;
-    int rc = batch_run(b->b, c->stream, c->max_configs, witness, b->stats, e);
+    int rc = batch_run(b->b, c->stream, ro, b->stats, e);
     if (rc) { c->err = e; return rc; }
     b->ran = true;
-    b->witness = witness;
+    b->witness = ro.witness;
     return 0;
   } catch (...) {
     c->err = "internal error";
@@ -354,74 +547,8 @@ int s2lc_batch_results(s2lc_ctx* c, s2lc_batch* b, s2lc_result* out, int with_wi
   if (!c || !b || (!out && b->b.n_hist)) return S2LC_EINVAL;
   if (!b->ran) { c->err = "batch has not been run"; return S2LC_EINVAL; }
   try {
-    DevBatch& B = b->b;
-    const bool want_w = with_witness && b->witness;
-    if (want_w && B.n_hist) {
-      B.h_moves.resize(B.moves_cap);
-      if (hipMemcpy(B.h_moves.data(), B.moves, B.moves_cap * sizeof(uint32_t), hipMemcpyDeviceToHost) != hipSuccess) {
-        c->err = "copy witness moves";
-        return S2LC_EHIP;
-      }
-    }
-    // Witness rebuild + CPU-model certification is independent per history:
-    // spread over worker threads (S2LC_THREADS, default min(16, cores)).
-    std::atomic<uint32_t> next{0};
-    std::atomic<int> oom{0};
-    auto work = [&]() {
-      for (;;) {
-        const uint32_t i = next.fetch_add(1);
-        if (i >= B.n_hist) return;
-        const HistResult& r = B.h_res[i];
-        s2lc_result& o = out[i];
-        memset(&o, 0, sizeof o);
-        o.verdict = (int32_t)r.verdict;
-        o.reason = (int32_t)r.reason;
-        o.configs_explored = r.configs;
-        o.rounds = r.rounds;
-        o.n_ops = B.src[i]->n_ops;
-        o.device_ms = b->stats.kernel_ms;
-        if (!want_w || r.has_witness != 1 || (r.verdict != V_OK && r.verdict != V_ILLEGAL)) continue;
-        const History& H = *B.src[i];
-        std::vector<uint32_t> order;
-        std::vector<uint8_t> ident;
-        try {
-          if (r.verdict == V_OK) {
-            const bool ok = rebuild_linearization(H, B.h_moves.data() + r.witness_off, r.witness_len, r.p4 != 0, order,
-                                                  ident, false) &&
-                            replay_path(H, order.data(), ident.data(), order.size());
-            if (!ok) {
-              o.reason = S2LC_R_WITNESS_INVALID;
-              continue;
-            }
-            o.witness = (int64_t*)malloc(sizeof(int64_t) * (order.size() ? order.size() : 1));
-            if (!o.witness) { oom = 1; continue; }
-            for (size_t k = 0; k < order.size(); ++k) o.witness[k] = H.op_ids[order[k]];
-            o.witness_len = (uint32_t)order.size();
-          } else if (rebuild_linearization(H, B.h_moves.data() + r.witness_off, r.witness_len, false, order, ident,
-                                           true) &&
-                     replay_prefix(H, order.data(), ident.data(), order.size())) {
-            o.partial = (int64_t*)malloc(sizeof(int64_t) * (order.size() ? order.size() : 1));
-            if (!o.partial) { oom = 1; continue; }
-            for (size_t k = 0; k < order.size(); ++k) o.partial[k] = H.op_ids[order[k]];
-            o.partial_len = (uint32_t)order.size();
-          }
-        } catch (...) {
-          oom = 1;
-        }
-      }
-    };
-    int n_threads = 1;
-    if (want_w) {
-      const char* e = getenv("S2LC_THREADS");
-      n_threads = e ? atoi(e) : (int)std::min(16u, std::max(1u, std::thread::hardware_concurrency()));
-      n_threads = std::max(1, std::min<int>(n_threads, (int)(B.n_hist / 64 + 1)));
-    }
-    std::vector<std::thread> ts;
-    for (int t = 1; t < n_threads; ++t) ts.emplace_back(work);
-    work();
-    for (auto& t : ts) t.join();
-    if (oom) { c->err = "out of memory"; return S2LC_ENOMEM; }
-    return 0;
+    if (hipSetDevice(b->b.device) != hipSuccess) { c->err = "hipSetDevice failed"; return S2LC_EHIP; }
+    return collect_results(b->b, b->stats, b->witness, out, with_witness, c->err);
   } catch (const std::bad_alloc&) {
     c->err = "out of memory";
     return S2LC_ENOMEM;
@@ -459,19 +586,100 @@ int s2lc_batch_stats_get(const s2lc_batch* b, s2lc_batch_stats* out) {
   return 0;
 }
 
+int s2lc_batch_round_counts(const s2lc_batch* b, size_t i, uint32_t* out, size_t cap, size_t* n) {
+  if (!b || !n || i >= b->b.n_hist) return S2LC_EINVAL;
+  const DevBatch& B = b->b;
+  if (!b->ran || !B.rc_valid) return S2LC_EINVAL;
+  const size_t k = B.forced[i] ? 0 : B.h_res[i].rounds;
+  *n = k;
+  if (!out) return 0;
+  if (cap < k) return S2LC_EINVAL;
+  for (size_t r = 0; r < k; ++r) out[r] = B.h_rcounts[B.h_moves_off[i] + r];
+  return 0;
+}
+
+// porcupine.CheckEventsVerbose over many histories (main.go:606 per history).
+// One device: the context's scratch batch. Several (s2lc_opts.devices): the
+// histories are placed longest-processing-time first (n_ops x K) on the least
+// loaded shard, every shard checks its part on its own thread and device, and
+// the verdicts land in out[] in input order.
 int s2lc_check_batch(s2lc_ctx* c, const s2lc_history* const* hs, size_t n, s2lc_result* out) {
-  s2lc_batch* b = nullptr;
-  int rc = s2lc_batch_create(c, hs, n, &b);
-  if (rc) return rc;
-  rc = s2lc_batch_check(c, b, out);
-  s2lc_batch_free(b);
-  return rc;
+  if (!c || (!hs && n) || (!out && n)) return S2LC_EINVAL;
+  try {
+    std::vector<const History*> v(n);
+    for (size_t i = 0; i < n; ++i) {
+      if (!hs[i]) { c->err = "null history"; return S2LC_EINVAL; }
+      v[i] = &hs[i]->h;
+    }
+    const size_t S = c->devices.size();
+    if (S <= 1) {
+      Shard& sh = shard_of(c, 0);
+      const int rc = shard_check(c, sh, v, out);
+      if (rc) c->err = sh.err;
+      return rc;
+    }
+    // LPT placement
+    std::vector<size_t> idx(n);
+    for (size_t i = 0; i < n; ++i) idx[i] = i;
+    auto work = [&](size_t i) { return (uint64_t)v[i]->n_ops * std::max<uint32_t>(v[i]->K, 1); };
+    std::stable_sort(idx.begin(), idx.end(), [&](size_t a, size_t b) { return work(a) > work(b); });
+    std::vector<uint64_t> load(S, 0);
+    std::vector<std::vector<size_t>> part(S);
+    for (size_t i : idx) {
+      const size_t k = (size_t)(std::min_element(load.begin(), load.end()) - load.begin());
+      part[k].push_back(i);
+      load[k] += work(i);
+    }
+    for (size_t k = 0; k < S; ++k) (void)shard_of(c, k);
+    std::vector<std::vector<s2lc_result>> res(S);
+    std::vector<int> rcs(S, 0);
+    std::vector<std::thread> ts;
+    for (size_t k = 0; k < S; ++k) {
+      ts.emplace_back([&, k]() {
+        try {
+          std::vector<const History*> sub;
+          for (size_t i : part[k]) sub.push_back(v[i]);
+          res[k].resize(sub.size());
+          rcs[k] = sub.empty() ? 0 : shard_check(c, *c->shards[k], sub, res[k].data());
+        } catch (...) {
+          rcs[k] = S2LC_ENOMEM;
+          c->shards[k]->err = "out of memory";
+        }
+      });
+    }
+    for (auto& t : ts) t.join();
+    (void)hipSetDevice(c->device);
+    int rc = 0;
+    for (size_t k = 0; k < S; ++k)  // verdict gather, input order
+      for (size_t q = 0; q < part[k].size(); ++q) out[part[k][q]] = res[k][q];
+    for (size_t k = 0; k < S && !rc; ++k)
+      if (rcs[k] && rcs[k] != S2LC_EWITNESS) { rc = rcs[k]; c->err = c->shards[k]->err; }
+    for (size_t k = 0; k < S && !rc; ++k)
+      if (rcs[k]) { rc = rcs[k]; c->err = c->shards[k]->err; }
+    if (rc && rc != S2LC_EWITNESS) {
+      for (size_t i = 0; i < n; ++i) s2lc_result_free(&out[i]);
+    }
+    return rc;
+  } catch (const std::bad_alloc&) {
+    c->err = "out of memory";
+    return S2LC_ENOMEM;
+  } catch (...) {
+    c->err = "internal error";
+    return S2LC_EHIP;
+  }
 }
 
 int s2lc_check(s2lc_ctx* c, const s2lc_history* h, s2lc_result* out) {
   if (!h) return S2LC_EINVAL;
   const s2lc_history* one[1] = {h};
   return s2lc_check_batch(c, one, 1, out);
+}
+
+int s2lc_device_fold(s2lc_ctx* c, const uint64_t* seeds, const uint64_t* pool, size_t pool_len, const uint32_t* offs,
+                     const uint32_t* cnts, size_t n, uint64_t* out) {
+  if (!c || (n && (!seeds || !offs || !cnts || !out)) || (pool_len && !pool)) return S2LC_EINVAL;
+  if (hipSetDevice(c->device) != hipSuccess) { c->err = "hipSetDevice failed"; return S2LC_EHIP; }
+  return device_fold(seeds, pool, pool_len, offs, cnts, n, out, c->stream, c->err);
 }
 
 void s2lc_result_free(s2lc_result* r) {
@@ -546,7 +754,7 @@ int s2lc_dist_create(s2lc_ctx* c, const s2lc_history* h, int rank, int world, s2
     if (hipSetDevice(c->device) != hipSuccess) { c->err = "hipSetDevice"; return S2LC_EHIP; }
     auto* x = new s2lc_dist();
     x->ctx = c;
-    const int rc = dist_create(x->d, &h->h, (uint32_t)rank, (uint32_t)world, c->err);
+    const int rc = dist_create(x->d, &h->h, (uint32_t)rank, (uint32_t)world, c->red_off, c->err);
     if (rc) { dist_release(x->d); delete x; return rc; }
     *out = x;
     return 0;

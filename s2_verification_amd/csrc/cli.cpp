@@ -17,8 +17,10 @@
 
 #include "s2lincheck.h"
 
+// main.go:565-566: Version is injected at build time from golang/VERSION
+// (Makefile:5-9); here from s2_verification_amd/VERSION by the Makefile.
 #ifndef S2LC_CLI_VERSION
-#define S2LC_CLI_VERSION "v0.4.1-gfx950"
+#define S2LC_CLI_VERSION "dev"
 #endif
 
 static std::string now_rfc3339() {
@@ -103,6 +105,15 @@ int main(int argc, char** argv) {
   s2lc_result r;
   memset(&r, 0, sizeof r);
   rc = s2lc_check(ctx, h, &r);
+  if (rc == S2LC_EWITNESS) {
+    // the GPU found a linearization that failed CPU-model certification: a
+    // checker bug, never a verdict (exit 3, distinct from 0 / 1)
+    slog("ERROR", "failed: witness certification", ",\"err\":" + jstr(s2lc_last_error(ctx)));
+    s2lc_result_free(&r);
+    s2lc_destroy(ctx);
+    s2lc_history_free(h);
+    return 3;
+  }
   if (rc) {
     fprintf(stderr, "s2-porcupine: check failed: %s\n", s2lc_last_error(ctx));
     s2lc_destroy(ctx);
@@ -137,7 +148,13 @@ int main(int argc, char** argv) {
   if (ok) {
     slog("INFO", "passed: is linearizable");
   } else {
-    slog("ERROR", "failed: is NOT linearizable", std::string(",\"res\":\"") + (r.verdict == S2LC_ILLEGAL ? "Illegal" : "Unknown") + "\"");
+    // main.go:636: res is porcupine's CheckResult; Unknown (a device capacity
+    // limit; the reference at timeout 0 never returns it) also names its reason
+    std::string extra = std::string(",\"res\":\"") + (r.verdict == S2LC_ILLEGAL ? "Illegal" : "Unknown") + "\"";
+    if (r.verdict == S2LC_UNKNOWN)
+      extra += std::string(",\"reason\":\"") + (r.reason == S2LC_R_FRONTIER ? "frontier exceeds device capacity" :
+                                                r.reason == S2LC_R_TIMEOUT ? "timeout" : r.reason == S2LC_R_BUDGET ? "budget" : "other") + "\"";
+    slog("ERROR", "failed: is NOT linearizable", extra);
   }
   s2lc_result_free(&r);
   s2lc_destroy(ctx);

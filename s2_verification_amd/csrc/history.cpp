@@ -125,6 +125,7 @@ int History::finalize() {
     else total += in.num_records;
     if (in.num_records == 0 && in.hash_cnt > 0) zero_with_hashes = true;
   }
+  hflags |= H_P4 | H_IDEFER;
   if (nowrap) hflags |= H_NOWRAP;
   if (nowrap && !zero_with_hashes) hflags |= H_P2OK;
 

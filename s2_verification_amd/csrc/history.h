@@ -26,9 +26,14 @@ struct Event {
   uint64_t tail = 0, stream_hash = 0;
 };
 
+// Per-history search flags (HistDesc.flags). Each gates one verdict-exact
+// reduction; batch_upload clears the ones a context disables
+// (s2lc_opts.reductions_off) for ablation tests.
 enum : uint16_t {
-  H_NOWRAP = 0x1,  // sum of all num_records <= 2^63: tails never wrap, P1 prune valid
-  H_P2OK = 0x2,    // NOWRAP and no 0-record append carries hashes: equal tail => equal hash needed
+  H_NOWRAP = 0x1,  // P1: sum of all num_records <= 2^63: tails never wrap, tail-bound prune valid
+  H_P2OK = 0x2,    // P2: NOWRAP and no 0-record append carries hashes: equal tail => equal hash needed
+  H_P4 = 0x4,      // P4: no pending observer left => complete
+  H_IDEFER = 0x8,  // indefinite append's identity outcome only when it holds minret
 };
 
 struct History {

@@ -6,6 +6,7 @@
 // next round. A round whose children or staged configurations exceed the
 // device buffers is re-run over halves of its frontier.
 #include <hip/hip_runtime.h>
+#include <stdlib.h>
 #include <string.h>
 
 #include <algorithm>
@@ -79,6 +80,12 @@ int level_buffers(DevBatch& b, uint32_t kmax, std::string& err) {
   uint64_t ccap = std::min<uint64_t>(1ull << 26, (uint64_t)(budget * 3 / 10) / sizeof(LChild));
   scap = std::max<uint64_t>(scap, 1024);
   ccap = std::max<uint64_t>(ccap, 4096);
+  // S2LC_LEVEL_SCAP (tests): a small staging capacity, to reach the
+  // frontier-overflow paths with small histories
+  if (const char* e = getenv("S2LC_LEVEL_SCAP")) {
+    const uint64_t v = strtoull(e, nullptr, 10);
+    if (v >= 64) scap = std::min<uint64_t>(scap, v);
+  }
   uint64_t ht = 1024;
   while (ht < 2 * scap) ht <<= 1;
   if (lv_ensure((void**)&L.child, L.child_bytes, ccap * sizeof(LChild), err)) return S2LC_EHIP;
@@ -105,8 +112,11 @@ void level_release(DevBatch& b) {
   L = LevelBufs{};
 }
 
-int level_search(DevBatch& b, uint32_t h, hipStream_t st, uint64_t max_configs, bool witness, LevelStats& ls,
+int level_search(DevBatch& b, uint32_t h, hipStream_t st, const RunOpts& ro, int64_t deadline_ns, LevelStats& ls,
                  std::string& err) {
+  const uint64_t max_configs = ro.max_configs;
+  const bool witness = ro.witness;
+  uint32_t* const rc = ro.round_counts && !b.h_rcounts.empty() ? b.h_rcounts.data() + b.h_moves_off[h] : nullptr;
   const HistDesc& hd = b.h_hist[h];
   const uint32_t K = hd.K;
   const uint32_t kmax = level_kmax(K);
@@ -165,6 +175,7 @@ int level_search(DevBatch& b, uint32_t h, hipStream_t st, uint64_t max_configs, 
   for (;;) {
     if (hc->found) { verdict = V_OK; reason = 0; break; }
     const uint32_t nf = hc->nnext;
+    if (rc) rc[rounds] = nf;
     if (nf == 0) {
       verdict = V_ILLEGAL; reason = S2LC_R_SEARCH_EXHAUSTED;
       if (rounds > 0 && p.witness) {
@@ -181,6 +192,7 @@ int level_search(DevBatch& b, uint32_t h, hipStream_t st, uint64_t max_configs, 
     max_frontier = std::max(max_frontier, nf);
     if (p.witness) tnext += nf;
     if (max_configs && configs > max_configs) { verdict = V_UNKNOWN; reason = S2LC_R_BUDGET; break; }
+    if (deadline_ns && steady_ns() > deadline_ns) { verdict = V_UNKNOWN; reason = S2LC_R_TIMEOUT; break; }
     cur ^= 1;
     p.cur = L.stg[cur]; p.cur_idx = L.idx[cur];
     p.stg = L.stg[cur ^ 1]; p.nxt_idx = L.idx[cur ^ 1];
@@ -290,10 +302,11 @@ int level_search(DevBatch& b, uint32_t h, hipStream_t st, uint64_t max_configs, 
 // of a witness crosses ranks; the caller gathers the pools at the end.
 // ============================================================================
 
-int dist_create(DistLevel& d, const History* h, uint32_t rank, uint32_t world, std::string& err) {
+int dist_create(DistLevel& d, const History* h, uint32_t rank, uint32_t world, uint32_t reductions_off,
+                std::string& err) {
   if (world < 1 || world > 8 || rank >= world) { err = "world must be 1..8"; return S2LC_EINVAL; }
   std::vector<const History*> hs{h};
-  int rc = batch_upload(d.b, hs, err);
+  int rc = batch_upload(d.b, hs, reductions_off, err);
   if (rc) return rc;
   d.rank = rank;
   d.world = world;

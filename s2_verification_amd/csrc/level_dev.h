@@ -202,7 +202,7 @@ __global__ __launch_bounds__(LV_BLOCK) void lv_expand(LvParams p) {
         if (take_opt || (r.flags & OPF_CLS_I)) {
           if (g) opt.hash = fold_hashes_blk(s.hash, p.pool + r.hash_off, r.hash_cnt);
         }
-        if (r.flags & OPF_CLS_I) take_id = r.ret_ev == pmin && !(g && state_eq(opt, s));
+        if (r.flags & OPF_CLS_I) take_id = (!(p.hflags & H_IDEFER) || r.ret_ev == pmin) && !(g && state_eq(opt, s));
         nk = (uint32_t)take_opt + (uint32_t)take_id;
       }
     }
@@ -230,6 +230,7 @@ __global__ __launch_bounds__(LV_BLOCK) void lv_close(LvParams p) {
   const uint32_t K = p.K;
   const bool nowrap = p.hflags & H_NOWRAP;
   const bool p2 = p.hflags & H_P2OK;
+  const bool p4 = p.hflags & H_P4;
   uint32_t csj[NQ];
 #pragma unroll
   for (int q = 0; q < NQ; ++q) {
@@ -303,7 +304,7 @@ __global__ __launch_bounds__(LV_BLOCK) void lv_close(LvParams p) {
       }
       if (__ballot(dead) || (nowrap && s.tail > bound)) { res = CL_DEAD; break; }
       if (!__ballot(adv != 0)) {
-        res = minret == EV_INF ? CL_COMPLETE : (bound == REQ_NONE ? CL_P4 : CL_ALIVE);
+        res = minret == EV_INF ? CL_COMPLETE : ((p4 && bound == REQ_NONE) ? CL_P4 : CL_ALIVE);
         break;
       }
 #pragma unroll

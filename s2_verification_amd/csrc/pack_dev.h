@@ -166,6 +166,7 @@ __device__ __forceinline__ int pack_closure(ChainLane& ch, const uint64_t* __res
                                             uint64_t gmask, uint32_t& minret_out) {
   const bool nowrap = hflags & H_NOWRAP;
   const bool p2 = hflags & H_P2OK;
+  const bool p4 = hflags & H_P4;
   for (;;) {
     ch.at(cnt);
     const OpRec& r = ch.r;
@@ -188,7 +189,7 @@ __device__ __forceinline__ int pack_closure(ChainLane& ch, const uint64_t* __res
     if ((__ballot(dead) & gmask) || (nowrap && s.tail > bound)) return CL_DEAD;
     if (!(__ballot(legal) & gmask)) {
       if (minret == EV_INF) return CL_COMPLETE;
-      return bound == REQ_NONE ? CL_P4 : CL_ALIVE;
+      return (p4 && bound == REQ_NONE) ? CL_P4 : CL_ALIVE;
     }
     cnt += legal ? 1u : 0u;
   }
@@ -228,7 +229,14 @@ __global__ __launch_bounds__(PACK_BLOCK) void pack_kernel(Params p) {
     const uint32_t h = p.order[hi];
     const HistDesc hd = p.hist[h];
     const int K = hd.K;
+    if (K > L) {  // never listed by the host; re-run by a workgroup pass if it were
+      if (gl == 0) { p.res[h].verdict = V_UNKNOWN; p.res[h].reason = S2LC_R_FRONTIER; }
+      continue;
+    }
     const bool on = gl < K;
+    const bool idefer = hd.flags & H_IDEFER;
+    const uint64_t deadline = p.deadline ? *p.deadline : 0ull;
+    uint32_t* const rc = p.rcounts ? p.rcounts + p.res[h].witness_off : nullptr;
     const uint32_t cs = on ? p.chain_start[hd.cs_base + gl] : 0u;
     const uint32_t ce = on ? p.chain_start[hd.cs_base + gl + 1] : 0u;
     ChainLane ch;
@@ -262,12 +270,15 @@ __global__ __launch_bounds__(PACK_BLOCK) void pack_kernel(Params p) {
         if (gl < L) c.cnt[gl] = on ? (uint16_t)cnt : 0;
         nf = 1;
         configs = 1;
+        if (rc && gl == 0) rc[0] = 1;
       }
       wave_lds_sync();
     }
 
     // ---- rounds: each linearizes one durable / indefinite append ----------
     while (nf != 0 && nf != 0xFFFFFFFFu) {
+      // s_memrealtime is a scalar read: the same value in every lane of the wave
+      if (deadline && wall_clock64() > deadline) { verdict = V_UNKNOWN; reason = S2LC_R_TIMEOUT; break; }
       C* const curf = fr + cur * PACK_F;
       C* const nxt = fr + (1 - cur) * PACK_F;
       uint32_t nn = 0;
@@ -297,7 +308,7 @@ __global__ __launch_bounds__(PACK_BLOCK) void pack_kernel(Params p) {
           if (take_opt) {
             opt.hash = fold_hashes_blk(s.hash, p.pool + r.hash_off, r.hash_cnt);
           }
-          if (r.flags & OPF_CLS_I) take_id = r.ret_ev == pmin && !(g && state_eq(opt, s));
+          if (r.flags & OPF_CLS_I) take_id = (!idefer || r.ret_ev == pmin) && !(g && state_eq(opt, s));
         }
         PK_LAP(0);
         uint64_t mo = __ballot(take_opt) & gmask;
@@ -350,6 +361,7 @@ __global__ __launch_bounds__(PACK_BLOCK) void pack_kernel(Params p) {
       if (found) { verdict = V_OK; reason = 0; rounds++; break; }
       if (overflow) { verdict = V_UNKNOWN; reason = S2LC_R_FRONTIER; break; }
       rounds++;
+      if (rc && gl == 0) rc[rounds] = nn;
       if (nn == 0) {
         verdict = V_ILLEGAL; reason = S2LC_R_SEARCH_EXHAUSTED;
         deep_trace = curf[0].trace;  // a configuration of the deepest non-empty round

@@ -78,40 +78,61 @@ struct LevelStats {
   uint32_t max_frontier = 0, histories = 0, chunk_retries = 0;
 };
 
+// A batch of histories resident on one device. Every buffer is grown on
+// demand and reused by later uploads/runs (a context's scratch batch serves
+// s2lc_check with no device allocation once it is large enough):
+//   device arena : recs | pool | chain_start | hist | order | res | moves | rcounts | list
+//   pinned stage : recs | pool | chain_start | hist | order | res   (one H2D copy)
 struct DevBatch {
   int device = 0;
   uint32_t n_hist = 0;
-  uint32_t kmax = 16;
+  uint32_t kmax = 16;               // template KMAX of the workgroup passes (max K <= 128)
   uint32_t n_recs = 0, n_pool = 0;
+  uint8_t* arena = nullptr;
+  size_t arena_cap = 0;
+  uint8_t* stage = nullptr;         // pinned host memory
+  size_t stage_cap = 0;
   OpRec* recs = nullptr;
   uint64_t* pool = nullptr;
   uint32_t* chain_start = nullptr;
   HistDesc* hist = nullptr;
-  uint32_t* order = nullptr;        // LPT processing order: [K<=16 | K<=32 | rest]
-  uint32_t n_pack16 = 0, n_pack32 = 0;
-  std::vector<uint8_t> in_pack16;   // per history: in the pack_kernel<16> list
-  std::vector<uint64_t> h_in_bytes; // per history: input SoA bytes (48 per op + 8 per record hash)
-  std::vector<uint32_t> h_rest;     // histories searched one per workgroup (32 < K <= 128)
-  std::vector<uint32_t> h_level;    // histories searched by the device-wide level search (K > 128)
-  LevelBufs lv;
+  uint32_t* order = nullptr;        // packed-kernel lists, LPT order: [K<=16 | 16<K<=32]
   HistResult* res = nullptr;
   uint32_t* moves = nullptr;        // witness moves (per history at witness_off)
-  uint32_t* counter = nullptr;      // work counters (scheduling)
+  uint32_t* rcounts = nullptr;      // per-round unique configurations (same offsets as moves)
+  uint32_t* list = nullptr;         // histories of a workgroup pass
+  uint32_t n_pack16 = 0, n_pack32 = 0;
+  std::vector<uint32_t> lpt;        // searchable histories, longest (n_ops x K) first
+  std::vector<uint64_t> h_in_bytes; // per history: input SoA bytes (48 per op + 8 per record hash)
+  LevelBufs lv;
+  uint32_t* counter = nullptr;      // work counters (scheduling) + the run's deadline (u64 at [16])
   TraceEnt* trace = nullptr;
   unsigned long long* trace_head = nullptr;
   uint64_t trace_cap = 0;
   uint8_t* slab = nullptr;
   size_t slab_cap = 0;
-  // host mirrors
-  std::vector<HistDesc> h_hist;
-  std::vector<HistResult> h_res;
-  bool h_res_pinned = false;          // h_res page-locked (hipHostRegister) for the per-run read-back
-  std::vector<uint32_t> h_moves_off;  // witness_off per history
+  hipEvent_t ev[6] = {nullptr, nullptr, nullptr, nullptr, nullptr, nullptr};
+  // host views
+  HistDesc* h_hist = nullptr;        // in stage
+  HistResult* h_res = nullptr;       // in stage (pinned: the per-run read-back is a direct DMA)
+  std::vector<uint32_t> h_moves_off; // witness_off per history
   uint64_t moves_cap = 0;
-  std::vector<uint32_t> h_moves;
-  std::vector<const History*> src;    // host histories (not owned)
-  std::vector<uint32_t> forced;       // per history: 0 search, else verdict fixed on host
+  uint32_t* h_moves = nullptr;       // pinned copy of the witness moves (results with witnesses)
+  size_t h_moves_cap = 0;
+  std::vector<uint32_t> h_rcounts;   // host copy of rcounts after a run with round counts
+  bool rc_valid = false;
+  std::vector<const History*> src;   // host histories (not owned)
+  std::vector<uint32_t> forced;      // per history: 0 search, else verdict fixed on host
   uint64_t algo_bytes_inputs = 0;
+};
+
+// Options of one batch_run (from the context, include/s2lincheck.h s2lc_opts).
+struct RunOpts {
+  uint64_t max_configs = 0;
+  bool witness = true;
+  bool round_counts = false;
+  uint32_t engine = 0;               // s2lc_engine
+  uint64_t timeout_us = 0;           // 0 = none
 };
 
 struct RunStats {
@@ -127,16 +148,24 @@ struct RunStats {
   LevelStats level;
 };
 
-int batch_upload(DevBatch& b, const std::vector<const History*>& hs, std::string& err);
+// reductions_off: S2LC_RED_* bits cleared from every history's flags.
+int batch_upload(DevBatch& b, const std::vector<const History*>& hs, uint32_t reductions_off, std::string& err);
 void batch_release(DevBatch& b);
-int batch_run(DevBatch& b, hipStream_t stream, uint64_t max_configs, bool witness, RunStats& st,
-              std::string& err);
+// Copy the witness moves of the last run into b.h_moves (pinned).
+int batch_fetch_moves(DevBatch& b, std::string& err);
+// out[i] = fold_hashes_blk(seeds[i], pool[offs[i] ..+ cnts[i]]) on the device.
+int device_fold(const uint64_t* seeds, const uint64_t* pool, size_t pool_len, const uint32_t* offs, const uint32_t* cnts,
+                size_t n, uint64_t* out, hipStream_t stream, std::string& err);
+int batch_run(DevBatch& b, hipStream_t stream, const RunOpts& ro, RunStats& st, std::string& err);
 
 constexpr uint32_t LEVEL_KMAX = 512;  // most chains the level search handles
 uint32_t level_kmax(uint32_t K);
-int level_search(DevBatch& b, uint32_t h, hipStream_t st, uint64_t max_configs, bool witness, LevelStats& ls,
+// deadline: steady-clock time in ns since epoch after which the search gives
+// Unknown (S2LC_R_TIMEOUT); 0 = none.
+int level_search(DevBatch& b, uint32_t h, hipStream_t st, const RunOpts& ro, int64_t deadline_ns, LevelStats& ls,
                  std::string& err);
 void level_release(DevBatch& b);
+int64_t steady_ns();
 
 // One rank's part of the distributed level search of a single history.
 struct DistLevel {
@@ -155,7 +184,8 @@ struct DistLevel {
   uint64_t configs = 0, children = 0, max_frontier = 0;
   double ms = 0;
 };
-int dist_create(DistLevel& d, const History* h, uint32_t rank, uint32_t world, std::string& err);
+int dist_create(DistLevel& d, const History* h, uint32_t rank, uint32_t world, uint32_t reductions_off,
+                std::string& err);
 void dist_release(DistLevel& d);
 int dist_expand(DistLevel& d, uint64_t* counts, int* found, std::string& err);
 int dist_pack(DistLevel& d, uint8_t* send, const uint64_t* counts, std::string& err);

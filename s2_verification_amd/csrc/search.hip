@@ -116,31 +116,64 @@ hipError_t launch_geom(const SearchGeom& g, const Params& prm, hipStream_t st) {
 
 }  // namespace
 
-int batch_upload(DevBatch& b, const std::vector<const History*>& hs, std::string& err) {
-  b.n_hist = (uint32_t)hs.size();
+int64_t steady_ns() {
+  return std::chrono::duration_cast<std::chrono::nanoseconds>(std::chrono::steady_clock::now().time_since_epoch())
+      .count();
+}
+
+namespace {
+
+size_t align256(size_t x) { return (x + 255) & ~(size_t)255; }
+
+// Grow-only device / pinned-host buffers (a context's scratch batch is reused
+// by every s2lc_check, so steady-state calls allocate nothing).
+int grow_device(uint8_t** p, size_t& cap, size_t need, std::string& err) {
+  if (need <= cap && *p) return 0;
+  if (*p) (void)hipFree(*p);
+  *p = nullptr;
+  cap = 0;
+  const size_t want = std::max<size_t>(need + need / 4, 1 << 16);
+  HIPCHK(hipMalloc(p, want));
+  cap = want;
+  return 0;
+}
+
+int grow_pinned(uint8_t** p, size_t& cap, size_t need, std::string& err) {
+  if (need <= cap && *p) return 0;
+  if (*p) (void)hipHostFree(*p);
+  *p = nullptr;
+  cap = 0;
+  const size_t want = std::max<size_t>(need + need / 4, 1 << 16);
+  HIPCHK(hipHostMalloc(p, want, hipHostMallocDefault));
+  cap = want;
+  return 0;
+}
+
+}  // namespace
+
+int batch_upload(DevBatch& b, const std::vector<const History*>& hs, uint32_t red_off, std::string& err) {
+  const uint16_t clear = (uint16_t)(((red_off & S2LC_RED_P1) ? H_NOWRAP : 0) | ((red_off & S2LC_RED_P2) ? H_P2OK : 0) |
+                                    ((red_off & S2LC_RED_P4) ? H_P4 : 0) | ((red_off & S2LC_RED_IDEFER) ? H_IDEFER : 0));
+  const size_t n = hs.size();
+  b.n_hist = (uint32_t)n;
   b.src = hs;
-  b.forced.assign(hs.size(), 0);
+  b.forced.assign(n, 0);
+  b.rc_valid = false;
   uint32_t kmax_needed = 1;
   size_t n_recs = 0, n_pool = 0, n_cs = 0;
   uint64_t moves_total = 0;
-  b.h_hist.resize(hs.size());
-  b.h_moves_off.resize(hs.size());
-  b.h_in_bytes.assign(hs.size(), 0);
-  for (size_t i = 0; i < hs.size(); ++i) {
+  b.h_moves_off.resize(n);
+  b.h_in_bytes.assign(n, 0);
+  b.algo_bytes_inputs = 0;
+  for (size_t i = 0; i < n; ++i) {
     const History& h = *hs[i];
     if (h.status != 0) { err = "history " + std::to_string(i) + ": " + h.error; return h.status; }
-    if (h.structural) { b.forced[i] = 1; }
+    if (h.structural) b.forced[i] = 1;
     if (h.K > LEVEL_KMAX) { err = "history has more than 512 concurrent chains"; return S2LC_EUNSUPPORTED; }
     if (h.max_chain_len >= 0xFFFF) { err = "chain longer than 65534 ops"; return S2LC_EUNSUPPORTED; }
     if (h.K <= 128) kmax_needed = std::max(kmax_needed, h.K);
-    HistDesc& d = b.h_hist[i];
-    d.rec_base = (uint32_t)n_recs;
-    d.cs_base = (uint32_t)n_cs;
-    d.K = (uint16_t)h.K;
-    d.flags = h.hflags;
-    d.n_ops = h.n_ops;
     n_recs += h.recs.size();
-    n_cs += h.K + 1;
+    n_cs += h.chain_start.empty() ? 1 : h.K + 1;
     n_pool += h.pool.size();
     b.h_moves_off[i] = (uint32_t)moves_total;
     moves_total += h.n_ops + 1;
@@ -154,108 +187,112 @@ int batch_upload(DevBatch& b, const std::vector<const History*>& hs, std::string
     return S2LC_EUNSUPPORTED;
   }
   b.kmax = kmax_needed <= 16 ? 16 : kmax_needed <= 32 ? 32 : kmax_needed <= 64 ? 64 : 128;
-  std::vector<OpRec> recs(std::max<size_t>(n_recs, 1));
-  std::vector<uint64_t> pool(std::max<size_t>(n_pool, 1));
-  std::vector<uint32_t> cs(std::max<size_t>(n_cs, 1));
+  b.moves_cap = moves_total;
+  b.n_recs = (uint32_t)std::max<size_t>(n_recs, 1);
+  b.n_pool = (uint32_t)std::max<size_t>(n_pool, 1);
+  // layout (stage = the uploaded prefix of the arena)
+  const size_t o_recs = 0;
+  const size_t o_pool = align256(o_recs + b.n_recs * sizeof(OpRec));
+  const size_t o_cs = align256(o_pool + b.n_pool * sizeof(uint64_t));
+  const size_t o_hist = align256(o_cs + std::max<size_t>(n_cs, 1) * sizeof(uint32_t));
+  const size_t o_order = align256(o_hist + std::max<size_t>(n, 1) * sizeof(HistDesc));
+  const size_t o_res = align256(o_order + std::max<size_t>(n, 1) * sizeof(uint32_t));
+  const size_t stage_bytes = align256(o_res + std::max<size_t>(n, 1) * sizeof(HistResult));
+  const size_t o_moves = stage_bytes;
+  const size_t o_rc = align256(o_moves + std::max<uint64_t>(moves_total, 1) * sizeof(uint32_t));
+  const size_t o_list = align256(o_rc + std::max<uint64_t>(moves_total, 1) * sizeof(uint32_t));
+  const size_t arena_bytes = align256(o_list + std::max<size_t>(n, 1) * sizeof(uint32_t));
+  if (grow_pinned(&b.stage, b.stage_cap, stage_bytes, err)) return S2LC_EHIP;
+  if (grow_device(&b.arena, b.arena_cap, arena_bytes, err)) return S2LC_EHIP;
+  OpRec* s_recs = reinterpret_cast<OpRec*>(b.stage + o_recs);
+  uint64_t* s_pool = reinterpret_cast<uint64_t*>(b.stage + o_pool);
+  uint32_t* s_cs = reinterpret_cast<uint32_t*>(b.stage + o_cs);
+  b.h_hist = reinterpret_cast<HistDesc*>(b.stage + o_hist);
+  uint32_t* s_order = reinterpret_cast<uint32_t*>(b.stage + o_order);
+  b.h_res = reinterpret_cast<HistResult*>(b.stage + o_res);
+  b.recs = reinterpret_cast<OpRec*>(b.arena + o_recs);
+  b.pool = reinterpret_cast<uint64_t*>(b.arena + o_pool);
+  b.chain_start = reinterpret_cast<uint32_t*>(b.arena + o_cs);
+  b.hist = reinterpret_cast<HistDesc*>(b.arena + o_hist);
+  b.order = reinterpret_cast<uint32_t*>(b.arena + o_order);
+  b.res = reinterpret_cast<HistResult*>(b.arena + o_res);
+  b.moves = reinterpret_cast<uint32_t*>(b.arena + o_moves);
+  b.rcounts = reinterpret_cast<uint32_t*>(b.arena + o_rc);
+  b.list = reinterpret_cast<uint32_t*>(b.arena + o_list);
   size_t pr = 0, pp = 0, pc = 0;
-  for (size_t i = 0; i < hs.size(); ++i) {
+  for (size_t i = 0; i < n; ++i) {
     const History& h = *hs[i];
+    HistDesc& d = b.h_hist[i];
+    d.rec_base = (uint32_t)pr;
+    d.cs_base = (uint32_t)pc;
+    d.K = (uint16_t)h.K;
+    d.flags = (uint16_t)(h.hflags & ~clear);
+    d.n_ops = h.n_ops;
     for (const OpRec& r0 : h.recs) {
       OpRec r = r0;
       r.hash_off = (uint32_t)(r0.hash_off + pp);
-      recs[pr++] = r;
+      s_recs[pr++] = r;
     }
-    for (uint32_t j = 0; j <= h.K && !h.chain_start.empty(); ++j) cs[pc++] = b.h_hist[i].rec_base + h.chain_start[j];
-    if (h.chain_start.empty()) cs[pc++] = b.h_hist[i].rec_base;
-    std::copy(h.pool.begin(), h.pool.end(), pool.begin() + pp);
+    if (h.chain_start.empty()) s_cs[pc++] = d.rec_base;
+    else for (uint32_t j = 0; j <= h.K; ++j) s_cs[pc++] = d.rec_base + h.chain_start[j];
+    if (!h.pool.empty()) memcpy(s_pool + pp, h.pool.data(), h.pool.size() * sizeof(uint64_t));
     pp += h.pool.size();
+    HistResult& R = b.h_res[i];
+    R = HistResult{};
+    R.verdict = V_UNKNOWN;
+    R.witness_off = b.h_moves_off[i];
   }
-  // longest-first processing order (LPT): work ~ ops x chains; split into the
-  // packed-group lists (K <= 16, K <= 32) and the rest (workgroup per history)
-  std::vector<uint32_t> order;
-  order.reserve(hs.size());
-  for (uint32_t i = 0; i < hs.size(); ++i)
-    if (!b.forced[i]) order.push_back(i);
-  std::stable_sort(order.begin(), order.end(), [&](uint32_t x, uint32_t y) {
+  // longest-first processing order (LPT): work ~ ops x chains
+  b.lpt.clear();
+  for (uint32_t i = 0; i < n; ++i)
+    if (!b.forced[i]) b.lpt.push_back(i);
+  std::stable_sort(b.lpt.begin(), b.lpt.end(), [&](uint32_t x, uint32_t y) {
     return (uint64_t)b.h_hist[x].n_ops * b.h_hist[x].K > (uint64_t)b.h_hist[y].n_ops * b.h_hist[y].K;
   });
-  {
-    std::vector<uint32_t> l16, l32, rest;
-    b.h_level.clear();
-    // S2LC_LEVEL_ONLY=1 (tests): every history through the level search
-    const char* lo = getenv("S2LC_LEVEL_ONLY");
-    const bool level_only = lo && lo[0] == '1';
-    for (uint32_t i : order) {
-      const uint32_t K = b.h_hist[i].K;
-      if (level_only) b.h_level.push_back(i);
-      else (K <= 16 ? l16 : K <= 32 ? l32 : K <= 128 ? rest : b.h_level).push_back(i);
-    }
-    b.n_pack16 = (uint32_t)l16.size();
-    b.in_pack16.assign(hs.size(), 0);
-    for (uint32_t i : l16) b.in_pack16[i] = 1;
-    b.n_pack32 = (uint32_t)l32.size();
-    b.h_rest = rest;
-    order = l16;
-    order.insert(order.end(), l32.begin(), l32.end());
-    order.insert(order.end(), rest.begin(), rest.end());
-  }
-  b.moves_cap = moves_total;
-  b.n_recs = (uint32_t)recs.size();
-  b.n_pool = (uint32_t)pool.size();
-  HIPCHK(hipMalloc(&b.recs, recs.size() * sizeof(OpRec)));
-  HIPCHK(hipMalloc(&b.pool, pool.size() * sizeof(uint64_t)));
-  HIPCHK(hipMalloc(&b.chain_start, cs.size() * sizeof(uint32_t)));
-  HIPCHK(hipMalloc(&b.hist, std::max<size_t>(hs.size(), 1) * sizeof(HistDesc)));
-  HIPCHK(hipMalloc(&b.order, std::max<size_t>(order.size(), 1) * sizeof(uint32_t)));
-  HIPCHK(hipMalloc(&b.res, std::max<size_t>(hs.size(), 1) * sizeof(HistResult)));
-  HIPCHK(hipMalloc(&b.moves, std::max<uint64_t>(moves_total, 1) * sizeof(uint32_t)));
-  HIPCHK(hipMalloc(&b.counter, 16 * sizeof(uint32_t)));
-  HIPCHK(hipMalloc(&b.trace_head, sizeof(unsigned long long)));
-  HIPCHK(hipMemcpy(b.recs, recs.data(), recs.size() * sizeof(OpRec), hipMemcpyHostToDevice));
-  HIPCHK(hipMemcpy(b.pool, pool.data(), pool.size() * sizeof(uint64_t), hipMemcpyHostToDevice));
-  HIPCHK(hipMemcpy(b.chain_start, cs.data(), cs.size() * sizeof(uint32_t), hipMemcpyHostToDevice));
-  if (!hs.empty()) HIPCHK(hipMemcpy(b.hist, b.h_hist.data(), hs.size() * sizeof(HistDesc), hipMemcpyHostToDevice));
-  if (!order.empty()) HIPCHK(hipMemcpy(b.order, order.data(), order.size() * sizeof(uint32_t), hipMemcpyHostToDevice));
-  if (b.h_res_pinned) { (void)hipHostUnregister(b.h_res.data()); b.h_res_pinned = false; }
-  b.h_res.assign(hs.size(), HistResult{});
-  for (size_t i = 0; i < hs.size(); ++i) b.h_res[i].witness_off = b.h_moves_off[i];
-  // every run reads the results back: page-lock them so that copy is a direct DMA
-  if (!hs.empty() && hipHostRegister(b.h_res.data(), hs.size() * sizeof(HistResult), hipHostRegisterDefault) == hipSuccess)
-    b.h_res_pinned = true;
-  (void)hipGetLastError();  // a failed registration only costs the staged copy
-  if (!hs.empty()) HIPCHK(hipMemcpy(b.res, b.h_res.data(), hs.size() * sizeof(HistResult), hipMemcpyHostToDevice));
+  // the packed-kernel lists (engine AUTO): K <= 16, then 16 < K <= 32
+  uint32_t no = 0;
+  for (uint32_t i : b.lpt) if (b.h_hist[i].K <= 16) s_order[no++] = i;
+  b.n_pack16 = no;
+  for (uint32_t i : b.lpt) if (b.h_hist[i].K > 16 && b.h_hist[i].K <= 32) s_order[no++] = i;
+  b.n_pack32 = no - b.n_pack16;
+  HIPCHK(hipMemcpy(b.arena, b.stage, stage_bytes, hipMemcpyHostToDevice));
   return 0;
 }
 
 void batch_release(DevBatch& b) {
   level_release(b);
-  if (b.h_res_pinned) { (void)hipHostUnregister(b.h_res.data()); b.h_res_pinned = false; }
-  void* ptrs[] = {b.recs, b.pool, b.chain_start, b.hist, b.order, b.res, b.moves, b.counter, b.trace, b.trace_head, b.slab};
-  for (void* q : ptrs) if (q) (void)hipFree(q);
+  void* dptrs[] = {b.arena, b.counter, b.trace, b.trace_head, b.slab};
+  for (void* q : dptrs) if (q) (void)hipFree(q);
+  if (b.stage) (void)hipHostFree(b.stage);
+  if (b.h_moves) (void)hipHostFree(b.h_moves);
+  for (hipEvent_t& e : b.ev) {
+    if (e) (void)hipEventDestroy(e);
+    e = nullptr;
+  }
+  b.arena = nullptr; b.arena_cap = 0; b.stage = nullptr; b.stage_cap = 0;
+  b.h_moves = nullptr; b.h_moves_cap = 0;
   b.recs = nullptr; b.pool = nullptr; b.chain_start = nullptr; b.hist = nullptr; b.order = nullptr;
-  b.res = nullptr; b.moves = nullptr; b.counter = nullptr; b.trace = nullptr; b.trace_head = nullptr;
-  b.slab = nullptr; b.slab_cap = 0; b.trace_cap = 0;
+  b.res = nullptr; b.moves = nullptr; b.rcounts = nullptr; b.list = nullptr; b.h_hist = nullptr; b.h_res = nullptr;
+  b.counter = nullptr; b.trace = nullptr; b.trace_head = nullptr; b.trace_cap = 0;
+  b.slab = nullptr; b.slab_cap = 0;
 }
 
-static int ensure(void** p, size_t& cap, size_t need, std::string& err) {
-  if (need <= cap) return 0;
-  if (*p) (void)hipFree(*p);
-  *p = nullptr;
-  cap = 0;
-  HIPCHK(hipMalloc(p, need));
-  cap = need;
-  return 0;
-}
-
-int batch_run(DevBatch& b, hipStream_t stream, uint64_t max_configs, bool witness, RunStats& st, std::string& err) {
+int batch_run(DevBatch& b, hipStream_t stream, const RunOpts& ro, RunStats& st, std::string& err) {
   st = RunStats{};
-  auto t0 = std::chrono::steady_clock::now();
+  const int64_t t0 = steady_ns();
+  const int64_t deadline_ns = ro.timeout_us ? t0 + (int64_t)std::min<uint64_t>(ro.timeout_us, 1ull << 40) * 1000 : 0;
+  const bool witness = ro.witness;
   int dev = 0;
   HIPCHK(hipGetDevice(&dev));
   int n_cu = 256;
   (void)hipDeviceGetAttribute(&n_cu, hipDeviceAttributeMultiprocessorCount, dev);
+  b.rc_valid = false;
 
-  // trace pool: generous, reused across runs
+  if (!b.counter) HIPCHK(hipMalloc(&b.counter, 32 * sizeof(uint32_t)));  // [0..15] work counters, [16..17] deadline
+  if (!b.trace_head) HIPCHK(hipMalloc(&b.trace_head, sizeof(unsigned long long)));
+  for (hipEvent_t& e : b.ev)
+    if (!e) HIPCHK(hipEventCreate(&e));
+  // trace pool: generous, allocated once per batch and reused across runs
   if (witness && b.trace_cap == 0) {
     size_t free_b = 0, total_b = 0;
     HIPCHK(hipMemGetInfo(&free_b, &total_b));
@@ -265,46 +302,62 @@ int batch_run(DevBatch& b, hipStream_t stream, uint64_t max_configs, bool witnes
     b.trace_cap = want;
   }
 
+  // engine routing; the environment overrides the context (diagnostics)
+  uint32_t engine = ro.engine;
+  {
+    const char* lo = getenv("S2LC_LEVEL_ONLY");
+    const char* np = getenv("S2LC_NO_PACK");
+    if (lo && lo[0] == '1') engine = S2LC_ENGINE_LEVEL;
+    else if (np && np[0] == '1' && engine == S2LC_ENGINE_AUTO) engine = S2LC_ENGINE_WORKGROUP;
+  }
+
   Params prm;
   memset(&prm, 0, sizeof prm);
   prm.recs = b.recs; prm.pool = b.pool; prm.chain_start = b.chain_start; prm.hist = b.hist;
   prm.trace = b.trace; prm.trace_head = b.trace_head; prm.trace_cap = witness ? b.trace_cap : 0;
-  prm.res = b.res; prm.max_configs = max_configs; prm.witness = witness ? 1 : 0;
+  prm.res = b.res; prm.max_configs = ro.max_configs; prm.witness = witness ? 1 : 0;
   prm.n_recs = b.n_recs; prm.n_pool = b.n_pool; prm.n_res = b.n_hist;
+  prm.rcounts = ro.round_counts ? b.rcounts : nullptr;
 
-  hipEvent_t e0, e1;
-  HIPCHK(hipEventCreate(&e0));
-  HIPCHK(hipEventCreate(&e1));
   HIPCHK(hipMemsetAsync(b.counter, 0, 16 * sizeof(uint32_t), stream));
   HIPCHK(hipMemsetAsync(b.trace_head, 0, sizeof(unsigned long long), stream));
+  if (b.n_hist) {
+    hipLaunchKernelGGL(reset_results_kernel, dim3((b.n_hist + 255) / 256), dim3(256), 0, stream, b.res, b.n_hist);
+    HIPCHK(hipGetLastError());
+  }
+  if (deadline_ns) {
+    int rate_khz = 100000;  // device wall clock (s_memrealtime); 100 MHz on gfx950
+    (void)hipDeviceGetAttribute(&rate_khz, hipDeviceAttributeWallClockRate, dev);
+    const int64_t left_ns = std::max<int64_t>(0, deadline_ns - steady_ns());
+    const unsigned long long ticks = (unsigned long long)((double)left_ns * 1e-6 * rate_khz);
+    unsigned long long* d = reinterpret_cast<unsigned long long*>(b.counter + 16);
+    hipLaunchKernelGGL(deadline_kernel, dim3(1), dim3(1), 0, stream, d, std::max<unsigned long long>(ticks, 1));
+    HIPCHK(hipGetLastError());
+    prm.deadline = d;
+  }
 
-  // Packed passes: one L-lane group per history (K <= 16: L = 16, K <= 32:
-  // L = 32), frontier <= PACK_F. Histories that outgrow that frontier, and
-  // those with K > 32, go on to the workgroup-per-history passes:
-  // Pass 0: LDS-resident search (small frontier / staging).
-  // Pass 1: HBM slab, 64 lanes, frontier 1024, for the ones that outgrew LDS.
-  // Pass 2: HBM slab, 256 lanes, frontier up to 2^20.
-  // Pass 0 sizing: one wave per workgroup; the LDS budget per workgroup is
-  // what the kernel's register occupancy allows (16 / 12 workgroups per CU for
-  // KMAX 16 / 32), so LDS never limits residency below the register limit.
-  const bool use_pack = getenv("S2LC_NO_PACK") == nullptr;
+  // the histories of each engine, LPT order
+  std::vector<uint32_t> todo;   // workgroup passes
+  std::vector<uint32_t> level;  // device-wide level search
+  const bool use_pack = engine == S2LC_ENGINE_AUTO;
+  for (uint32_t i : b.lpt) {
+    const uint32_t K = b.h_hist[i].K;
+    if (engine == S2LC_ENGINE_LEVEL || K > 128) level.push_back(i);
+    else if (!use_pack || K > 32) todo.push_back(i);
+  }
   // histories settled by pack_kernel<16> (roofline accounting of that kernel)
   std::vector<uint8_t> pack16_done(b.n_hist, 0);
-  if (use_pack)
-    for (uint32_t i = 0; i < b.n_hist; ++i) pack16_done[i] = b.in_pack16[i];
-  std::vector<uint32_t> todo;  // histories for the workgroup-per-history passes
-  if (use_pack) {
+  if (use_pack && b.n_pack16 + b.n_pack32) {
 #ifdef S2LC_PROF
     {
       unsigned long long z[16] = {0};
       HIPCHK(hipMemcpyToSymbol(HIP_SYMBOL(g_prof), z, sizeof z));
     }
 #endif
-    // Both packed launches, then (witness on) the walk of the histories they
-    // settled, then one results read-back: a batch that needs no other pass
-    // (all of C4) costs a single host sync per run.
-    hipEvent_t pe[4];
-    for (hipEvent_t& e : pe) HIPCHK(hipEventCreate(&e));
+    // Packed passes: one L-lane group per history (K <= 16: L = 16, K <= 32:
+    // L = 32), frontier <= PACK_F. Both launches, then (witness on) the walk of
+    // the histories they settled, then one results read-back: a batch that
+    // needs no other pass (all of C4) costs a single host sync per run.
     bool launched[2] = {false, false};
     for (int li = 0; li < 2; ++li) {
       const uint32_t n_l = li == 0 ? b.n_pack16 : b.n_pack32;
@@ -321,32 +374,29 @@ int batch_run(DevBatch& b, hipStream_t stream, uint64_t max_configs, bool witnes
       const uint32_t groups = PACK_BLOCK / L;
       const uint32_t grid = std::max<uint32_t>(
           1, std::min<uint32_t>((n_l + groups - 1) / groups, (uint32_t)n_cu * (uint32_t)std::max(1, bpc)));
-      HIPCHK(hipEventRecord(pe[2 * li], stream));
+      HIPCHK(hipEventRecord(b.ev[2 * li], stream));
       if (li == 0) hipLaunchKernelGGL(pack_kernel<16>, dim3(grid), dim3(PACK_BLOCK), smem, stream, pp);
       else hipLaunchKernelGGL(pack_kernel<32>, dim3(grid), dim3(PACK_BLOCK), smem, stream, pp);
       HIPCHK(hipGetLastError());
-      HIPCHK(hipEventRecord(pe[2 * li + 1], stream));
+      HIPCHK(hipEventRecord(b.ev[2 * li + 1], stream));
       launched[li] = true;
       st.launches++;
     }
-    if (b.n_pack16 + b.n_pack32) {
-      if (witness) {
-        hipLaunchKernelGGL(walk_kernel, dim3((b.n_hist + 255) / 256), dim3(256), 0, stream, b.n_hist, b.res,
-                           (const TraceEnt*)b.trace, b.moves);
-        HIPCHK(hipGetLastError());
-      }
-      HIPCHK(hipMemcpyAsync(b.h_res.data(), b.res, b.n_hist * sizeof(HistResult), hipMemcpyDeviceToHost, stream));
-      HIPCHK(hipStreamSynchronize(stream));
+    if (witness) {
+      hipLaunchKernelGGL(walk_kernel, dim3((b.n_hist + 255) / 256), dim3(256), 0, stream, b.n_hist, b.res,
+                         (const TraceEnt*)b.trace, b.moves);
+      HIPCHK(hipGetLastError());
     }
+    HIPCHK(hipMemcpyAsync(b.h_res, b.res, b.n_hist * sizeof(HistResult), hipMemcpyDeviceToHost, stream));
+    HIPCHK(hipStreamSynchronize(stream));
     for (int li = 0; li < 2; ++li) {
       if (!launched[li]) continue;
       float ms = 0;
-      HIPCHK(hipEventElapsedTime(&ms, pe[2 * li], pe[2 * li + 1]));
+      HIPCHK(hipEventElapsedTime(&ms, b.ev[2 * li], b.ev[2 * li + 1]));
       st.kernel_ms += ms;
       st.pack_ms += ms;
       if (li == 0) st.pack16_ms = ms;
     }
-    for (hipEvent_t e : pe) (void)hipEventDestroy(e);
 #ifdef S2LC_PROF
     {
       unsigned long long gp[16];
@@ -356,24 +406,24 @@ int batch_run(DevBatch& b, hipStream_t stream, uint64_t max_configs, bool witnes
               gp[13], gp[15], gp[10] / rd, gp[11] / rd, gp[12] / rd);
     }
 #endif
-    for (uint32_t i = 0; i < b.n_hist; ++i)
-      if (!b.forced[i] && b.h_hist[i].K <= 32 && b.h_res[i].verdict == V_UNKNOWN && b.h_res[i].reason == S2LC_R_FRONTIER)
-        todo.push_back(i);
-    st.n_overflow = (uint32_t)todo.size();
-    for (uint32_t i : todo) pack16_done[i] = 0;
-    todo.insert(todo.end(), b.h_rest.begin(), b.h_rest.end());
-  } else {
-    std::vector<uint32_t> all(b.n_pack16 + b.n_pack32 + b.h_rest.size());
-    if (!all.empty()) HIPCHK(hipMemcpy(all.data(), b.order, all.size() * sizeof(uint32_t), hipMemcpyDeviceToHost));
-    todo = all;
+    // histories that outgrew the packed frontier go on to the workgroup passes
+    std::vector<uint32_t> over;
+    for (uint32_t i : b.lpt) {
+      const uint32_t K = b.h_hist[i].K;
+      if (K > 32) continue;
+      if (b.h_res[i].verdict == V_UNKNOWN && b.h_res[i].reason == S2LC_R_FRONTIER) over.push_back(i);
+      else if (K <= 16) pack16_done[i] = 1;
+    }
+    st.n_overflow = (uint32_t)over.size();
+    over.insert(over.end(), todo.begin(), todo.end());
+    todo.swap(over);
   }
   const uint32_t lds_fcap = 8;
   const uint32_t lds_stage = 32;
   const size_t lds_budget = b.kmax <= 16 ? 10240 : b.kmax <= 32 ? 13312 : 0;
-  uint32_t* d_list = nullptr;
   int n_passes_run = 0;
-  for (int pass = 0; pass < 2; ++pass) {
-    uint32_t n_pass = (uint32_t)todo.size();
+  for (int pass = engine == S2LC_ENGINE_WORKGROUP_HBM ? 1 : 0; pass < 2; ++pass) {
+    const uint32_t n_pass = (uint32_t)todo.size();
     if (n_pass == 0) break;
     ++n_passes_run;
     SearchGeom g;
@@ -385,13 +435,10 @@ int batch_run(DevBatch& b, hipStream_t stream, uint64_t max_configs, bool witnes
       g = make_geom(b.kmax, false, 64, 1024, 512, 256, 1, 0);
       g.grid = std::max<uint32_t>(1, std::min<uint32_t>(n_pass, (uint32_t)n_cu * 16));
     }
-    if (!g.shared && ensure((void**)&b.slab, b.slab_cap, g.slab_bytes * g.grid, err)) return S2LC_EHIP;
+    if (!g.shared && grow_device(&b.slab, b.slab_cap, g.slab_bytes * g.grid, err)) return S2LC_EHIP;
     Params pp = prm;
-    if (d_list) (void)hipFree(d_list);
-    d_list = nullptr;
-    HIPCHK(hipMalloc(&d_list, todo.size() * sizeof(uint32_t)));
-    HIPCHK(hipMemcpyAsync(d_list, todo.data(), todo.size() * sizeof(uint32_t), hipMemcpyHostToDevice, stream));
-    pp.order = d_list;
+    HIPCHK(hipMemcpyAsync(b.list, todo.data(), todo.size() * sizeof(uint32_t), hipMemcpyHostToDevice, stream));
+    pp.order = b.list;
     pp.n_hist = n_pass;
     pp.counter = b.counter + 4 * pass;
     pp.slab = b.slab;
@@ -410,11 +457,11 @@ int batch_run(DevBatch& b, hipStream_t stream, uint64_t max_configs, bool witnes
       HIPCHK(hipMemcpyToSymbol(HIP_SYMBOL(g_prof), z, sizeof z));
     }
 #endif
-    HIPCHK(hipEventRecord(e0, stream));
+    HIPCHK(hipEventRecord(b.ev[4], stream));
     HIPCHK(launch_geom(g, pp, stream));
-    HIPCHK(hipEventRecord(e1, stream));
+    HIPCHK(hipEventRecord(b.ev[5], stream));
     st.launches++;
-    HIPCHK(hipMemcpyAsync(b.h_res.data(), b.res, b.n_hist * sizeof(HistResult), hipMemcpyDeviceToHost, stream));
+    HIPCHK(hipMemcpyAsync(b.h_res, b.res, b.n_hist * sizeof(HistResult), hipMemcpyDeviceToHost, stream));
     HIPCHK(hipStreamSynchronize(stream));
 #ifdef S2LC_GUARD
     {
@@ -428,7 +475,7 @@ int batch_run(DevBatch& b, hipStream_t stream, uint64_t max_configs, bool witnes
     }
 #endif
     float ms = 0;
-    HIPCHK(hipEventElapsedTime(&ms, e0, e1));
+    HIPCHK(hipEventElapsedTime(&ms, b.ev[4], b.ev[5]));
 #ifdef S2LC_PROF
     {
       unsigned long long gp[16];
@@ -445,35 +492,38 @@ int batch_run(DevBatch& b, hipStream_t stream, uint64_t max_configs, bool witnes
 #endif
     st.kernel_ms += ms;
     if (pass == 0) st.pass0_ms = ms;
-    // histories that outgrew this pass's frontier go to the next pass
+    // histories of THIS pass that outgrew its frontier go to the next pass
     std::vector<uint32_t> next;
-    for (uint32_t i = 0; i < b.n_hist; ++i)
-      if (!b.forced[i] && b.h_res[i].verdict == V_UNKNOWN && b.h_res[i].reason == S2LC_R_FRONTIER) next.push_back(i);
+    for (uint32_t i : todo)
+      if (b.h_res[i].verdict == V_UNKNOWN && b.h_res[i].reason == S2LC_R_FRONTIER) next.push_back(i);
     if (pass == 0) st.n_overflow += (uint32_t)next.size();
     else st.n_overflow2 += (uint32_t)next.size();
     todo.swap(next);
   }
-  if (d_list) (void)hipFree(d_list);
-  // Pass 2: the device-wide level search, one history at a time: histories
-  // with more than 128 chains and those whose frontier outgrew pass 1.
-  todo.insert(todo.end(), b.h_level.begin(), b.h_level.end());
+  if (ro.round_counts) {
+    b.h_rcounts.resize(std::max<uint64_t>(b.moves_cap, 1));
+    HIPCHK(hipMemcpyAsync(b.h_rcounts.data(), b.rcounts, b.moves_cap * sizeof(uint32_t), hipMemcpyDeviceToHost, stream));
+    HIPCHK(hipStreamSynchronize(stream));
+  }
+  // the device-wide level search, one history at a time: histories with more
+  // than 128 chains and those whose frontier outgrew the workgroup passes
+  todo.insert(todo.end(), level.begin(), level.end());
   for (uint32_t h : todo) {
-    const int rc = level_search(b, h, stream, max_configs, witness, st.level, err);
+    const int rc = level_search(b, h, stream, ro, deadline_ns, st.level, err);
     if (rc) return rc;
   }
   st.kernel_ms += st.level.ms;
   // the packed histories were walked with the packed launches; walk again only
   // for what the other passes settled (walk_kernel skips walked histories)
-  const bool other_work = !use_pack || n_passes_run > 0 || !todo.empty();
+  const bool other_work = n_passes_run > 0 || !todo.empty() || !use_pack;
   if (witness && b.n_hist && other_work) {
     hipLaunchKernelGGL(walk_kernel, dim3((b.n_hist + 255) / 256), dim3(256), 0, stream, b.n_hist, b.res,
                        (const TraceEnt*)b.trace, b.moves);
     HIPCHK(hipGetLastError());
-    HIPCHK(hipMemcpyAsync(b.h_res.data(), b.res, b.n_hist * sizeof(HistResult), hipMemcpyDeviceToHost, stream));
-    HIPCHK(hipStreamSynchronize(stream));
   }
-  HIPCHK(hipEventDestroy(e0));
-  HIPCHK(hipEventDestroy(e1));
+  if (b.n_hist && (other_work || !(b.n_pack16 + b.n_pack32)))
+    HIPCHK(hipMemcpyAsync(b.h_res, b.res, b.n_hist * sizeof(HistResult), hipMemcpyDeviceToHost, stream));
+  HIPCHK(hipStreamSynchronize(stream));
   for (uint32_t i = 0; i < b.n_hist; ++i) {
     if (b.forced[i]) {
       b.h_res[i] = HistResult{};
@@ -494,8 +544,53 @@ int batch_run(DevBatch& b, hipStream_t stream, uint64_t max_configs, bool witnes
       st.pack16_histories++;
     }
   }
+  b.rc_valid = ro.round_counts;
   st.algo_bytes += b.algo_bytes_inputs;
-  st.total_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+  st.total_ms = (double)(steady_ns() - t0) * 1e-6;
+  return 0;
+}
+
+
+int batch_fetch_moves(DevBatch& b, std::string& err) {
+  if (grow_pinned(reinterpret_cast<uint8_t**>(&b.h_moves), b.h_moves_cap, std::max<uint64_t>(b.moves_cap, 1) * sizeof(uint32_t),
+                  err))
+    return S2LC_EHIP;
+  if (b.moves_cap) HIPCHK(hipMemcpy(b.h_moves, b.moves, b.moves_cap * sizeof(uint32_t), hipMemcpyDeviceToHost));
+  return 0;
+}
+
+namespace {
+// foldRecordHashes through the search kernels' own device routine
+__global__ void fold_kernel(uint32_t n, const uint64_t* seeds, const uint64_t* pool, const uint32_t* offs,
+                            const uint32_t* cnts, uint64_t* out) {
+  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < n) out[i] = fold_hashes_blk(seeds[i], pool + offs[i], cnts[i]);
+}
+}  // namespace
+
+int device_fold(const uint64_t* seeds, const uint64_t* pool, size_t pool_len, const uint32_t* offs, const uint32_t* cnts,
+                size_t n, uint64_t* out, hipStream_t stream, std::string& err) {
+  for (size_t i = 0; i < n; ++i)
+    if ((uint64_t)offs[i] + cnts[i] > pool_len) { err = "fold range outside the pool"; return S2LC_EINVAL; }
+  if (n == 0) return 0;
+  uint8_t* d = nullptr;
+  const size_t o_pool = align256(n * 8), o_offs = align256(o_pool + std::max<size_t>(pool_len, 1) * 8),
+               o_cnts = align256(o_offs + n * 4), o_out = align256(o_cnts + n * 4), total = o_out + n * 8;
+  HIPCHK(hipMalloc(&d, total));
+  hipError_t e = hipMemcpyAsync(d, seeds, n * 8, hipMemcpyHostToDevice, stream);
+  if (e == hipSuccess && pool_len) e = hipMemcpyAsync(d + o_pool, pool, pool_len * 8, hipMemcpyHostToDevice, stream);
+  if (e == hipSuccess) e = hipMemcpyAsync(d + o_offs, offs, n * 4, hipMemcpyHostToDevice, stream);
+  if (e == hipSuccess) e = hipMemcpyAsync(d + o_cnts, cnts, n * 4, hipMemcpyHostToDevice, stream);
+  if (e == hipSuccess) {
+    hipLaunchKernelGGL(fold_kernel, dim3((uint32_t)((n + 255) / 256)), dim3(256), 0, stream, (uint32_t)n,
+                       (const uint64_t*)d, (const uint64_t*)(d + o_pool), (const uint32_t*)(d + o_offs),
+                       (const uint32_t*)(d + o_cnts), (uint64_t*)(d + o_out));
+    e = hipGetLastError();
+  }
+  if (e == hipSuccess) e = hipMemcpyAsync(out, d + o_out, n * 8, hipMemcpyDeviceToHost, stream);
+  if (e == hipSuccess) e = hipStreamSynchronize(stream);
+  (void)hipFree(d);
+  if (e != hipSuccess) { err = std::string("device fold: ") + hipGetErrorString(e); return S2LC_EHIP; }
   return 0;
 }
 

@@ -100,7 +100,28 @@ struct Params {
   uint32_t witness;
   uint32_t n_recs, n_pool, n_res;  // buffer sizes (guard build checks)
   uint32_t win_recs;               // LDS record-window capacity (SHARED mode; 0 = none)
+  uint32_t* rcounts;               // per-round unique configurations at res[h].witness_off (nullable)
+  const unsigned long long* deadline;  // wall_clock64() value after which histories give Unknown (nullable)
 };
+
+// The run's deadline in device wall-clock ticks (written once per run, read by
+// the search kernels; see batch_run).
+__global__ __attribute__((unused)) void deadline_kernel(unsigned long long* d, unsigned long long ticks) { *d = wall_clock64() + ticks; }
+
+// Every history of the batch starts a run undecided (a history that no engine
+// reaches in this run, e.g. after a timeout, must not keep a stale verdict).
+__global__ __attribute__((unused)) void reset_results_kernel(HistResult* res, uint32_t n) {
+  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  HistResult& r = res[i];
+  r.verdict = V_UNKNOWN;
+  r.reason = S2LC_R_NONE;
+  r.rounds = 0;
+  r.has_witness = 0;
+  r.witness_len = 0;
+  r.configs = 0;
+  r.children = 0;
+}
 
 __device__ __forceinline__ uint64_t mix64(uint64_t x) {
   x ^= x >> 33;
@@ -204,6 +225,7 @@ __device__ __forceinline__ int closure(Cfg<KMAX>* c, int K, const RecSrc& src, u
   const State s{c->tail, c->hash, c->tok};
   const bool nowrap = hflags & H_NOWRAP;
   const bool p2 = hflags & H_P2OK;
+  const bool p4 = hflags & H_P4;
   uint32_t pk[NP];
   if constexpr (REG) {
     const uint4* w = reinterpret_cast<const uint4*>(c->cnt);
@@ -264,7 +286,7 @@ __device__ __forceinline__ int closure(Cfg<KMAX>* c, int K, const RecSrc& src, u
     // Final only if nothing changed AND eligibility was judged with the exact minret.
     if (!changed && minret == minret_prev) {
       if (minret == EV_INF) result = CL_COMPLETE;
-      else if (bound == REQ_NONE) result = CL_P4;           // P4: nothing left constrains the state
+      else if (p4 && bound == REQ_NONE) result = CL_P4;     // P4: nothing left constrains the state
       break;
     }
     minret_prev = minret;
@@ -322,7 +344,7 @@ struct __attribute__((aligned(16))) WgState {
   uint32_t wb[KMAX];      // record-window base (count) per chain
   uint32_t h, nstage, nnext, found, overflow, children;
   uint32_t found_parent, found_move, found_p4;
-  uint32_t tb, tleft, witness_ok;
+  uint32_t tb, tleft, witness_ok, timed_out;
   unsigned long long tbase;
   HistDesc hd;
 };
@@ -434,6 +456,14 @@ __global__ __launch_bounds__(BT) void search_kernel(Params p) {
     __syncthreads();
     const HistDesc hd = S.hd;
     const int K = hd.K;
+    if (K > KMAX) {  // the host sizes KMAX to the batch; never taken
+      if (tid == 0) { p.res[h].verdict = V_UNKNOWN; p.res[h].reason = S2LC_R_FRONTIER; }
+      __syncthreads();
+      continue;
+    }
+    const bool idefer = hd.flags & H_IDEFER;
+    const unsigned long long deadline = p.deadline ? *p.deadline : 0ull;
+    uint32_t* const rc = p.rcounts ? p.rcounts + p.res[h].witness_off : nullptr;
     const int nw = (K + 7) >> 3;
     const OpRec* __restrict__ recs = p.recs;
     // cs[0..K] are the chain starts (cs[K] = end); cs[K+1..KMAX] hold the index
@@ -472,6 +502,11 @@ __global__ __launch_bounds__(BT) void search_kernel(Params p) {
         deep_trace = rounds > 0 ? nxt[0].trace : TRACE_NONE;
         deep_len = rounds > 0 ? rounds - 1 : 0;
         break;
+      }
+      if (deadline) {  // one lane reads the clock: waves of a workgroup may see different values
+        if (tid == 0) S.timed_out = wall_clock64() > deadline ? 1u : 0u;
+        __syncthreads();
+        if (S.timed_out) { verdict = V_UNKNOWN; reason = S2LC_R_TIMEOUT; break; }
       }
       if (tid == 0) S.nnext = 0;
       if (SHARED && W) window_refill<KMAX, BT>(S, win, recs, cur, ncur, K, W, init);
@@ -518,7 +553,7 @@ __global__ __launch_bounds__(BT) void search_kernel(Params p) {
               take_id = false;
             } else {  // indefinite: opt any time; identity only when it holds the minimal return
               take_opt = g;
-              take_id = r.ret_ev == pc->minret && !(g && state_eq(opt, s));
+              take_id = (!idefer || r.ret_ev == pc->minret) && !(g && state_eq(opt, s));
             }
             const int nk = (int)take_opt + (int)take_id;
             if (nk) atomicAdd(&S.children, (uint32_t)nk);
@@ -655,6 +690,7 @@ __global__ __launch_bounds__(BT) void search_kernel(Params p) {
       PROF_STAMP(5);
       configs += nn;
       rounds += init ? 0u : 1u;
+      if (rc && tid == 0) rc[rounds] = nn;
       if (S.found) { verdict = V_OK; reason = 0; break; }
       if (p.max_configs && configs > p.max_configs) { verdict = V_UNKNOWN; reason = S2LC_R_BUDGET; break; }
       C* t = cur; cur = nxt; nxt = t;
@@ -686,7 +722,7 @@ __global__ __launch_bounds__(BT) void search_kernel(Params p) {
 // and writes the move list in order. Ok: the completing move after the path
 // to its parent. Illegal: the path to a configuration of the deepest
 // non-empty round (the partial linearization the visualization shows).
-__global__ void walk_kernel(uint32_t n, HistResult* res, const TraceEnt* trace, uint32_t* moves) {
+__global__ __attribute__((unused)) void walk_kernel(uint32_t n, HistResult* res, const TraceEnt* trace, uint32_t* moves) {
   const uint32_t h = blockIdx.x * blockDim.x + threadIdx.x;
   if (h >= n) return;
   HistResult r = res[h];

@@ -31,6 +31,17 @@ CONFIGS = {
                  **{**BASE, "p_indefinite": 0.015}),
     "H212": dict(workflow=WF_REGULAR, num_clients=32, ops_per_client=1000, seed=6, max_client_ids=1 << 20,
                  **{**BASE, "p_indefinite": 0.02}),
+    # 32 < K <= 128 (the workgroup-per-history engine, search_kernel): many
+    # clients with the collector's client-id cap (ids start above 20, so a
+    # client stops at its first indefinite failure); porcupine's DFS does not
+    # finish on them, the CPU reduced search does in milliseconds
+    "H48": dict(workflow=WF_REGULAR, num_clients=48, ops_per_client=200, seed=7, **{**BASE, "p_indefinite": 0.003}),
+    "H48bad": dict(workflow=WF_REGULAR, num_clients=48, ops_per_client=200, seed=7, violation=VIOL_READ_HASH,
+                   **{**BASE, "p_indefinite": 0.003}),
+    "H96": dict(workflow=WF_REGULAR, num_clients=96, ops_per_client=80, seed=3, **BASE),
+    "H100": dict(workflow=WF_REGULAR, num_clients=100, ops_per_client=60, seed=9, **{**BASE, "p_indefinite": 0.003}),
+    "H120m": dict(workflow=WF_MATCH_SEQ_NUM, num_clients=120, ops_per_client=50, seed=9,
+                  **{**BASE, "p_indefinite": 0.003}),
     # the round-1 C5 (client-id cap 20: clients stop at their first indefinite failure)
     "C5capped": dict(workflow=WF_REGULAR, num_clients=32, ops_per_client=1000, seed=5,
                      **{**BASE, "p_indefinite": 0.002}),

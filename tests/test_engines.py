@@ -1,0 +1,280 @@
+"""GPU parity of every search engine, forced route by route, and of the search
+itself (per-round configuration counts) under reduction ablations.
+
+The checker picks an engine per history (packed lane groups for K <= 32, one
+workgroup per history for K <= 128, the device-wide level search above), so
+the default route never sends the small parity cases through search_kernel.
+Here the context forces each engine (s2lc_opts.engine) over the same cases:
+
+  ENGINE_WORKGROUP      search_kernel, LDS pass then HBM-slab pass
+  ENGINE_WORKGROUP_HBM  search_kernel, HBM-slab pass only
+  ENGINE_LEVEL          lv_expand / lv_close / lv_insert
+
+Round counts: with the same reductions on, the set of unique configurations
+of every round is fixed (closure is canonical, dedupe exact), so the GPU's
+count per completed round must equal oracle/reduced.c's. That pins the
+search, not only the final verdict. Reductions are switched off one at a
+time (s2lc_opts.reductions_off) on histories where the unreduced search stays
+small; the hard histories are compared against committed counts
+(tests/golden/hard_round_counts.json, tests/golden/make_round_counts.py).
+"""
+import os
+import random
+import subprocess
+
+import pytest
+
+import oracle as orc
+import s2_verification_amd as s2
+from helpers import GOLDEN, config_digest, from_s2_events, golden, random_history, to_s2_events
+
+pytestmark = pytest.mark.gpu
+
+ENGINES = {"auto": s2.ENGINE_AUTO, "workgroup": s2.ENGINE_WORKGROUP, "workgroup_hbm": s2.ENGINE_WORKGROUP_HBM,
+           "level": s2.ENGINE_LEVEL}
+_checkers = {}
+
+
+def checker_for(engine=s2.ENGINE_AUTO, red=0, rc=False):
+    key = (engine, red, rc)
+    if key not in _checkers:
+        _checkers[key] = s2.Checker(engine=engine, reductions_off=red, round_counts=rc)
+    return _checkers[key]
+
+
+def run(c, hs):
+    b = c.batch(hs)
+    res = b.check()
+    return b, res
+
+
+@pytest.mark.parametrize("engine", list(ENGINES))
+def test_engine_reference_cases(engine):
+    hs, expect = [], []
+    for c in golden("reference_cases.json")["cases"]:
+        hs.append(s2.History.from_events(to_s2_events(c["events"])))
+        expect.append(c["expected"])
+    _, res = run(checker_for(ENGINES[engine]), hs)
+    for h, r, e in zip(hs, res, expect):
+        assert r.verdict == e, (engine, r, e)
+        if r.verdict == s2.Ok:
+            assert r.witness is not None and len(r.witness) == h.info()["n_ops"]
+
+
+@pytest.mark.parametrize("engine", list(ENGINES))
+def test_engine_random_small_vs_brute_and_wgl(engine):
+    rng = random.Random(7)
+    hs, expect = [], []
+    for _ in range(400):
+        n = rng.randint(1, 9)
+        ev = random_history(rng, n, n_clients=rng.randint(1, 4))
+        b, _ = orc.check_brute(ev)
+        w, _ = orc.check_wgl(ev)
+        assert b == w
+        hs.append(s2.History.from_events(to_s2_events(ev)))
+        expect.append(w)
+    bt, res = run(checker_for(ENGINES[engine]), hs)
+    assert [r.verdict for r in res] == expect, engine
+    assert all(r.witness is not None for r in res if r.verdict == s2.Ok)
+    if engine == "level":
+        assert bt.stats()["level_histories"] == len(hs)
+
+
+@pytest.mark.parametrize("engine", ["workgroup", "workgroup_hbm", "level"])
+@pytest.mark.parametrize("wf", [s2.WF_REGULAR, s2.WF_MATCH_SEQ_NUM, s2.WF_FENCING])
+def test_engine_simulated_vs_wgl(engine, wf):
+    viols = [s2.VIOL_NONE, s2.VIOL_READ_HASH, s2.VIOL_TAIL, s2.VIOL_DEFINITE_APPLIED, s2.VIOL_STALE_MSN]
+    hs, expect = [], []
+    for seed in range(30):
+        h = s2.simulate_history(workflow=wf, num_clients=3 + seed % 4, ops_per_client=60, seed=1000 + seed,
+                                violation=viols[seed % len(viols)], p_indefinite=0.03)
+        w, _ = orc.check_wgl(from_s2_events(h.events()), timeout=20.0)
+        if w == "Unknown":
+            continue
+        hs.append(h)
+        expect.append(w)
+    _, res = run(checker_for(ENGINES[engine]), hs)
+    assert [r.verdict for r in res] == expect, (engine, wf)
+
+
+@pytest.mark.parametrize("engine", ["workgroup", "workgroup_hbm", "level"])
+def test_engine_c4_sample_vs_wgl(engine):
+    from s2_verification_amd import workloads as W
+    hs = W.c4_histories(300, first_seed=500)
+    expect = [orc.check_wgl(orc.from_s2lc_numpy(h.events_numpy()))[0] for h in hs]
+    _, res = run(checker_for(ENGINES[engine]), hs)
+    assert [r.verdict for r in res] == expect, engine
+    assert all(r.witness is not None for r in res if r.verdict == s2.Ok)
+
+
+@pytest.mark.parametrize("name", ["H48", "H48bad", "H96", "H100", "H120m"])
+def test_mid_k_histories_take_search_kernel(name):
+    """32 < K <= 128 with the collector's client-id cap: the default route is
+    the workgroup engine (search_kernel), not the packed or level kernels.
+    Porcupine's DFS does not finish; verdict = the CPU reduced search."""
+    from s2_verification_amd import workloads as W
+    h = W.config_history(name)
+    K = h.info()["n_chains"]
+    assert 32 < K <= 128
+    v, _ = orc.check_reduced(orc.from_s2lc_numpy(h.events_numpy()))
+    b, res = run(checker_for(), [h])
+    r = res[0]
+    st = b.stats()
+    assert st["pack16_histories"] == 0 and st["level_histories"] == 0, st
+    assert r.verdict == v, (name, r)
+    if r.verdict == s2.Ok:
+        assert r.witness is not None and len(r.witness) == h.info()["n_ops"]
+
+
+ABLATIONS = {"all_on": 0, "no_p1": s2.RED_P1, "no_p2": s2.RED_P2, "no_p4": s2.RED_P4, "no_idefer": s2.RED_IDEFER}
+# histories whose search stays small with any one reduction off (oracle/reduced.c, this container: < 2 s each)
+ROUND_CASES = ["C1", "C2", "C3", "H48", "H48bad", "H100", "H120m"]
+
+
+def _round_cases():
+    from s2_verification_amd import workloads as W
+    hs = [W.config_history(n) for n in ROUND_CASES]
+    hs += W.c4_histories(40, first_seed=7000)
+    return hs
+
+
+@pytest.mark.parametrize("engine", list(ENGINES))
+@pytest.mark.parametrize("abl", list(ABLATIONS))
+def test_round_counts_match_reduced_search(engine, abl):
+    """Verdict and the unique-configuration count of every completed round
+    equal the CPU reduced search with the same reductions switched off."""
+    red = ABLATIONS[abl]
+    hs = _round_cases()
+    b, res = run(checker_for(ENGINES[engine], red, rc=True), hs)
+    for i, (h, r) in enumerate(zip(hs, res)):
+        v, st = orc.check_reduced(orc.from_s2lc_numpy(h.events_numpy()), reductions_off=red, round_counts=True)
+        assert r.verdict == v, (engine, abl, i, r, v)
+        assert r.rounds == st["rounds"], (engine, abl, i, r.rounds, st["rounds"])
+        got = b.round_counts(i)
+        assert got == st["round_counts"], (engine, abl, i, [k for k, (x, y) in enumerate(zip(got, st["round_counts"]))
+                                                             if x != y][:5])
+
+
+@pytest.mark.parametrize("name,off", [("H174", 0), ("H174", 2), ("H212", 0), ("H212", 2), ("C5bad", 0),
+                                      ("C5bad", 2), ("C5bad", 4)])
+def test_hard_round_counts(name, off):
+    """Hard single histories (> 128 chains, the level search): per-round counts
+    against the committed CPU reduced-search counts."""
+    from s2_verification_amd import workloads as W
+    ref = golden("hard_round_counts.json")[name]
+    assert config_digest(name) == ref["digest"], "simulator output changed: regenerate the fixture"
+    want = ref[str(off)]
+    h = W.config_history(name)
+    b, res = run(checker_for(s2.ENGINE_AUTO, off, rc=True), [h])
+    r = res[0]
+    assert r.verdict == want["verdict"], (name, off, r)
+    assert r.rounds == want["rounds"]
+    got = b.round_counts(0)
+    bad = [k for k, (x, y) in enumerate(zip(got, want["counts"])) if x != y]
+    assert got == want["counts"], (name, off, bad[:5])
+    if r.verdict == s2.Ok:
+        assert r.witness is not None
+
+
+def test_rerun_does_not_reuse_stale_results(monkeypatch):
+    """a batch run twice, where a level-search history ends in
+    Unknown (frontier beyond capacity, forced small with S2LC_LEVEL_SCAP),
+    must give the same results both times and never re-route that history
+    through the workgroup passes."""
+    from s2_verification_amd import workloads as W
+    monkeypatch.setenv("S2LC_LEVEL_SCAP", "128")
+    hs = [W.config_history("H174")] + W.c4_histories(50, first_seed=9000)
+    c = s2.Checker()
+    b = c.batch(hs)
+    r1 = b.check()
+    st1 = b.stats()
+    r2 = b.check()
+    st2 = b.stats()
+    assert r1[0].verdict == s2.Unknown and r1[0].reason == "frontier", r1[0]
+    assert [(r.verdict, r.reason, r.configs_explored) for r in r1] == [(r.verdict, r.reason, r.configs_explored)
+                                                                      for r in r2]
+    assert st1["level_histories"] == st2["level_histories"] == 1
+    assert st2["n_overflow"] == 0
+    expect = [orc.check_wgl(orc.from_s2lc_numpy(h.events_numpy()))[0] for h in hs[1:]]
+    assert [r.verdict for r in r2[1:]] == expect
+
+
+def test_timeout_gives_unknown():
+    """CheckEventsVerbose's timeout (main.go:606 passes 0): past it, Unknown."""
+    from s2_verification_amd import workloads as W
+    h = W.config_history("C5")  # ~0.5 s of level search
+    r = s2.Checker(timeout=0.005).check(h)
+    assert r.verdict == s2.Unknown and r.reason == "timeout", r
+    hs = W.c4_histories(200)
+    res = s2.Checker(timeout=1e-6).check_many(hs)
+    assert all(r.verdict in (s2.Unknown, s2.Ok, s2.Illegal) for r in res)
+    assert any(r.reason == "timeout" for r in res)
+    # no timeout: decided
+    res = s2.Checker(timeout=60).check_many(hs)
+    assert all(r.verdict != s2.Unknown for r in res)
+    v, info = s2.check_events_verbose(None, h, timeout=0.005)
+    assert v == s2.Unknown
+
+
+def test_witness_certificate_failure_is_loud(monkeypatch, tmp_path):
+    """an Ok whose witness fails CPU replay must not pass as Ok
+    (test hook S2LC_FAULT_WITNESS corrupts every witness before certification)."""
+    from s2_verification_amd import workloads as W
+    monkeypatch.setenv("S2LC_FAULT_WITNESS", "1")
+    c = s2.Checker()
+    h = W.config_history("C1")
+    with pytest.raises(s2.S2LCError) as e:
+        c.check(h)
+    assert e.value.status == s2.EWITNESS
+    b = c.batch(W.c4_histories(20))
+    b.run()
+    with pytest.raises(s2.S2LCError) as e:
+        b.results(with_witness=True)
+    assert e.value.status == s2.EWITNESS
+    assert all(r.verdict != s2.Unknown for r in b.results(with_witness=False))
+    p = subprocess.run([s2.CLI_PATH, "-file=" + os.path.join(GOLDEN, "ref_BasicNoConcurrency.jsonl")],
+                       capture_output=True, text=True, timeout=120, cwd=tmp_path, env=dict(os.environ))
+    assert p.returncode == 3 and "failed: witness certification" in p.stderr, p.stderr
+
+
+def test_multi_device_sharded_check_batch():
+    """s2lc_opts.devices: LPT placement over shards (two shards on this one GPU),
+    verdicts gathered in input order, equal to the single-shard run."""
+    from s2_verification_amd import workloads as W
+    hs = W.c4_histories(300, first_seed=1234) + [W.config_history("C2"), W.config_history("H48")]
+    one = s2.Checker().check_many(hs)
+    two = s2.Checker(devices=[0, 0]).check_many(hs)
+    three = s2.Checker(devices=[0, 0, 0]).check_many(hs, as_numpy=True)
+    assert [r.verdict for r in one] == [r.verdict for r in two] == [r.verdict for r in three]
+    assert [r.configs_explored for r in one] == [r.configs_explored for r in two]
+    for a, c in zip(one, three):
+        assert (a.witness is None) == (c.witness is None)
+        if a.witness is not None:
+            assert list(c.witness) == a.witness
+
+
+def test_device_fold_known_answers():
+    """foldRecordHashes on the device (the search kernels' routine) against the
+    reference vectors (main_test.go:15-32) and the python-xxhash golden pairs."""
+    g = golden("chain_hash_vectors.json")
+    c = s2.Checker()
+    seeds = [h for h, _, _ in g["pairs"]] + [h for h, _, _ in g["folds"]]
+    folds = [[r] for _, r, _ in g["pairs"]] + [list(rs) for _, rs, _ in g["folds"]]
+    want = [w for _, _, w in g["pairs"]] + [w for _, _, w in g["folds"]]
+    assert len(g["pairs"]) >= 449 and len(g["folds"]) >= 40
+    assert c.device_fold(seeds, folds) == want
+    # chain over foo, bar, baz from seed 0 (main_test.go:15-32)
+    ref = g["reference"]
+    x = ref["xxh3"]
+    assert c.device_fold([0, 0, 0], [x[:1], x[:2], x]) == [ref["h1"], ref["h2"], ref["h3"]]
+
+
+def test_check_reuses_scratch_and_matches_batch():
+    """s2lc_check through the context's scratch batch, called repeatedly with
+    histories of growing and shrinking size, gives the batch path's verdicts."""
+    from s2_verification_amd import workloads as W
+    c = s2.Checker()
+    hs = [W.config_history(n) for n in ("C1", "C3", "C2", "H48", "C1")] + W.c4_histories(20)
+    want = [r.verdict for r in s2.Checker().check_batch(hs)]
+    got = [c.check(h).verdict for h in hs]
+    assert got == want

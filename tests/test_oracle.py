@@ -89,3 +89,39 @@ def test_reduced_search_matches_wgl():
                                     violation=seed % 5, p_indefinite=0.03)
             ea = orc.from_s2lc_numpy(h.events_numpy())
             assert orc.check_reduced(ea)[0] == orc.check_wgl(ea)[0]
+
+
+def test_reduced_search_ablations_agree_with_wgl():
+    """oracle/reduced.c with each verdict-exact reduction switched off (the
+    product's RED_* bits) gives porcupine's verdict (WGL restatement) on the
+    bench workload and on random small histories, and its per-round counts
+    account for every configuration it inserted."""
+    import random
+
+    from helpers import random_history
+    from s2_verification_amd import workloads as W
+    hs = [orc.from_s2lc_numpy(h.events_numpy()) for h in W.c4_histories(120, first_seed=4000)]
+    rng = random.Random(3)
+    hs += [random_history(rng, rng.randint(1, 9), n_clients=rng.randint(1, 4)) for _ in range(300)]
+    for ev in hs:
+        w, _ = orc.check_wgl(ev)
+        for off in range(16):
+            v, st = orc.check_reduced(ev, reductions_off=off, round_counts=True)
+            assert v == w, (off, v, w)
+            assert len(st["round_counts"]) == st["rounds"]
+            if v == "Illegal":  # every round completed: the counts are all the configurations (+ round 0)
+                assert sum(st["round_counts"]) == st["configs"] + (1 if st["rounds"] else 0)
+
+
+def test_reduced_p2_only_prunes():
+    """P2 (a minimal read at the current tail with another hash is dead) only
+    removes configurations: per-round counts with it on never exceed those
+    with it off, and the rounds are the same (hard fixtures, committed)."""
+    from helpers import golden
+    g = golden("hard_round_counts.json")
+    for name in ("H174", "H212", "C5bad"):
+        on, off = g[name]["0"], g[name]["2"]
+        assert on["verdict"] == off["verdict"]
+        if on["verdict"] == "Ok":
+            assert on["rounds"] == off["rounds"]
+        assert all(a <= b for a, b in zip(on["counts"], off["counts"]))
