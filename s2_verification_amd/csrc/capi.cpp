@@ -780,7 +780,7 @@ int s2lc_dist_expand(s2lc_dist* x, uint64_t* counts, int32_t* found) {
 }
 
 int s2lc_dist_pack(s2lc_dist* x, void* send, const uint64_t* counts) {
-  if (!x || !counts || (!send && x->d.nstage)) return S2LC_EINVAL;
+  if (!x || !counts) return S2LC_EINVAL;
   return dist_pack(x->d, (uint8_t*)send, counts, x->ctx->err);
 }
 

@@ -1,11 +1,19 @@
 // level.hip — host driver of the device-wide level-synchronous search of one
 // history (kernels in level_dev.h). Called by batch_run for histories with
 // more than 128 chains and for histories whose frontier outgrew the
-// per-workgroup passes. One round = lv_expand -> lv_close -> lv_insert, then
-// one 64-byte control read-back decides: found (Ok), empty (Illegal), or the
-// next round. A round whose children or staged configurations exceed the
-// device buffers is re-run over halves of its frontier.
+// per-workgroup passes. A round is lv_round (expand + close + stage) then
+// lv_insert (dedupe; its last block closes the round on the device).
+//
+// Rounds are enqueued in batches with no host synchronization in between:
+// every kernel reads the frontier size and the run state from device memory,
+// and the kernels of a finished search return immediately. The host reads the
+// host-mapped run state once per batch. Narrow frontiers use long batches
+// (the round latency is then a few kernel launches); wide frontiers one round
+// per batch, so the launch grids follow the frontier. A round whose staged
+// configurations exceed the device buffers is re-run over chunks of its
+// frontier (host-driven).
 #include <hip/hip_runtime.h>
+#include <stdio.h>
 #include <stdlib.h>
 #include <string.h>
 
@@ -30,31 +38,43 @@ namespace {
     }                                                                    \
   } while (0)
 
-size_t lv_cfg_bytes(uint32_t kmax) { return 48 + 2 * (size_t)kmax; }
+enum LvKernel { LK_ROUND = 0, LK_INSERT, LK_BUCKET, LK_SCATTER, LK_KEEP, LK_GATHER, LK_CLOSE };
 
-template <int KMAX>
+size_t lv_cfg_bytes(uint32_t nq) { return 48 + 128 * (size_t)nq; }
+
+// a host-driven round's bookkeeping, after its last chunk (one thread)
+__global__ void lv_close_kernel(LvParams p) { lv_close_round(p); }
+
+template <int NQ>
 hipError_t lv_launch(int which, uint32_t grid, const LvParams& p, hipStream_t st) {
-  if (which == 0) hipLaunchKernelGGL(lv_expand<KMAX>, dim3(grid), dim3(LV_BLOCK), 0, st, p);
-  else if (which == 1) hipLaunchKernelGGL(lv_close<KMAX>, dim3(grid), dim3(LV_BLOCK), 0, st, p);
-  else if (which == 2) hipLaunchKernelGGL(lv_insert<KMAX>, dim3(grid), dim3(LV_BLOCK), 0, st, p);
-  else if (which == 3) hipLaunchKernelGGL(lv_bucket<KMAX>, dim3(grid), dim3(LV_BLOCK), 0, st, p);
-  else if (which == 4) hipLaunchKernelGGL(lv_scatter<KMAX>, dim3(grid), dim3(LV_BLOCK), 0, st, p);
-  else if (which == 5) hipLaunchKernelGGL(lv_keep<KMAX>, dim3(grid), dim3(LV_BLOCK), 0, st, p, (uint32_t)(p.tgid >> 29));
-  else hipLaunchKernelGGL(lv_gather_frontier<KMAX>, dim3(grid), dim3(LV_BLOCK), 0, st, p);
+  switch (which) {
+    case LK_ROUND: hipLaunchKernelGGL(lv_round<NQ>, dim3(grid), dim3(LV_BLOCK), 0, st, p); break;
+    case LK_INSERT: hipLaunchKernelGGL(lv_insert<NQ>, dim3(grid), dim3(LV_BLOCK), 0, st, p); break;
+    case LK_BUCKET: hipLaunchKernelGGL(lv_bucket<NQ>, dim3(grid), dim3(LV_BLOCK), 0, st, p); break;
+    case LK_SCATTER: hipLaunchKernelGGL(lv_scatter<NQ>, dim3(grid), dim3(LV_BLOCK), 0, st, p); break;
+    case LK_KEEP: hipLaunchKernelGGL(lv_keep<NQ>, dim3(grid), dim3(LV_BLOCK), 0, st, p, (uint32_t)(p.tgid >> 29)); break;
+    case LK_GATHER: hipLaunchKernelGGL(lv_gather_frontier<NQ>, dim3(grid), dim3(LV_BLOCK), 0, st, p); break;
+    default: hipLaunchKernelGGL(lv_close_kernel, dim3(1), dim3(1), 0, st, p); break;
+  }
   return hipGetLastError();
 }
 
-hipError_t lv_dispatch(uint32_t kmax, int which, uint32_t grid, const LvParams& p, hipStream_t st) {
-  switch (kmax) {
-    case 64: return lv_launch<64>(which, grid, p, st);
-    case 128: return lv_launch<128>(which, grid, p, st);
-    case 256: return lv_launch<256>(which, grid, p, st);
-    default: return lv_launch<512>(which, grid, p, st);
+hipError_t lv_dispatch(uint32_t nq, int which, uint32_t grid, const LvParams& p, hipStream_t st) {
+  grid = std::max<uint32_t>(grid, 1);
+  switch (nq) {
+    case 1: return lv_launch<1>(which, grid, p, st);
+    case 2: return lv_launch<2>(which, grid, p, st);
+    case 3: return lv_launch<3>(which, grid, p, st);
+    case 4: return lv_launch<4>(which, grid, p, st);
+    case 5: return lv_launch<5>(which, grid, p, st);
+    case 6: return lv_launch<6>(which, grid, p, st);
+    case 7: return lv_launch<7>(which, grid, p, st);
+    default: return lv_launch<8>(which, grid, p, st);
   }
 }
 
 int lv_ensure(void** p, size_t& cap, size_t need, std::string& err) {
-  if (need <= cap) return 0;
+  if (need <= cap && *p) return 0;
   if (*p) (void)hipFree(*p);
   *p = nullptr;
   cap = 0;
@@ -63,225 +83,283 @@ int lv_ensure(void** p, size_t& cap, size_t need, std::string& err) {
   return 0;
 }
 
+int n_cus(std::string& err) {
+  int dev = 0, n = 256;
+  LVCHK(hipGetDevice(&dev));
+  (void)hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev);
+  return n;
+}
+
+// persistent grids of lv_round<NQ> / lv_insert<NQ>: the blocks the chip holds at once
+template <int NQ>
+int lv_grids_t(LevelBufs& L, std::string& err) {
+  const int n_cu = n_cus(err);
+  int br = 1, bi = 1;
+  LVCHK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&br, lv_round<NQ>, LV_BLOCK, 0));
+  LVCHK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&bi, lv_insert<NQ>, LV_BLOCK, 0));
+  L.grid_round = (uint32_t)(std::max(1, br) * n_cu);
+  L.grid_insert = (uint32_t)(std::max(1, bi) * n_cu);
+  L.grid_nq = (uint32_t)NQ;
+  return 0;
+}
+
+int lv_grids(LevelBufs& L, uint32_t nq, std::string& err) {
+  if (L.grid_nq == nq) return 0;
+  switch (nq) {
+    case 1: return lv_grids_t<1>(L, err);
+    case 2: return lv_grids_t<2>(L, err);
+    case 3: return lv_grids_t<3>(L, err);
+    case 4: return lv_grids_t<4>(L, err);
+    case 5: return lv_grids_t<5>(L, err);
+    case 6: return lv_grids_t<6>(L, err);
+    case 7: return lv_grids_t<7>(L, err);
+    default: return lv_grids_t<8>(L, err);
+  }
+}
+
 }  // namespace
 
-uint32_t level_kmax(uint32_t K) { return K <= 64 ? 64 : K <= 128 ? 128 : K <= 256 ? 256 : 512; }
+uint32_t level_nq(uint32_t K) { return std::max<uint32_t>(1, std::min<uint32_t>(8, (K + 63) / 64)); }
 
-int level_buffers(DevBatch& b, uint32_t kmax, std::string& err) {
+int level_buffers(DevBatch& b, uint32_t nq, std::string& err) {
   LevelBufs& L = b.lv;
-  if (L.kmax >= kmax && L.ctl) return 0;
+  if (L.nq >= nq && L.ctl) return 0;
   size_t free_b = 0, total_b = 0;
   LVCHK(hipMemGetInfo(&free_b, &total_b));
-  // a quarter of free HBM (at most 48 GiB): two staging arrays + index
-  // lists + table, and the children array
+  // a quarter of free HBM (at most 48 GiB): two staging arrays, their index
+  // lists and the table (2 slots per staged configuration)
   const size_t budget = std::min<size_t>(free_b / 4, 48ull << 30);
-  const size_t cb = lv_cfg_bytes(kmax);
-  uint64_t scap = std::min<uint64_t>(1ull << 24, (uint64_t)(budget * 6 / 10) / (2 * cb + 2 * 4 + 2 * 8));
-  uint64_t ccap = std::min<uint64_t>(1ull << 26, (uint64_t)(budget * 3 / 10) / sizeof(LChild));
-  scap = std::max<uint64_t>(scap, 1024);
-  ccap = std::max<uint64_t>(ccap, 4096);
+  const size_t cb = lv_cfg_bytes(8);  // sized for the widest layout: reused by every history
+  uint64_t scap = std::min<uint64_t>(1ull << 25, (uint64_t)budget / (2 * cb + 2 * 4 + 4 * 8));
+  scap = std::max<uint64_t>(scap, 64 * LV_STRIPES);
   // S2LC_LEVEL_SCAP (tests): a small staging capacity, to reach the
   // frontier-overflow paths with small histories
   if (const char* e = getenv("S2LC_LEVEL_SCAP")) {
     const uint64_t v = strtoull(e, nullptr, 10);
-    if (v >= 64) scap = std::min<uint64_t>(scap, v);
+    if (v >= LV_STRIPES) scap = std::min<uint64_t>(scap, v);
   }
+  scap -= scap % LV_STRIPES;  // whole stripes
   uint64_t ht = 1024;
   while (ht < 2 * scap) ht <<= 1;
-  if (lv_ensure((void**)&L.child, L.child_bytes, ccap * sizeof(LChild), err)) return S2LC_EHIP;
   for (int i = 0; i < 2; ++i) {
     if (lv_ensure((void**)&L.stg[i], L.stg_bytes[i], scap * cb, err)) return S2LC_EHIP;
     if (lv_ensure((void**)&L.idx[i], L.idx_bytes[i], scap * sizeof(uint32_t), err)) return S2LC_EHIP;
   }
   if (lv_ensure((void**)&L.ht, L.ht_bytes, ht * 8, err)) return S2LC_EHIP;
-  if (!L.ctl) LVCHK(hipMalloc(&L.ctl, 2 * sizeof(LvCtl)));  // double buffered by round
+  if (!L.ctl) LVCHK(hipMalloc(&L.ctl, 2 * sizeof(LvCtl)));
+  if (!L.run) LVCHK(hipMalloc(&L.run, sizeof(LvRun)));
+  if (!L.h_run) LVCHK(hipHostMalloc(&L.h_run, sizeof(LvRun), hipHostMallocMapped));
   if (!L.h_ctl) LVCHK(hipHostMalloc(&L.h_ctl, sizeof(LvCtl), hipHostMallocDefault));
+  for (hipEvent_t& e : L.ev)
+    if (!e) LVCHK(hipEventCreate(&e));
   LVCHK(hipMemset(L.ht, 0xFF, ht * 8));
-  L.kmax = kmax;
+  L.nq = 8;
   L.scap = (uint32_t)scap;
-  L.ccap = (uint32_t)ccap;
   L.ht_mask = (uint32_t)(ht - 1);
   return 0;
 }
 
 void level_release(DevBatch& b) {
   LevelBufs& L = b.lv;
-  void* ptrs[] = {L.child, L.stg[0], L.stg[1], L.idx[0], L.idx[1], L.ht, L.ctl};
+  void* ptrs[] = {L.stg[0], L.stg[1], L.idx[0], L.idx[1], L.ht, L.ctl, L.run};
   for (void* q : ptrs) if (q) (void)hipFree(q);
+  if (L.h_run) (void)hipHostFree(L.h_run);
   if (L.h_ctl) (void)hipHostFree(L.h_ctl);
+  for (hipEvent_t e : L.ev) if (e) (void)hipEventDestroy(e);
   L = LevelBufs{};
 }
 
 int level_search(DevBatch& b, uint32_t h, hipStream_t st, const RunOpts& ro, int64_t deadline_ns, LevelStats& ls,
                  std::string& err) {
-  const uint64_t max_configs = ro.max_configs;
-  const bool witness = ro.witness;
-  uint32_t* const rc = ro.round_counts && !b.h_rcounts.empty() ? b.h_rcounts.data() + b.h_moves_off[h] : nullptr;
   const HistDesc& hd = b.h_hist[h];
   const uint32_t K = hd.K;
-  const uint32_t kmax = level_kmax(K);
-  if (level_buffers(b, kmax, err)) return S2LC_EHIP;
+  const uint32_t nq = level_nq(K);
+  if (level_buffers(b, nq, err)) return S2LC_EHIP;
   LevelBufs& L = b.lv;
-  LvCtl* hc = reinterpret_cast<LvCtl*>(L.h_ctl);
-  int dev = 0;
-  LVCHK(hipGetDevice(&dev));
-  int n_cu = 256;
-  (void)hipDeviceGetAttribute(&n_cu, hipDeviceAttributeMultiprocessorCount, dev);
-  const uint32_t max_grid = (uint32_t)n_cu * 8;
+  if (lv_grids(L, nq, err)) return S2LC_EHIP;
+  LvRun* hr = reinterpret_cast<LvRun*>(L.h_run);
+  LvRun* d_pub = nullptr;  // device view of the host-mapped mirror
+  LVCHK(hipHostGetDevicePointer((void**)&d_pub, hr, 0));
+  LvRun* const run = reinterpret_cast<LvRun*>(L.run);
+  LvCtl* const ctl = reinterpret_cast<LvCtl*>(L.ctl);
 
   // trace entries continue after what earlier passes / histories used
   unsigned long long tb0 = 0;
-  if (witness && b.trace) {
+  if (ro.witness && b.trace) {
     LVCHK(hipMemcpyAsync(&tb0, b.trace_head, sizeof tb0, hipMemcpyDeviceToHost, st));
     LVCHK(hipStreamSynchronize(st));
   }
-  bool wit = witness && b.trace != nullptr;
-
-  LvCtl* d_hc = nullptr;  // device view of the host-mapped control mirror
-  LVCHK(hipHostGetDevicePointer((void**)&d_hc, hc, 0));
-  LVCHK(hipMemsetAsync(L.ctl, 0, 2 * sizeof(LvCtl), st));
+  const bool wit0 = ro.witness && b.trace != nullptr && tb0 + L.scap <= b.trace_cap;
 
   LvParams p;
   memset(&p, 0, sizeof p);
   p.recs = b.recs; p.pool = b.pool; p.cs = b.chain_start + hd.cs_base; p.K = K; p.hflags = hd.flags;
-  p.child = reinterpret_cast<LChild*>(L.child); p.ccap = L.ccap; p.scap = L.scap; p.ht = L.ht; p.ht_mask = L.ht_mask;
-  p.trace = b.trace; p.ctl = reinterpret_cast<LvCtl*>(L.ctl);
+  p.scap = L.scap; p.scs = L.scap / LV_STRIPES; p.ht = L.ht; p.ht_mask = L.ht_mask;
+  p.trace = b.trace; p.trace_cap = b.trace_cap;
+  p.run = run; p.publish = d_pub; p.close_round = 1; p.publish_always = 1;
+  p.rcounts = ro.round_counts ? b.rcounts + b.h_moves_off[h] : nullptr;
 
-  hipEvent_t e0, e1;
-  LVCHK(hipEventCreate(&e0));
-  LVCHK(hipEventCreate(&e1));
-  LVCHK(hipEventRecord(e0, st));
-
-  // round 0: the initial configuration as the only child, closed + inserted
-  memset(hc, 0, sizeof(LvCtl));
-  hc->nchild = 1;
-  const LChild c0{0, 0, 0, LV_NONE, LV_NONE, 0};
-  LVCHK(hipMemcpyAsync(L.child, &c0, sizeof c0, hipMemcpyHostToDevice, st));
-  LVCHK(hipMemcpyAsync(L.ctl, hc, sizeof(LvCtl), hipMemcpyHostToDevice, st));
-  int cur = 0;  // round r stages into stg[cur ^ 1]; its frontier is stg[cur]
-  p.cur = L.stg[cur]; p.cur_idx = L.idx[cur];
-  p.stg = L.stg[cur ^ 1]; p.nxt_idx = L.idx[cur ^ 1];
-  p.tbase = (uint32_t)tb0; p.witness = wit ? 1u : 0u;
-  if (wit && tb0 + 1 > b.trace_cap) { wit = false; p.witness = 0; }
-  LVCHK(lv_dispatch(kmax, 1, 1, p, st));
-  LVCHK(lv_dispatch(kmax, 2, 1, p, st));
-  LVCHK(hipMemcpyAsync(hc, L.ctl, sizeof(LvCtl), hipMemcpyDeviceToHost, st));
+#ifdef S2LC_PROF
+  unsigned long long* d_prof = nullptr;
+  LVCHK(hipMalloc(&d_prof, 16 * sizeof(unsigned long long)));
+  LVCHK(hipMemset(d_prof, 0, 16 * sizeof(unsigned long long)));
+  p.prof = d_prof;
+#endif
+  LVCHK(hipEventRecord(L.ev[0], st));
+  memset(hr, 0, sizeof(LvRun));
+  LVCHK(hipMemsetAsync(L.ctl, 0, 2 * sizeof(LvCtl), st));
+  hipLaunchKernelGGL(lv_run_init, dim3(1), dim3(1), 0, st, run, tb0, wit0 ? 1u : 0u,
+                     (unsigned long long)ro.max_configs);
+  LVCHK(hipGetLastError());
+  // round 0: the closed initial configuration, staged into stg[0]
+  auto set_round = [&](uint32_t r) {
+    const int w = (int)(r & 1), pr = (int)((r + 1) & 1);  // round r stages into w; its frontier is in pr
+    p.round = r;
+    p.cur = L.stg[pr]; p.cur_idx = L.idx[pr];
+    p.stg = L.stg[w]; p.nxt_idx = L.idx[w];
+    p.ctl = ctl + w; p.ctl_next = ctl + pr;
+  };
+  set_round(0);
+  p.init = 1; p.f0 = 0; p.f1 = 1; p.clear_slots = 0;
+  LVCHK(lv_dispatch(nq, LK_ROUND, 1, p, st));
+  LVCHK(lv_dispatch(nq, LK_INSERT, 1, p, st));
   LVCHK(hipStreamSynchronize(st));
+  p.init = 0;
 
-  uint64_t configs = 0, children = 0, tnext = tb0;
-  uint32_t rounds = 0, max_frontier = 0;
-  uint32_t verdict = V_ILLEGAL, reason = S2LC_R_SEARCH_EXHAUSTED;
-  uint32_t deep_trace = TRACE_NONE, deep_len = 0;
-  for (;;) {
-    if (hc->found) { verdict = V_OK; reason = 0; break; }
-    const uint32_t nf = hc->nnext;
-    if (rc) rc[rounds] = nf;
-    if (nf == 0) {
-      verdict = V_ILLEGAL; reason = S2LC_R_SEARCH_EXHAUSTED;
-      if (rounds > 0 && p.witness) {
-        // a configuration of the deepest non-empty round (the input of the last one)
-        uint32_t k = 0;
-        LVCHK(hipMemcpy(&k, L.idx[cur], sizeof k, hipMemcpyDeviceToHost));
-        LVCHK(hipMemcpy(&deep_trace, L.stg[cur] + (size_t)k * lv_cfg_bytes(kmax) + 40, sizeof deep_trace,
-                        hipMemcpyDeviceToHost));  // LCfg::trace
-        deep_len = rounds - 1;
-      }
-      break;
+  uint32_t next_round = 1;         // first round not yet enqueued
+  uint32_t nf_last = hr->nf;        // frontier size at the last sync
+  bool timed_out = false;
+  uint32_t syncs = 1;
+  while (hr->done == LVR_RUNNING) {
+    if (deadline_ns && steady_ns() > deadline_ns) { timed_out = true; break; }
+    // batch length from the last known frontier; the kernels are persistent
+    // (grid = what the chip holds at once) and size their work on the device
+    const bool narrow = nf_last < 4096;
+    const uint32_t batch = narrow ? 16 : 1;
+    const uint32_t g_round = L.grid_round;
+    // lv_insert's last block closes the round: its done-counter atomics grow
+    // with the grid (~11 ns each), so narrow rounds use a small grid
+    const uint32_t g_ins = narrow ? std::min<uint32_t>(L.grid_insert, 128) : L.grid_insert;
+    p.f0 = 0; p.f1 = LV_NONE; p.clear_slots = 1;
+    for (uint32_t k = 0; k < batch; ++k) {
+      set_round(next_round + k);
+      p.publish_always = k + 1 == batch;  // the host reads the state after the batch
+      LVCHK(lv_dispatch(nq, LK_ROUND, g_round, p, st));
+      LVCHK(lv_dispatch(nq, LK_INSERT, g_ins, p, st));
     }
-    configs += nf;
-    max_frontier = std::max(max_frontier, nf);
-    if (p.witness) tnext += nf;
-    if (max_configs && configs > max_configs) { verdict = V_UNKNOWN; reason = S2LC_R_BUDGET; break; }
-    if (deadline_ns && steady_ns() > deadline_ns) { verdict = V_UNKNOWN; reason = S2LC_R_TIMEOUT; break; }
-    cur ^= 1;
-    p.cur = L.stg[cur]; p.cur_idx = L.idx[cur];
-    p.stg = L.stg[cur ^ 1]; p.nxt_idx = L.idx[cur ^ 1];
-    p.clear_slots = 1;
-    if (wit && tnext + L.scap > b.trace_cap) wit = false;
-    p.witness = wit ? 1u : 0u;
-    p.tbase = (uint32_t)tnext;
-    ++rounds;
-    // one round, in frontier chunks (normally one). Round r uses control
-    // block r & 1, which round r-1's lv_expand zeroed, and lv_insert publishes
-    // it to the host-mapped mirror hc: the single-chunk round needs no copies.
-    LvCtl* const ctl_r = reinterpret_cast<LvCtl*>(L.ctl) + (rounds & 1);
-    p.ctl = ctl_r;
-    p.ctl_next = reinterpret_cast<LvCtl*>(L.ctl) + ((rounds + 1) & 1);
-    p.publish = d_hc;
-    uint32_t f0 = 0, chunk = nf, st_lo = 0, nn_lo = 0;
-    bool stop = false;
-    bool first = true;
-    while (f0 < nf) {
-      const uint32_t f1 = (uint32_t)std::min<uint64_t>(nf, (uint64_t)f0 + chunk);
-      if (!first) {
-        memset(hc, 0, sizeof(LvCtl));
-        hc->nchild = 0; hc->nstage = st_lo; hc->nnext = nn_lo; hc->overflow = 0;
-        LVCHK(hipMemcpyAsync(ctl_r, hc, sizeof(LvCtl), hipMemcpyHostToDevice, st));
+    p.publish_always = 1;
+    next_round += batch;
+    LVCHK(hipStreamSynchronize(st));
+    ++syncs;
+    if (hr->done == LVR_OVERFLOW) {
+      // round r overflowed the staging array: its frontier (stg[(r+1)&1]) is
+      // intact; re-run it host-driven over halves of the frontier
+      const uint32_t r = hr->round + 1;
+      const uint32_t nf = hr->nf;
+      LvRun cont = *hr;
+      cont.done = LVR_RUNNING;
+      LVCHK(hipMemcpyAsync(run, &cont, sizeof cont, hipMemcpyHostToDevice, st));
+      set_round(r);
+      p.clear_slots = 0;  // a chunk must not break the probe chains of earlier chunks' entries
+      p.close_round = 0;
+      uint32_t f0 = 0, chunk = nf;
+      LvCtl* hc = reinterpret_cast<LvCtl*>(L.h_ctl);
+      LvCtl snap;  // the counters before the current chunk (restored when it overflows)
+      memset(&snap, 0, sizeof snap);
+      bool stop = false;
+      while (f0 < nf) {
+        const uint32_t f1 = (uint32_t)std::min<uint64_t>(nf, (uint64_t)f0 + chunk);
+        LVCHK(hipMemcpyAsync(p.ctl, &snap, sizeof(LvCtl), hipMemcpyHostToDevice, st));
+        p.f0 = f0; p.f1 = f1;
+        LVCHK(lv_dispatch(nq, LK_ROUND, L.grid_round, p, st));
+        LVCHK(lv_dispatch(nq, LK_INSERT, L.grid_insert, p, st));
+        LVCHK(hipMemcpyAsync(hc, p.ctl, sizeof(LvCtl), hipMemcpyDeviceToHost, st));
+        LVCHK(hipStreamSynchronize(st));
+        ++syncs;
+        if (hc->found) break;
+        if (hc->overflow) {
+          if (f1 - f0 == 1) { stop = true; break; }
+          chunk = std::max<uint32_t>(1, (f1 - f0) / 2);
+          ++ls.chunk_retries;
+          continue;
+        }
+        // this chunk's staging is inserted: the next chunk inserts from here on
+        snap = *hc;
+        for (int s_ = 0; s_ < LV_STRIPES; ++s_) snap.lo[s_] = std::min(snap.cnt[16 * s_], p.scs);
+        snap.done_blocks = 0;
+        f0 = f1;
       }
-      first = false;
-      p.f0 = f0; p.f1 = f1; p.st_lo = st_lo;
-      const uint64_t lanes = (uint64_t)(f1 - f0) * K;
-      const uint32_t g_exp = (uint32_t)std::min<uint64_t>(max_grid, (lanes + LV_BLOCK - 1) / LV_BLOCK);
-      const uint64_t kids_ub = std::min<uint64_t>(2 * lanes, L.ccap);
-      const uint32_t g_cls = (uint32_t)std::min<uint64_t>(max_grid, (kids_ub + 3) / 4);
-      const uint32_t g_ins = (uint32_t)std::min<uint64_t>(max_grid, (std::min<uint64_t>(kids_ub, L.scap) + LV_BLOCK - 1) / LV_BLOCK);
-      LVCHK(lv_dispatch(kmax, 0, std::max<uint32_t>(1, g_exp), p, st));
-      LVCHK(lv_dispatch(kmax, 1, std::max<uint32_t>(1, g_cls), p, st));
-      LVCHK(lv_dispatch(kmax, 2, std::max<uint32_t>(1, g_ins), p, st));
-      LVCHK(hipStreamSynchronize(st));  // hc was published by lv_insert's last block
-      if (hc->found) break;
-      if (hc->overflow) {
-        if (f1 - f0 == 1) { verdict = V_UNKNOWN; reason = S2LC_R_FRONTIER; stop = true; break; }
-        chunk = std::max<uint32_t>(1, (f1 - f0) / 2);
-        ++ls.chunk_retries;
-        continue;
-      }
-      children += std::min(hc->nchild, L.ccap);
-      st_lo = std::min(hc->nstage, L.scap);
-      nn_lo = hc->nnext;
-      f0 = f1;
+      if (stop) break;  // hr->done stays LVR_OVERFLOW: Unknown (frontier)
+      LVCHK(lv_dispatch(nq, LK_CLOSE, 1, p, st));  // the round's bookkeeping (publishes hr)
+      // chunked rounds did not clear their frontier's table slots: reset the table
+      LVCHK(hipMemsetAsync(L.ht, 0xFF, ((size_t)L.ht_mask + 1) * 8, st));
+      LVCHK(hipStreamSynchronize(st));
+      p.close_round = 1;
+      next_round = r + 1;
     }
-    if (hc->found) children += std::min(hc->nchild, L.ccap);
-    if (stop) break;
+    nf_last = hr->nf;
   }
-  LVCHK(hipEventRecord(e1, st));
-  LVCHK(hipEventSynchronize(e1));
+  LVCHK(hipEventRecord(L.ev[1], st));
+  LVCHK(hipEventSynchronize(L.ev[1]));
   float ms = 0;
-  LVCHK(hipEventElapsedTime(&ms, e0, e1));
-  LVCHK(hipEventDestroy(e0));
-  LVCHK(hipEventDestroy(e1));
-  // clear the table for the next search (slots of the last frontier; cheap
-  // enough to reset whole when the frontier was large)
+  LVCHK(hipEventElapsedTime(&ms, L.ev[0], L.ev[1]));
+  const LvRun fin = *hr;
+#ifdef S2LC_PROF
+  {
+    unsigned long long g[16];
+    LVCHK(hipMemcpy(g, d_prof, sizeof g, hipMemcpyDeviceToHost));
+    (void)hipFree(d_prof);
+    const double it = g[5] ? (double)g[5] : 1.0, ch = g[6] ? (double)g[6] : 1.0;
+    fprintf(stderr,
+            "[s2lc lvprof] items %llu children %llu syncs %u | cycles/item parent %.0f heads+fp %.0f moves %.0f | "
+            "cycles/child closure %.0f stage+restore %.0f | total Gcycles %.2f\n",
+            g[5], g[6], syncs, g[0] / it, g[1] / it, g[2] / it, g[3] / ch, g[4] / ch,
+            (g[0] + g[1] + g[2] + g[3] + g[4]) * 1e-9);
+  }
+#endif
+  // clear the table for the next search
   LVCHK(hipMemsetAsync(L.ht, 0xFF, ((size_t)L.ht_mask + 1) * 8, st));
 
+  uint32_t verdict, reason;
+  switch (fin.done) {
+    case LVR_FOUND: verdict = V_OK; reason = 0; break;
+    case LVR_EMPTY: verdict = V_ILLEGAL; reason = S2LC_R_SEARCH_EXHAUSTED; break;
+    case LVR_BUDGET: verdict = V_UNKNOWN; reason = S2LC_R_BUDGET; break;
+    case LVR_OVERFLOW: verdict = V_UNKNOWN; reason = S2LC_R_FRONTIER; break;
+    default: verdict = V_UNKNOWN; reason = timed_out ? S2LC_R_TIMEOUT : S2LC_R_FRONTIER; break;
+  }
   HistResult& R = b.h_res[h];
   const uint32_t woff = R.witness_off;
   R = HistResult{};
   R.witness_off = woff;
   R.verdict = verdict;
   R.reason = reason;
-  R.rounds = rounds;
-  R.configs = configs;
-  R.children = children;
-  R.p4 = verdict == V_OK ? hc->found_p4 : 0;
-  const bool have_w = verdict == V_OK && wit;
-  R.final_parent = have_w ? hc->found_parent : TRACE_NONE;
-  R.final_move = verdict == V_OK ? hc->found_move : TRACE_NONE;
-  R.deep_trace = deep_trace;
-  R.deep_len = deep_len;
-  R.has_witness = (have_w || deep_trace != TRACE_NONE) ? 2u : 0u;
+  // rounds: expansion rounds run (the found / empty round included; an
+  // overflowing round counts, a timed-out search stops after a completed one)
+  R.rounds = fin.done == LVR_OVERFLOW ? fin.round + 1 : fin.round;
+  R.configs = fin.configs;
+  R.children = fin.children;
+  R.p4 = verdict == V_OK ? fin.found_p4 : 0;
+  const bool have_w = verdict == V_OK && fin.witness && fin.found_parent != TRACE_NONE;
+  const bool root_w = verdict == V_OK && fin.witness && fin.round == 0;  // completed by the initial closure
+  R.final_parent = have_w ? fin.found_parent : TRACE_NONE;
+  R.final_move = verdict == V_OK ? fin.found_move : TRACE_NONE;
+  R.deep_trace = verdict == V_ILLEGAL ? fin.deep_trace : TRACE_NONE;
+  R.deep_len = fin.deep_len;
+  R.has_witness = (have_w || root_w || R.deep_trace != TRACE_NONE) ? 2u : 0u;
   LVCHK(hipMemcpyAsync(b.res + h, &R, sizeof R, hipMemcpyHostToDevice, st));
-  if (witness && b.trace) {
-    unsigned long long th = tnext;
+  if (ro.witness && b.trace) {
+    unsigned long long th = fin.tnext;
     LVCHK(hipMemcpyAsync(b.trace_head, &th, sizeof th, hipMemcpyHostToDevice, st));
   }
   LVCHK(hipStreamSynchronize(st));
   ls.ms += ms;
-  ls.rounds += rounds;
-  ls.configs += configs;
-  ls.children += children;
-  ls.max_frontier = std::max(ls.max_frontier, max_frontier);
+  ls.rounds += R.rounds;
+  ls.configs += fin.configs;
+  ls.children += fin.children;
+  ls.max_frontier = std::max(ls.max_frontier, fin.max_frontier);
   ls.histories++;
+  ls.syncs += syncs;
   return 0;
 }
 
@@ -290,7 +368,7 @@ int level_search(DevBatch& b, uint32_t h, hipStream_t st, const RunOpts& ro, int
 // Distributed level search of one history (BASELINE config C5 over several
 // GPUs). Configurations are owned by rank lv_owner(fp). A round
 // on each rank:
-//   dist_expand : expand + close the local frontier (as above) into local
+//   dist_expand : expand + close the local frontier (lv_round) into local
 //                 staging, count the staged configurations per owner rank
 //   (caller)    : all-to-all of the counts, allocate the send buffer
 //   dist_pack   : copy the staged configurations into owner-major buckets
@@ -299,7 +377,8 @@ int level_search(DevBatch& b, uint32_t h, hipStream_t st, const RunOpts& ro, int
 //                 the local table; the winners are its next frontier
 // The received buffer stays the frontier of the next round (the caller keeps
 // it alive). Trace ids are rank << 29 | local pool index, so the parent chain
-// of a witness crosses ranks; the caller gathers the pools at the end.
+// of a witness crosses ranks; the caller gathers the pools at the end. These
+// rounds are host-driven (the caller's collectives sit between the kernels).
 // ============================================================================
 
 int dist_create(DistLevel& d, const History* h, uint32_t rank, uint32_t world, uint32_t reductions_off,
@@ -311,10 +390,11 @@ int dist_create(DistLevel& d, const History* h, uint32_t rank, uint32_t world, u
   d.rank = rank;
   d.world = world;
   d.K = d.b.h_hist[0].K;
-  d.kmax = level_kmax(d.K);
-  d.cb = lv_cfg_bytes(d.kmax);
+  d.nq = level_nq(d.K);
+  d.cb = lv_cfg_bytes(d.nq);
   if (d.b.forced[0]) { err = "history is structurally illegal (unmatched events)"; return S2LC_EINVAL; }
-  if (level_buffers(d.b, d.kmax, err)) return S2LC_EHIP;
+  if (level_buffers(d.b, d.nq, err)) return S2LC_EHIP;
+  if (lv_grids(d.b.lv, d.nq, err)) return S2LC_EHIP;
   LVCHK(hipMalloc(&d.own_cnt, 8 * sizeof(uint32_t)));
   LVCHK(hipMalloc(&d.own_pos, (size_t)d.b.lv.scap * sizeof(uint32_t)));
   size_t free_b = 0, total_b = 0;
@@ -341,69 +421,63 @@ static LvParams dist_params(DistLevel& d) {
   LvParams p;
   memset(&p, 0, sizeof p);
   p.recs = d.b.recs; p.pool = d.b.pool; p.cs = d.b.chain_start + hd.cs_base; p.K = d.K; p.hflags = hd.flags;
-  p.child = reinterpret_cast<LChild*>(L.child); p.ccap = L.ccap; p.scap = L.scap;
-  p.ht = L.ht; p.ht_mask = L.ht_mask;
-  p.trace = d.trace; p.ctl = reinterpret_cast<LvCtl*>(L.ctl);
+  p.scap = L.scap; p.scs = L.scap / LV_STRIPES; p.ht = L.ht; p.ht_mask = L.ht_mask;
+  p.trace = d.trace; p.trace_cap = d.trace_cap;
+  p.ctl = reinterpret_cast<LvCtl*>(L.ctl);
   p.world = d.world; p.own_cnt = d.own_cnt; p.own_pos = d.own_pos;
   // local staging (the closed children of this rank): the array that does not
   // hold the current frontier
   p.stg = d.cur == L.stg[0] ? L.stg[1] : L.stg[0];
   p.cur = d.cur; p.cur_idx = L.idx[d.cur_sel];
   p.tgid = d.rank << 29;
+  p.witness_host = 1;
   return p;
+}
+
+// expand + close this rank's frontier (round 0: the initial configuration, on
+// rank 0 only) into local staging; host-driven, control block 0
+static int dist_stage(DistLevel& d, LvParams& p, std::string& err) {
+  hipStream_t st = d.stream;
+  LVCHK(hipMemsetAsync(p.ctl, 0, sizeof(LvCtl), st));
+  if (d.round == 0) {
+    if (d.rank == 0) {
+      p.init = 1; p.f0 = 0; p.f1 = 1;
+      LVCHK(lv_dispatch(d.nq, LK_ROUND, 1, p, st));
+      p.init = 0;
+    }
+  } else if (d.nf) {
+    p.f0 = 0; p.f1 = d.nf; p.clear_slots = 1;
+    LVCHK(lv_dispatch(d.nq, LK_ROUND, d.b.lv.grid_round, p, st));
+  }
+  return 0;
 }
 
 int dist_expand(DistLevel& d, uint64_t* counts, int* found, std::string& err) {
   LevelBufs& L = d.b.lv;
   LvCtl* hc = reinterpret_cast<LvCtl*>(L.h_ctl);
-  int dev = 0;
-  LVCHK(hipGetDevice(&dev));
-  int n_cu = 256;
-  (void)hipDeviceGetAttribute(&n_cu, hipDeviceAttributeMultiprocessorCount, dev);
-  const uint32_t max_grid = (uint32_t)n_cu * 8;
+  const uint32_t max_grid = (uint32_t)n_cus(err) * 8;
   hipStream_t st = d.stream;
   LvParams p = dist_params(d);
-  hipEvent_t e0, e1;
-  LVCHK(hipEventCreate(&e0));
-  LVCHK(hipEventCreate(&e1));
-  LVCHK(hipEventRecord(e0, st));
-  memset(hc, 0, sizeof(LvCtl));
+  LVCHK(hipEventRecord(L.ev[0], st));
   LVCHK(hipMemsetAsync(d.own_cnt, 0, 8 * sizeof(uint32_t), st));
-  if (d.round == 0) {
-    // the initial configuration: closed on rank 0 only
-    if (d.rank == 0) {
-      hc->nchild = 1;
-      const LChild c0{0, 0, 0, LV_NONE, LV_NONE, 0};
-      LVCHK(hipMemcpyAsync(L.child, &c0, sizeof c0, hipMemcpyHostToDevice, st));
-    }
-    LVCHK(hipMemcpyAsync(L.ctl, hc, sizeof(LvCtl), hipMemcpyHostToDevice, st));
-    if (d.rank == 0) LVCHK(lv_dispatch(d.kmax, 1, 1, p, st));
-  } else {
-    LVCHK(hipMemcpyAsync(L.ctl, hc, sizeof(LvCtl), hipMemcpyHostToDevice, st));
-    if (d.nf) {
-      p.f0 = 0; p.f1 = d.nf; p.clear_slots = 1;
-      const uint64_t lanes = (uint64_t)d.nf * d.K;
-      const uint64_t kids_ub = std::min<uint64_t>(2 * lanes, L.ccap);
-      LVCHK(lv_dispatch(d.kmax, 0, (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>(max_grid, (lanes + LV_BLOCK - 1) / LV_BLOCK)), p, st));
-      LVCHK(lv_dispatch(d.kmax, 1, (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>(max_grid, (kids_ub + 3) / 4)), p, st));
-    }
-  }
-  // ownership buckets
-  const uint32_t g_b = max_grid;
-  LVCHK(lv_dispatch(d.kmax, 3, g_b, p, st));
+  if (dist_stage(d, p, err)) return S2LC_EHIP;
+  LVCHK(hipMemcpyAsync(hc, L.ctl, sizeof(LvCtl), hipMemcpyDeviceToHost, st));
+  LVCHK(hipStreamSynchronize(st));
+  uint32_t maxc = 0;  // the longest staging stripe
+  for (int s_ = 0; s_ < LV_STRIPES; ++s_) maxc = std::max(maxc, std::min(hc->cnt[16 * s_], p.scs));
+  d.slot_hi = maxc * LV_STRIPES;
+  p.dense = d.slot_hi;
+  if (d.slot_hi)
+    LVCHK(lv_dispatch(d.nq, LK_BUCKET, (uint32_t)std::min<uint64_t>(max_grid, (d.slot_hi + LV_BLOCK - 1) / LV_BLOCK), p, st));
   uint32_t cnt[8] = {0};
   LVCHK(hipMemcpyAsync(cnt, d.own_cnt, sizeof cnt, hipMemcpyDeviceToHost, st));
-  LVCHK(hipMemcpyAsync(hc, L.ctl, sizeof(LvCtl), hipMemcpyDeviceToHost, st));
-  LVCHK(hipEventRecord(e1, st));
+  LVCHK(hipEventRecord(L.ev[1], st));
   LVCHK(hipStreamSynchronize(st));
   float ms = 0;
-  LVCHK(hipEventElapsedTime(&ms, e0, e1));
-  (void)hipEventDestroy(e0);
-  (void)hipEventDestroy(e1);
+  LVCHK(hipEventElapsedTime(&ms, L.ev[0], L.ev[1]));
   d.ms += ms;
   if (hc->overflow) { err = "distributed round exceeds the device buffers"; return S2LC_ENOMEM; }
-  d.children += std::min(hc->nchild, L.ccap);
-  d.nstage = std::min(hc->nstage, L.scap);
+  d.children += hc->children;
   for (uint32_t o = 0; o < d.world; ++o) counts[o] = cnt[o];
   *found = hc->found ? 1 : 0;
   if (hc->found) { d.found_parent = hc->found_parent; d.found_move = hc->found_move; d.found_p4 = hc->found_p4; }
@@ -414,11 +488,13 @@ int dist_pack(DistLevel& d, uint8_t* send, const uint64_t* counts, std::string& 
   LvParams p = dist_params(d);
   uint64_t off = 0;
   for (uint32_t o = 0; o < d.world; ++o) { p.own_off[o] = off; off += counts[o]; }
-  if (off != d.nstage) { err = "bucket counts do not match the staged configurations"; return S2LC_EINVAL; }
+  if (off > d.slot_hi) { err = "bucket counts exceed the staged configurations"; return S2LC_EINVAL; }
+  if (off && !send) { err = "null send buffer"; return S2LC_EINVAL; }
   p.send = send;
-  if (d.nstage) {
-    const uint64_t pieces = (uint64_t)d.nstage * (d.cb / 16);
-    LVCHK(lv_dispatch(d.kmax, 4, (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>(2048, (pieces + LV_BLOCK - 1) / LV_BLOCK)), p, d.stream));
+  p.dense = d.slot_hi;
+  if (d.slot_hi && off) {
+    const uint64_t pieces = (uint64_t)d.slot_hi * (d.cb / 16);
+    LVCHK(lv_dispatch(d.nq, LK_SCATTER, (uint32_t)std::min<uint64_t>(2048, (pieces + LV_BLOCK - 1) / LV_BLOCK), p, d.stream));
   }
   LVCHK(hipStreamSynchronize(d.stream));
   return 0;
@@ -431,30 +507,21 @@ int dist_insert(DistLevel& d, uint8_t* recv, uint64_t n_recv, uint64_t* n_next, 
   hipStream_t st = d.stream;
   const int sel = d.cur_sel ^ 1;
   LvParams p = dist_params(d);
-  p.stg = recv; p.nxt_idx = L.idx[sel]; p.st_lo = 0;
-  p.witness = 1;
+  p.stg = recv; p.nxt_idx = L.idx[sel]; p.dense = (uint32_t)n_recv;
   if (d.tnext + n_recv > d.trace_cap) { err = "trace pool full"; return S2LC_ENOMEM; }
-  p.tbase = (uint32_t)d.tnext;
+  p.tbase_host = (uint32_t)d.tnext;
   memset(hc, 0, sizeof(LvCtl));
-  hc->nstage = (uint32_t)n_recv;
-  hipEvent_t e0, e1;
-  LVCHK(hipEventCreate(&e0));
-  LVCHK(hipEventCreate(&e1));
-  LVCHK(hipEventRecord(e0, st));
+  LVCHK(hipEventRecord(L.ev[0], st));
   LVCHK(hipMemcpyAsync(L.ctl, hc, sizeof(LvCtl), hipMemcpyHostToDevice, st));
   if (n_recv) {
-    int dev = 0, n_cu = 256;
-    LVCHK(hipGetDevice(&dev));
-    (void)hipDeviceGetAttribute(&n_cu, hipDeviceAttributeMultiprocessorCount, dev);
-    LVCHK(lv_dispatch(d.kmax, 2, (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>((uint64_t)n_cu * 8, (n_recv + LV_BLOCK - 1) / LV_BLOCK)), p, st));
+    const uint32_t max_grid = (uint32_t)n_cus(err) * 8;
+    LVCHK(lv_dispatch(d.nq, LK_INSERT, (uint32_t)std::min<uint64_t>(max_grid, (n_recv + LV_BLOCK - 1) / LV_BLOCK), p, st));
   }
   LVCHK(hipMemcpyAsync(hc, L.ctl, sizeof(LvCtl), hipMemcpyDeviceToHost, st));
-  LVCHK(hipEventRecord(e1, st));
+  LVCHK(hipEventRecord(L.ev[1], st));
   LVCHK(hipStreamSynchronize(st));
   float ms = 0;
-  LVCHK(hipEventElapsedTime(&ms, e0, e1));
-  (void)hipEventDestroy(e0);
-  (void)hipEventDestroy(e1);
+  LVCHK(hipEventElapsedTime(&ms, L.ev[0], L.ev[1]));
   d.ms += ms;
   d.cur = recv;
   d.cur_sel = sel;
@@ -473,47 +540,29 @@ int dist_insert(DistLevel& d, uint8_t* recv, uint64_t n_recv, uint64_t* n_next, 
 int dist_local_round(DistLevel& d, uint64_t* n_next, int* found, std::string& err) {
   LevelBufs& L = d.b.lv;
   LvCtl* hc = reinterpret_cast<LvCtl*>(L.h_ctl);
-  int dev = 0, n_cu = 256;
-  LVCHK(hipGetDevice(&dev));
-  (void)hipDeviceGetAttribute(&n_cu, hipDeviceAttributeMultiprocessorCount, dev);
-  const uint64_t max_grid = (uint64_t)n_cu * 8;
+  const uint32_t max_grid = (uint32_t)n_cus(err) * 8;
   hipStream_t st = d.stream;
   LvParams p = dist_params(d);
   p.nxt_idx = L.idx[d.cur_sel ^ 1];
-  p.witness = 1;
   if (d.tnext + L.scap > d.trace_cap) { err = "trace pool full"; return S2LC_ENOMEM; }
-  p.tbase = (uint32_t)d.tnext;
-  hipEvent_t e0, e1;
-  LVCHK(hipEventCreate(&e0));
-  LVCHK(hipEventCreate(&e1));
-  LVCHK(hipEventRecord(e0, st));
-  memset(hc, 0, sizeof(LvCtl));
-  if (d.round == 0) {
-    hc->nchild = 1;
-    const LChild c0{0, 0, 0, LV_NONE, LV_NONE, 0};
-    LVCHK(hipMemcpyAsync(L.child, &c0, sizeof c0, hipMemcpyHostToDevice, st));
-    LVCHK(hipMemcpyAsync(L.ctl, hc, sizeof(LvCtl), hipMemcpyHostToDevice, st));
-    LVCHK(lv_dispatch(d.kmax, 1, 1, p, st));
-    LVCHK(lv_dispatch(d.kmax, 2, 1, p, st));
-  } else {
-    LVCHK(hipMemcpyAsync(L.ctl, hc, sizeof(LvCtl), hipMemcpyHostToDevice, st));
-    p.f0 = 0; p.f1 = d.nf; p.clear_slots = 1;
-    const uint64_t lanes = (uint64_t)d.nf * d.K;
-    const uint64_t kids_ub = std::min<uint64_t>(2 * lanes, L.ccap);
-    LVCHK(lv_dispatch(d.kmax, 0, (uint32_t)std::max<uint64_t>(1, std::min(max_grid, (lanes + LV_BLOCK - 1) / LV_BLOCK)), p, st));
-    LVCHK(lv_dispatch(d.kmax, 1, (uint32_t)std::max<uint64_t>(1, std::min(max_grid, (kids_ub + 3) / 4)), p, st));
-    LVCHK(lv_dispatch(d.kmax, 2, (uint32_t)std::max<uint64_t>(1, std::min(max_grid, (std::min<uint64_t>(kids_ub, L.scap) + LV_BLOCK - 1) / LV_BLOCK)), p, st));
-  }
+  p.tbase_host = (uint32_t)d.tnext;
+  LVCHK(hipEventRecord(L.ev[0], st));
+  const bool first = d.round == 0;
+  const uint32_t rank = d.rank;
+  d.rank = 0;  // replicated: every rank closes the initial configuration
+  const int rc = dist_stage(d, p, err);
+  d.rank = rank;
+  if (rc) return rc;
+  const uint64_t ins = first ? 1 : std::min<uint64_t>(max_grid, std::max<uint64_t>(4, (uint64_t)d.nf * 64 / LV_BLOCK));
+  LVCHK(lv_dispatch(d.nq, LK_INSERT, (uint32_t)ins, p, st));
   LVCHK(hipMemcpyAsync(hc, L.ctl, sizeof(LvCtl), hipMemcpyDeviceToHost, st));
-  LVCHK(hipEventRecord(e1, st));
+  LVCHK(hipEventRecord(L.ev[1], st));
   LVCHK(hipStreamSynchronize(st));
   float ms = 0;
-  LVCHK(hipEventElapsedTime(&ms, e0, e1));
-  (void)hipEventDestroy(e0);
-  (void)hipEventDestroy(e1);
+  LVCHK(hipEventElapsedTime(&ms, L.ev[0], L.ev[1]));
   d.ms += ms;
   if (hc->overflow && !hc->found) { err = "replicated round exceeds the device buffers"; return S2LC_ENOMEM; }
-  d.children += std::min(hc->nchild, L.ccap);
+  d.children += hc->children;
   *found = hc->found ? 1 : 0;
   if (hc->found) {
     d.found_parent = hc->found_parent; d.found_move = hc->found_move; d.found_p4 = hc->found_p4;
@@ -541,7 +590,7 @@ int dist_keep_owned(DistLevel& d, uint64_t* n_kept, std::string& err) {
   p.nxt_idx = L.idx[d.cur_sel ^ 1];
   memset(hc, 0, sizeof(LvCtl));
   LVCHK(hipMemcpyAsync(L.ctl, hc, sizeof(LvCtl), hipMemcpyHostToDevice, st));
-  if (d.nf) LVCHK(lv_dispatch(d.kmax, 5, (uint32_t)std::min<uint64_t>(2048, (d.nf + LV_BLOCK - 1) / LV_BLOCK), p, st));
+  if (d.nf) LVCHK(lv_dispatch(d.nq, LK_KEEP, (uint32_t)std::min<uint64_t>(2048, (d.nf + LV_BLOCK - 1) / LV_BLOCK), p, st));
   // the table still holds the dropped configurations' slots: reset it
   LVCHK(hipMemsetAsync(L.ht, 0xFF, ((size_t)L.ht_mask + 1) * 8, st));
   LVCHK(hipMemcpyAsync(hc, L.ctl, sizeof(LvCtl), hipMemcpyDeviceToHost, st));
@@ -559,7 +608,7 @@ int dist_frontier_pack(DistLevel& d, uint8_t* buf, std::string& err) {
   p.send = buf;
   if (d.nf) {
     const uint64_t pieces = (uint64_t)d.nf * (d.cb / 16);
-    LVCHK(lv_dispatch(d.kmax, 6, (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>(2048, (pieces + LV_BLOCK - 1) / LV_BLOCK)), p, d.stream));
+    LVCHK(lv_dispatch(d.nq, LK_GATHER, (uint32_t)std::min<uint64_t>(2048, (pieces + LV_BLOCK - 1) / LV_BLOCK), p, d.stream));
   }
   LVCHK(hipStreamSynchronize(d.stream));
   return 0;

@@ -4,70 +4,103 @@
 // chains (single hard histories, BASELINE config C5). Same search as
 // search_dev.h (rounds of one durable/indefinite append, E-closure,
 // I-identity deferral, P1/P2/P4), replacing porcupine v1.0.3 checkSingle
-// (called at golang/s2-porcupine/main.go:606), but every phase of a round is a
-// grid-wide launch over the whole chip:
+// (called at golang/s2-porcupine/main.go:606). A round is two grid-wide
+// kernels:
 //
-//   lv_expand : one lane per (frontier configuration, chain) candidate
-//               -> raw children (parent, move, successor state), 32 B each
-//   lv_close  : one WAVE per child; lane l owns chains l, l+64, ...; a closure
-//               pass is one head load per owned chain + wave min-reductions of
-//               minret (return events) and the P1 bound; all legal minimal
-//               identity ops advance together -> closed configuration staged
-//               in HBM with its fingerprint
+//   lv_round  : one WAVE per (frontier configuration, slice of its candidate
+//               moves). Lane l owns chains l, l+64, ..., l+64(NQ-1) and loads
+//               their head records ONCE into registers. For every child in its
+//               slice (a minimal durable/indefinite append at a chain head, and
+//               its outcome) the wave runs the E-closure against those cached
+//               heads: only the chains the closure advances load a record. The
+//               closed child is staged in HBM with an incrementally updated
+//               fingerprint (the parent's chain terms XOR the changed ones).
 //   lv_insert : one lane per staged configuration; 64-bit atomicCAS
 //               open-addressing table (32-bit tag | staging index), full-key
-//               compare on a tag hit; winners form the next frontier (an
-//               index list into the staging array) and get a trace entry
+//               compare on a tag hit; the winners form the next frontier (an
+//               index list into the staging array) and get a trace entry.
+//               Its last block closes the round on the device (counters,
+//               Ok / Illegal / budget / overflow decisions, per-round counts)
+//               and publishes the run state to host-mapped memory.
 //
-// The frontier of round r is the staging array written in round r (double
-// buffered), so a surviving configuration is written exactly once.
+// Because the round's bookkeeping is on the device, the host enqueues many
+// rounds back to back and reads the run state once per batch (level.hip);
+// every kernel of a finished run returns at once.
+//
+// Layout: NQ = ceil(K / 64) register slots per lane; a configuration holds
+// 64 * NQ u16 chain counters, so K = 319 stores 320 counters (not 512).
 #pragma once
 
 namespace s2lc {
 namespace {
 
 constexpr uint32_t LV_NONE = 0xFFFFFFFFu;
+constexpr uint32_t LV_HOLE = 0xFFFFFFFEu;  // LCfg::move of a reserved, unused staging slot
 constexpr int LV_BLOCK = 256;
+constexpr uint32_t LV_RESERVE = 8;          // staging slots a wave reserves per atomic
 
-// A staged / frontier configuration: 48 + 2*KMAX bytes.
-template <int KMAX>
+// A staged / frontier configuration: 48 + 128 * NQ bytes.
+template <int NQ>
 struct __attribute__((aligned(16))) LCfg {
   uint64_t tail;
   uint64_t hash;
   uint64_t fp;      // fingerprint (dedupe / ownership)
   uint32_t tok;
   uint32_t minret;  // exact minret of the closed configuration
-  uint32_t ptrace;  // trace index of the parent
-  uint32_t move;    // chain | MOVE_IDENT, LV_NONE for the initial configuration
-  uint32_t trace;   // own trace index once in a frontier
+  uint32_t ptrace;  // trace id of the parent
+  uint32_t move;    // chain | MOVE_IDENT; LV_NONE initial configuration; LV_HOLE unused slot
+  uint32_t trace;   // own trace id once in a frontier
   uint32_t slot;    // table slot (cleared when this configuration is expanded)
-  uint16_t cnt[KMAX];
+  uint16_t cnt[64 * NQ];
 };
-static_assert(offsetof(LCfg<64>, trace) == 40, "LCfg::trace offset (read by the host)");
+static_assert(offsetof(LCfg<1>, trace) == 40, "LCfg::trace offset");
 
-// A raw child: successor state of frontier configuration `parent` (staging
-// index) after the op at the head of chain move & 0xFFFF.
-struct __attribute__((aligned(16))) LChild {
-  uint64_t tail;
-  uint64_t hash;
-  uint32_t tok;
-  uint32_t parent;  // staging index of the parent, LV_NONE = the all-zero initial configuration
-  uint32_t move;
-  uint32_t _pad;
-};
-
-// Device-side counters of one round.
+// Per-round device counters (double buffered by round parity). Staging is
+// split into LV_STRIPES stripes with a counter each, 64 bytes apart: a single
+// counter serializes same-address atomics (~11 ns each on MI355X), and a wide
+// round stages millions of configurations.
+constexpr int LV_STRIPES = 64;
 struct LvCtl {
-  uint32_t nchild;    // children produced by lv_expand
-  uint32_t nstage;    // closed configurations staged by lv_close
   uint32_t nnext;     // unique configurations inserted by lv_insert
   uint32_t found;     // a child completed (Ok)
-  uint32_t overflow;  // 1: children over capacity, 2: staging over capacity
-  uint32_t found_parent, found_move, found_p4;
-  unsigned long long children;  // running total
-  uint32_t done_blocks;         // lv_insert blocks finished (the last one publishes)
-  uint32_t _pad[5];
+  uint32_t overflow;  // a staging stripe over capacity
+  uint32_t done_blocks;  // lv_insert blocks finished (the last one closes the round)
+  uint32_t found_parent, found_move, found_p4, _p0;
+  unsigned long long children;  // children generated this round
+  uint32_t _pad[6];
+  uint32_t lo[LV_STRIPES];        // lv_insert: first slot of each stripe not inserted yet (chunked rounds)
+  uint32_t cnt[LV_STRIPES * 16];  // stripe s reserves slots at cnt[16 s] (holes included)
 };
+static_assert(sizeof(LvCtl) == 64 + 4 * LV_STRIPES + 64 * LV_STRIPES, "LvCtl layout");
+
+__device__ __forceinline__ uint32_t ld_agent(const uint32_t* p) {
+  return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ unsigned long long ld_agent64(const unsigned long long* p) {
+  return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+// State of one level search, kept on the device across rounds and published
+// to host-mapped memory by the last lv_insert block of every round.
+enum : uint32_t { LVR_RUNNING = 0, LVR_FOUND = 1, LVR_EMPTY = 2, LVR_BUDGET = 3, LVR_OVERFLOW = 4 };
+struct LvRun {
+  uint32_t done;           // LVR_*
+  uint32_t round;          // expansion rounds completed (round 0 = the initial closure)
+  uint32_t nf;             // current frontier size
+  uint32_t max_frontier;
+  unsigned long long configs;   // sum of the frontiers (round 0 included)
+  unsigned long long children;
+  unsigned long long tnext;     // next trace index of this process's pool
+  unsigned long long max_configs;  // budget (0 = none)
+  uint32_t found_parent, found_move, found_p4;
+  uint32_t witness;        // recording trace entries
+  uint32_t deep_trace, deep_len;  // Illegal: a configuration of the deepest non-empty round
+  uint32_t last_tbase;     // trace index of the first winner of the last non-empty round
+  uint32_t last_nf;        // frontier expanded by the last round
+  unsigned long long last_children;  // children it generated (slices per configuration)
+  uint32_t _pad[2];
+};
+static_assert(sizeof(LvRun) == 96, "LvRun layout");
 
 struct LvParams {
   const OpRec* __restrict__ recs;
@@ -75,68 +108,95 @@ struct LvParams {
   const uint32_t* __restrict__ cs;  // K+1 absolute chain starts of this history
   uint32_t K;
   uint32_t hflags;
-  // current frontier: positions [f0, f1) of cur_idx index cur (staging array)
+  // current frontier: positions [f0, f1) of cur_idx index cur (staging array);
+  // f1 = LV_NONE: the whole frontier, size read from run->nf on the device
   const uint8_t* cur;
   const uint32_t* cur_idx;
   uint32_t f0, f1;
-  // children
-  LChild* child;
-  uint32_t ccap;
   // staging of this round (becomes the next frontier) + its index list
   uint8_t* stg;
   uint32_t* nxt_idx;
   uint32_t scap;
-  uint32_t st_lo;  // lv_insert: first staged configuration of this chunk
+  uint32_t scs;          // staging slots per stripe (scap / LV_STRIPES); slot = stripe * scs + index
+  uint32_t dense;        // lv_insert: a dense input of this many configurations (distributed receive), else striped
   unsigned long long* ht;
   uint32_t ht_mask;
-  uint32_t clear_slots;  // lv_expand clears the table slots of the frontier it expands
-  LvCtl* ctl_next;       // lv_expand zeroes the next round's control block (double buffer)
-  LvCtl* publish;        // host-mapped mirror lv_insert's last block copies the control block to
+  uint32_t clear_slots;  // lv_round clears the table slots of the frontier it expands
+  uint32_t init;         // lv_round: round 0 (close the initial configuration)
+  uint32_t round;        // the round this launch belongs to (host count)
+  LvCtl* ctl;            // this round's counters
+  LvCtl* ctl_next;       // lv_round zeroes the next round's counters (double buffer)
+  LvRun* run;            // device run state
+  LvRun* publish;        // host-mapped mirror of *run (the last lv_insert block copies it)
+  uint32_t close_round;  // lv_insert's last block closes the round (0: a chunk of a host-driven round)
+  uint32_t publish_always;  // publish the run state after this round (else only when the search ends)
+  uint32_t* rcounts;     // per-round unique configurations (nullable)
   TraceEnt* trace;
-  uint32_t tbase;        // trace index of nxt_idx[0] (in this process's pool)
-  uint32_t witness;
+  uint64_t trace_cap;
   uint32_t tgid;         // added to pool indices to form trace ids (distributed: rank << 29)
-  LvCtl* ctl;
+  uint32_t tbase_host;   // distributed / host-driven: trace index of nxt_idx[0] when run == nullptr
+  uint32_t witness_host; // trace recording when run == nullptr
   // distributed search: ownership buckets of the staged configurations
   uint32_t world;
   uint32_t* own_cnt;     // [world] configurations per owner rank
   uint32_t* own_pos;     // per staged configuration: owner << 27 | position within the owner's bucket
   uint8_t* send;         // bucketed configurations, owner-major
   uint64_t own_off[8];   // first configuration of each owner's bucket in send
+  unsigned long long* prof;  // S2LC_PROF builds: lv_round phase cycles (nullable)
 };
 
-template <int KMAX>
-__device__ __forceinline__ const LCfg<KMAX>* lv_cfg(const uint8_t* base, uint32_t i) {
-  return reinterpret_cast<const LCfg<KMAX>*>(base + (size_t)i * sizeof(LCfg<KMAX>));
+template <int NQ>
+__device__ __forceinline__ const LCfg<NQ>* lv_cfg(const uint8_t* base, uint32_t i) {
+  return reinterpret_cast<const LCfg<NQ>*>(base + (size_t)i * sizeof(LCfg<NQ>));
 }
-template <int KMAX>
-__device__ __forceinline__ LCfg<KMAX>* lv_cfg(uint8_t* base, uint32_t i) {
-  return reinterpret_cast<LCfg<KMAX>*>(base + (size_t)i * sizeof(LCfg<KMAX>));
+template <int NQ>
+__device__ __forceinline__ LCfg<NQ>* lv_cfg(uint8_t* base, uint32_t i) {
+  return reinterpret_cast<LCfg<NQ>*>(base + (size_t)i * sizeof(LCfg<NQ>));
 }
 
+// ---- wave reductions: DPP inside each 16-lane row, then one readlane per row
+// (the result is wave-uniform, in scalar registers) ------------------------
+template <int CTRL>
+__device__ __forceinline__ uint32_t lv_dpp(uint32_t v) {
+  return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, CTRL, 0xF, 0xF, false);
+}
+__device__ __forceinline__ uint32_t rl(uint32_t v, int lane) { return (uint32_t)__builtin_amdgcn_readlane((int)v, lane); }
+
 __device__ __forceinline__ uint32_t wave_min_u32(uint32_t v) {
-#pragma unroll
-  for (int o = 32; o > 0; o >>= 1) v = min(v, (uint32_t)__shfl_xor((int)v, o, 64));
-  return v;
+  v = min(v, lv_dpp<0xB1>(v));   // quad_perm [1,0,3,2]
+  v = min(v, lv_dpp<0x4E>(v));   // quad_perm [2,3,0,1]
+  v = min(v, lv_dpp<0x124>(v));  // row_ror:4
+  v = min(v, lv_dpp<0x128>(v));  // row_ror:8
+  return min(min(rl(v, 0), rl(v, 16)), min(rl(v, 32), rl(v, 48)));
+}
+__device__ __forceinline__ uint32_t wave_max_u32(uint32_t v) {
+  v = max(v, lv_dpp<0xB1>(v));
+  v = max(v, lv_dpp<0x4E>(v));
+  v = max(v, lv_dpp<0x124>(v));
+  v = max(v, lv_dpp<0x128>(v));
+  return max(max(rl(v, 0), rl(v, 16)), max(rl(v, 32), rl(v, 48)));
+}
+__device__ __forceinline__ uint64_t lv_min64(uint64_t a, uint64_t b) { return a < b ? a : b; }
+template <int CTRL>
+__device__ __forceinline__ uint64_t lv_dpp64(uint64_t v) {
+  return ((uint64_t)lv_dpp<CTRL>((uint32_t)(v >> 32)) << 32) | lv_dpp<CTRL>((uint32_t)v);
+}
+__device__ __forceinline__ uint64_t rl64(uint64_t v, int lane) {
+  return ((uint64_t)rl((uint32_t)(v >> 32), lane) << 32) | rl((uint32_t)v, lane);
 }
 __device__ __forceinline__ uint64_t wave_min_u64(uint64_t v) {
-#pragma unroll
-  for (int o = 32; o > 0; o >>= 1) {
-    const uint32_t lo = (uint32_t)__shfl_xor((int)(uint32_t)v, o, 64);
-    const uint32_t hi = (uint32_t)__shfl_xor((int)(uint32_t)(v >> 32), o, 64);
-    const uint64_t w = ((uint64_t)hi << 32) | lo;
-    v = w < v ? w : v;
-  }
-  return v;
+  v = lv_min64(v, lv_dpp64<0xB1>(v));
+  v = lv_min64(v, lv_dpp64<0x4E>(v));
+  v = lv_min64(v, lv_dpp64<0x124>(v));
+  v = lv_min64(v, lv_dpp64<0x128>(v));
+  return lv_min64(lv_min64(rl64(v, 0), rl64(v, 16)), lv_min64(rl64(v, 32), rl64(v, 48)));
 }
 __device__ __forceinline__ uint64_t wave_xor_u64(uint64_t v) {
-#pragma unroll
-  for (int o = 32; o > 0; o >>= 1) {
-    const uint32_t lo = (uint32_t)__shfl_xor((int)(uint32_t)v, o, 64);
-    const uint32_t hi = (uint32_t)__shfl_xor((int)(uint32_t)(v >> 32), o, 64);
-    v ^= ((uint64_t)hi << 32) | lo;
-  }
-  return v;
+  v ^= lv_dpp64<0xB1>(v);
+  v ^= lv_dpp64<0x4E>(v);
+  v ^= lv_dpp64<0x124>(v);
+  v ^= lv_dpp64<0x128>(v);
+  return rl64(v, 0) ^ rl64(v, 16) ^ rl64(v, 32) ^ rl64(v, 48);
 }
 
 // Wave-aggregated bump allocation: lane asks for `want` entries; returns its
@@ -156,8 +216,10 @@ __device__ __forceinline__ uint32_t wave_alloc(uint32_t* ctr, uint32_t want) {
   return base + incl - want;
 }
 
-// Configuration fingerprint: state mix ^ XOR over chains of mix(chain, count).
-// Commutative over chains, so a wave computes it with one XOR reduction.
+// Configuration fingerprint: state term ^ XOR over chains of a per-(chain,
+// count) term. Commutative over chains, so a wave computes it with one XOR
+// reduction, and a child's differs from its parent's only in the chains the
+// move and its closure advanced.
 __device__ __forceinline__ uint64_t lv_chain_term(uint32_t j, uint32_t c) {
   return mix64(((uint64_t)j << 32 | c) * 0x9E3779B97F4A7C15ull + 0x2545F4914F6CDD1Dull);
 }
@@ -165,192 +227,374 @@ __device__ __forceinline__ uint64_t lv_state_term(uint64_t tail, uint64_t hash, 
   return mix64(tail ^ 0x9E3779B97F4A7C15ull) ^ mix64(hash + 0x632BE59BD9B4E019ull * (tok + 1));
 }
 
-// ---- expand: one lane per (frontier position, chain) ----------------------
-template <int KMAX>
-__global__ __launch_bounds__(LV_BLOCK) void lv_expand(LvParams p) {
-  if (p.ctl_next && blockIdx.x == 0 && threadIdx.x < sizeof(LvCtl) / 4)
-    reinterpret_cast<uint32_t*>(p.ctl_next)[threadIdx.x] = 0;
-  const uint32_t K = p.K;
-  const uint64_t total = (uint64_t)(p.f1 - p.f0) * K;
-  const uint64_t stride = (uint64_t)gridDim.x * LV_BLOCK;
-  for (uint64_t b0 = (uint64_t)blockIdx.x * LV_BLOCK; b0 < total; b0 += stride) {
-    const uint64_t it = b0 + threadIdx.x;
-    const bool act = it < total;
-    uint32_t nk = 0;
-    bool take_opt = false, take_id = false;
-    State opt{0, 0, 0}, s{0, 0, 0};
-    uint32_t k = 0, j = 0;
-    if (act) {
-      const uint32_t i = p.f0 + (uint32_t)(it / K);
-      j = (uint32_t)(it % K);
-      k = p.cur_idx[i];
-      const LCfg<KMAX>* pc = lv_cfg<KMAX>(p.cur, k);
-      if (j == 0 && p.clear_slots && pc->slot <= p.ht_mask) p.ht[pc->slot] = HT_EMPTY;
-      const uint32_t c = pc->cnt[j];
-      const OpRec* rp = p.recs + p.cs[j] + c;
-      const uint32_t f = rp->flags;
-      const uint32_t pmin = pc->minret;
-      if (!(f & (OPF_SENTINEL | OPF_CLS_E)) && rp->call_ev < pmin) {
-        const OpRec r = load_rec(rp);
-        s = State{pc->tail, pc->hash, pc->tok};
-        const bool g = append_guards_ok(r, s);
-        opt.tail = s.tail + r.num_records;
-        opt.tok = r.set_tok ? r.set_tok : s.tok;
-        opt.hash = s.hash;
-        if (r.flags & OPF_CLS_D) take_opt = g && opt.tail == r.out_tail;
-        else take_opt = g;
-        if (take_opt || (r.flags & OPF_CLS_I)) {
-          if (g) opt.hash = fold_hashes_blk(s.hash, p.pool + r.hash_off, r.hash_cnt);
-        }
-        if (r.flags & OPF_CLS_I) take_id = (!(p.hflags & H_IDEFER) || r.ret_ev == pmin) && !(g && state_eq(opt, s));
-        nk = (uint32_t)take_opt + (uint32_t)take_id;
+// The hot fields of a chain head the closure reads every pass; a head's
+// observation (out_tail / out_hash) is only read when it is an eligible
+// identity op. For a head loaded during a child's closure the state is fixed,
+// so its legality at that state (and the P2 verdict) is computed once at load
+// time and kept as flag bits.
+struct LvHot {
+  uint64_t suf;
+  uint32_t call, ret, fl;
+};
+constexpr uint32_t HB_KNOWN = 1u << 31;   // legality bits below are valid (a head loaded by this child)
+constexpr uint32_t HB_LEGAL = 1u << 30;   // legal at the child's state
+constexpr uint32_t HB_P2DEAD = 1u << 29;  // P2: a successful read at this tail with another hash
+
+// legality of an identity-class head at s (ident_legal) + the P2 condition
+__device__ __forceinline__ uint32_t lv_legal_bits(uint32_t fl, uint64_t otail, uint64_t ohash, const State& s) {
+  if ((fl & OPF_KIND_MASK) == 0) return HB_LEGAL;  // definite append failure: {s}
+  const bool hash_bad = (fl & OPF_HAS_HASH) && s.hash != ohash;
+  const bool tail_bad = !(fl & OPF_FAIL) && s.tail != otail;
+  uint32_t b = (!hash_bad && !tail_bad) ? HB_LEGAL : 0u;
+  if (hash_bad && !(fl & OPF_FAIL) && otail == s.tail) b |= HB_P2DEAD;
+  return b;
+}
+
+__device__ __forceinline__ LvHot lv_hot_null() {
+  LvHot h;
+  h.suf = REQ_NONE; h.call = EV_INF; h.ret = EV_INF; h.fl = OPF_SENTINEL;
+  return h;
+}
+
+// The parent's heads of one wave, in LDS (structure of arrays: lane-indexed,
+// so every access is conflict-free).
+template <int NQ>
+struct LvHeadsLds {
+  uint64_t otail[NQ][64], ohash[NQ][64], suf[NQ][64];
+  uint32_t call[NQ][64], ret[NQ][64], fl[NQ][64];
+};
+
+// Load the head at rec into LDS slot q and return its hot fields.
+template <int NQ>
+__device__ __forceinline__ LvHot lv_load_parent_head(const OpRec* r, LvHeadsLds<NQ>& L, int q, int lane) {
+  const uint4 a = ld16(r, 16);
+  const uint4 b = ld16(r, 32);
+  LvHot h;
+  h.suf = (uint64_t)b.x | ((uint64_t)b.y << 32);
+  h.call = b.z;
+  h.ret = b.w;
+  h.fl = r->flags;
+  L.otail[q][lane] = (uint64_t)a.x | ((uint64_t)a.y << 32);
+  L.ohash[q][lane] = (uint64_t)a.z | ((uint64_t)a.w << 32);
+  L.suf[q][lane] = h.suf;
+  L.call[q][lane] = h.call;
+  L.ret[q][lane] = h.ret;
+  L.fl[q][lane] = h.fl;
+  return h;
+}
+template <int NQ>
+__device__ __forceinline__ LvHot lv_parent_hot(const LvHeadsLds<NQ>& L, int q, int lane) {
+  LvHot h;
+  h.suf = L.suf[q][lane]; h.call = L.call[q][lane]; h.ret = L.ret[q][lane]; h.fl = L.fl[q][lane];
+  return h;
+}
+// A head loaded during a child's closure: hot fields + legality at s.
+__device__ __forceinline__ LvHot lv_load_child_head(const OpRec* r, const State& s) {
+  const uint4 a = ld16(r, 16);
+  const uint4 b = ld16(r, 32);
+  LvHot h;
+  h.suf = (uint64_t)b.x | ((uint64_t)b.y << 32);
+  h.call = b.z;
+  h.ret = b.w;
+  const uint32_t fl = r->flags;
+  h.fl = fl | HB_KNOWN |
+         lv_legal_bits(fl, (uint64_t)a.x | ((uint64_t)a.y << 32), (uint64_t)a.z | ((uint64_t)a.w << 32), s);
+  return h;
+}
+
+// E-closure of one child. H[q] = hot fields of the child's current head on
+// slot q (the parent's, unless the move or the closure advanced that chain),
+// d[q] = ops the child linearized on slot q beyond the parent's count.
+// A pass takes every identity head that is minimal under the previous pass's
+// minret (a lower bound of the current one: minret only grows, so such an op
+// is minimal now) and legal at s; all of them advance together (the closure
+// is order-independent). A pass that changes nothing has read exactly the
+// final heads, so its minret / P1 bound are exact; it ends the closure once
+// its eligibility test also used that exact minret. Seeded with the parent's
+// minret. Only advancing chains load a record.
+template <int NQ>
+__device__ __forceinline__ int lv_closure(LvHot (&H)[NQ], uint32_t (&d)[NQ], const uint32_t (&cnt)[NQ],
+                                          const uint32_t* s_cs, const LvHeadsLds<NQ>& PL, int lane, const State& s,
+                                          uint32_t hflags, uint32_t minret_seed, const OpRec* __restrict__ recs,
+                                          uint32_t& minret_out) {
+  const bool nowrap = hflags & H_NOWRAP;
+  const bool p2 = hflags & H_P2OK;
+  const bool p4 = hflags & H_P4;
+  uint32_t minret_prev = minret_seed;
+  for (;;) {
+    uint32_t mr = EV_INF;
+    uint64_t bd = REQ_NONE;
+    uint32_t adv = 0;
+    bool dead = false;
+#pragma unroll
+    for (int q = 0; q < NQ; ++q) {
+      const LvHot& h = H[q];
+      mr = min(mr, h.ret);
+      bd = lv_min64(bd, h.suf);
+      if (!(h.fl & OPF_CLS_E) || h.call >= minret_prev) continue;
+      uint32_t bits = h.fl;
+      if (!(bits & HB_KNOWN)) bits = lv_legal_bits(h.fl, PL.otail[q][lane], PL.ohash[q][lane], s);
+      if (bits & HB_LEGAL) adv |= 1u << q;
+      else if (p2 && (bits & HB_P2DEAD)) dead = true;
+    }
+    const uint32_t minret = wave_min_u32(mr);
+    const uint64_t bound = wave_min_u64(bd);
+    if (__ballot(dead) || (nowrap && s.tail > bound)) return CL_DEAD;
+    const bool changed = __ballot(adv != 0) != 0;
+    if (!changed && minret == minret_prev) {
+      minret_out = minret;
+      return minret == EV_INF ? CL_COMPLETE : ((p4 && bound == REQ_NONE) ? CL_P4 : CL_ALIVE);
+    }
+#pragma unroll
+    for (int q = 0; q < NQ; ++q) {
+      if ((adv >> q) & 1u) {
+        d[q] += 1;
+        H[q] = lv_load_child_head(recs + s_cs[64 * q + lane] + cnt[q] + d[q], s);
       }
     }
-    const uint32_t base = wave_alloc(&p.ctl->nchild, nk);
-    if (nk) {
-      uint32_t q = base;
-      if (take_opt) {
-        if (q < p.ccap) p.child[q] = LChild{opt.tail, opt.hash, opt.tok, k, j, 0};
-        ++q;
-      }
-      if (take_id) {
-        if (q < p.ccap) p.child[q] = LChild{s.tail, s.hash, s.tok, k, j | MOVE_IDENT, 0};
-        ++q;
-      }
-      if (q > p.ccap) p.ctl->overflow = 1;
-    }
+    minret_prev = minret;
   }
 }
 
-// ---- close: one wave per child --------------------------------------------
-template <int KMAX>
-__global__ __launch_bounds__(LV_BLOCK) void lv_close(LvParams p) {
-  constexpr int NQ = KMAX / 64;
+// Stage one closed child into stripe `st` of the staging array; the wave
+// reserves LV_RESERVE slots of its stripe at a time (rk / rleft, wave-uniform).
+template <int NQ>
+__device__ __forceinline__ void lv_stage(const LvParams& p, uint32_t st, uint32_t& rk, uint32_t& rleft, const State& s,
+                                         uint64_t fp, uint32_t minret, uint32_t ptrace, uint32_t move,
+                                         const uint32_t (&cnt)[NQ], const uint32_t (&d)[NQ]) {
+  const int lane = (int)(threadIdx.x & 63);
+  if (rleft == 0) {
+    uint32_t b = 0;
+    if (lane == 0) b = atomicAdd(&p.ctl->cnt[16 * st], LV_RESERVE);
+    rk = (uint32_t)__shfl((int)b, 0, 64);
+    rleft = LV_RESERVE;
+  }
+  const uint32_t i = rk++;
+  rleft--;
+  if (i >= p.scs) {
+    if (lane == 0) atomicExch(&p.ctl->overflow, 1u);
+    return;
+  }
+  LCfg<NQ>* o = lv_cfg<NQ>(p.stg, st * p.scs + i);
+  if (lane == 0) {
+    o->tail = s.tail; o->hash = s.hash; o->fp = fp; o->tok = s.tok;
+    o->minret = minret; o->ptrace = ptrace; o->move = move;
+    o->trace = TRACE_NONE; o->slot = LV_NONE;
+  }
+#pragma unroll
+  for (int q = 0; q < NQ; ++q) o->cnt[lane + 64 * q] = (uint16_t)(cnt[q] + d[q]);
+}
+
+// Unused reserved slots become holes (lv_insert and the distributed kernels skip them).
+template <int NQ>
+__device__ __forceinline__ void lv_release(const LvParams& p, uint32_t st, uint32_t rk, uint32_t rleft) {
+  const int lane = (int)(threadIdx.x & 63);
+  for (uint32_t i = lane; i < rleft; i += 64)
+    if (rk + i < p.scs) lv_cfg<NQ>(p.stg, st * p.scs + rk + i)->move = LV_HOLE;
+}
+
+// S2LC_PROF: per-phase cycle counts of lv_round (lane 0 of every wave, summed
+// into g_lvprof): [0] parent load, [1] heads + fingerprint, [2] move states,
+// [3] closures, [4] stage + restore, [5] items, [6] children, [7] closure passes
+#ifdef S2LC_PROF
+#define LV_T0() lv_t = clock64()
+#define LV_LAP(i) do { const unsigned long long t_ = clock64(); lv_acc[i] += t_ - lv_t; lv_t = t_; } while (0)
+#define LV_ADD(i, v) lv_acc[i] += (v)
+#else
+#define LV_T0() do { } while (0)
+#define LV_LAP(i) do { } while (0)
+#define LV_ADD(i, v) do { } while (0)
+#endif
+
+// cnt[q] for a wave-uniform runtime slot q (a select chain, no scratch)
+template <int NQ>
+__device__ __forceinline__ uint32_t sel_cnt(const uint32_t (&cnt)[NQ], uint32_t q) {
+  uint32_t v = cnt[0];
+#pragma unroll
+  for (int i = 1; i < NQ; ++i) v = q == (uint32_t)i ? cnt[i] : v;
+  return v;
+}
+
+// ---- round: one wave per (frontier configuration, slice of its candidates) --
+template <int NQ>
+__global__ __launch_bounds__(LV_BLOCK) void lv_round(LvParams p) {
+  if (p.run && p.run->done) return;  // the search ended in an earlier round of this batch
+  if (p.ctl_next && blockIdx.x == 0)
+    for (uint32_t i = threadIdx.x; i < sizeof(LvCtl) / 4; i += LV_BLOCK) reinterpret_cast<uint32_t*>(p.ctl_next)[i] = 0;
+  __shared__ LvHeadsLds<NQ> s_heads[LV_BLOCK / 64];
+  __shared__ uint32_t s_cs[64 * NQ];  // chain starts (slot q of lane l = chain l + 64 q), shared by the block
+  LvHeadsLds<NQ>& PL = s_heads[threadIdx.x >> 6];
   const int lane = (int)(threadIdx.x & 63);
   const uint32_t K = p.K;
-  const bool nowrap = p.hflags & H_NOWRAP;
-  const bool p2 = p.hflags & H_P2OK;
-  const bool p4 = p.hflags & H_P4;
-  uint32_t csj[NQ];
-#pragma unroll
-  for (int q = 0; q < NQ; ++q) {
-    const uint32_t j = (uint32_t)lane + 64u * q;
-    csj[q] = j < K ? p.cs[j] : 0u;
-  }
-  const uint32_t nch = min(p.ctl->nchild, p.ccap);
+  const bool idefer = p.hflags & H_IDEFER;
+  for (uint32_t x = threadIdx.x; x < 64u * NQ; x += LV_BLOCK) s_cs[x] = x < K ? p.cs[x] : 0u;
+  __syncthreads();
+  uint32_t f0 = p.f0, f1 = p.f1;
+  if (f1 == LV_NONE) { f0 = 0; f1 = p.run->nf; }
+  const uint32_t nf = p.init ? 1u : f1 - f0;
   const uint32_t nwaves = gridDim.x * (LV_BLOCK / 64);
-  for (uint32_t ci = blockIdx.x * (LV_BLOCK / 64) + (threadIdx.x >> 6); ci < nch; ci += nwaves) {
-    const LChild ch = p.child[ci];
-    const State s{ch.tail, ch.hash, ch.tok};
-    const LCfg<KMAX>* pc = ch.parent == LV_NONE ? nullptr : lv_cfg<KMAX>(p.cur, ch.parent);
-    const uint32_t mj = ch.move == LV_NONE ? LV_NONE : (ch.move & 0xFFFFu);
-    uint32_t cnt[NQ];
+  // Slices per configuration: narrow frontiers spread a configuration's moves
+  // over several waves (down to about one child per wave), wide ones give a
+  // wave whole configurations (the chip is full either way). The expected
+  // moves per configuration come from the previous round.
+  uint32_t c_est = p.K;
+  if (p.run && p.run->last_nf) c_est = (uint32_t)min<unsigned long long>(p.K, p.run->last_children / p.run->last_nf + 1);
+  const uint32_t S = p.init ? 1u : max(1u, min(c_est + (c_est >> 2) + 1, (2u * nwaves + nf - 1) / max(nf, 1u)));
+  const uint32_t items = nf * S;
+  uint32_t rk = 0, rleft = 0;  // reserved staging slots (wave-uniform)
+  const uint32_t wave_id = blockIdx.x * (LV_BLOCK / 64) + (threadIdx.x >> 6);
+  const uint32_t stripe = wave_id & (LV_STRIPES - 1);
+  if (wave_id < items) {  // the first reservation, in flight with the first item's loads
+    uint32_t b0 = 0;
+    if (lane == 0) b0 = atomicAdd(&p.ctl->cnt[16 * stripe], LV_RESERVE);
+    rk = (uint32_t)__shfl((int)b0, 0, 64);
+    rleft = LV_RESERVE;
+  }
+  unsigned long long kids = 0;
+#ifdef S2LC_PROF
+  unsigned long long lv_acc[8] = {0, 0, 0, 0, 0, 0, 0, 0}, lv_t = 0;
+#endif
+  for (uint32_t it = blockIdx.x * (LV_BLOCK / 64) + (threadIdx.x >> 6); it < items; it += nwaves) {
+    LV_T0();
+    LV_ADD(5, 1);
+    const uint32_t f = f0 + it / S;
+    const uint32_t slice = it % S;
+    // parent configuration (round 0: the all-zero initial one)
+    const LCfg<NQ>* pc = p.init ? nullptr : lv_cfg<NQ>(p.cur, p.cur_idx[f]);
+    State ps{0, 0, 0};
+    uint32_t pmin = 0, ptrace = TRACE_NONE;
+    if (pc) {
+      ps = State{pc->tail, pc->hash, pc->tok};
+      pmin = pc->minret;
+      ptrace = pc->trace;
+      if (slice == 0 && lane == 0 && p.clear_slots && pc->slot <= p.ht_mask) p.ht[pc->slot] = HT_EMPTY;
+    }
+    uint32_t cnt[NQ], d[NQ];
+    LvHot H[NQ];
+    LV_LAP(0);
+    uint64_t chx = 0;  // this lane's part of the parent's chain fingerprint
+    uint32_t cand = 0;
 #pragma unroll
     for (int q = 0; q < NQ; ++q) {
       const uint32_t j = (uint32_t)lane + 64u * q;
       cnt[q] = (j < K && pc) ? (uint32_t)pc->cnt[j] : 0u;
-      if (j == mj) cnt[q] += 1;
+      d[q] = 0;
+      if (j < K) {
+        H[q] = lv_load_parent_head<NQ>(p.recs + s_cs[64 * q + lane] + cnt[q], PL, q, lane);
+      } else {
+        H[q] = lv_hot_null();
+        PL.fl[q][lane] = OPF_SENTINEL; PL.call[q][lane] = EV_INF; PL.ret[q][lane] = EV_INF; PL.suf[q][lane] = REQ_NONE;
+      }
+      if (j < K) chx ^= lv_chain_term(j, cnt[q]);
+      // candidate moves: minimal durable / indefinite appends at the chain heads
+      if (pc && !(H[q].fl & (OPF_SENTINEL | OPF_CLS_E)) && H[q].call < pmin) cand |= 1u << q;
     }
-    int res;
-    uint32_t minret;
-    // Head fields of the owned chains, kept in registers across passes: a pass
-    // reloads only the chains the previous pass advanced (the first pass loads
-    // every head), so the closure's L2 traffic is one head per chain plus one
-    // per advanced op instead of one per chain per pass.
-    uint32_t callv[NQ], flv[NQ], retv[NQ];
-    uint64_t otl[NQ], ohs[NQ], smv[NQ];
-    uint32_t need = (1u << NQ) - 1u;
+    const uint64_t parent_chx = wave_xor_u64(chx);
+    LV_LAP(1);
+    uint32_t n_cand = 0;
+#pragma unroll
+    for (int q = 0; q < NQ; ++q) n_cand += (uint32_t)__popcll(__ballot((cand >> q) & 1u));
+    // round 0 has one pseudo-move: the initial configuration itself
+    const uint32_t n_moves = pc ? n_cand : 1u;
+    const uint32_t c0 = (uint32_t)(((uint64_t)n_moves * slice) / S);
+    const uint32_t c1 = (uint32_t)(((uint64_t)n_moves * (slice + 1)) / S);
+    uint32_t ord = 0, q_cur = 0;
+    uint64_t m = pc ? __ballot(cand & 1u) : 1ull;
     for (;;) {
-      uint32_t mr = EV_INF;
-      uint64_t bd = REQ_NONE;
+      // next move (wave-uniform): slot q_cur, owner lane src
+      while (m == 0 && q_cur + 1 < (uint32_t)NQ && pc) {
+        ++q_cur;
+        m = __ballot((cand >> q_cur) & 1u);
+      }
+      if (m == 0 || ord >= c1) break;
+      const int src = __ffsll((unsigned long long)m) - 1;
+      m &= m - 1;
+      const uint32_t o = ord++;
+      if (o < c0) continue;
+      // children of the move: on the owner lane (round 0: the unchanged initial state)
+      bool take_opt = !pc, take_id = false;
+      State opt = ps;
+      uint4 nx_obs = make_uint4(0, 0, 0, 0), nx_mid = make_uint4(0, 0, 0, 0);
+      uint32_t nx_fl = 0;
+      if (pc && lane == src) {
+        // the move's record, and the chain's next head (the child's first new head) with it
+        const OpRec* mrec = p.recs + s_cs[64 * q_cur + lane] + sel_cnt<NQ>(cnt, q_cur);
+        const OpRec* nx = mrec + 1;
+        nx_obs = ld16(nx, 16);
+        nx_mid = ld16(nx, 32);
+        nx_fl = nx->flags;
+        const OpRec r = load_rec(mrec);
+        const bool g = append_guards_ok(r, ps);
+        opt.tail = ps.tail + r.num_records;
+        opt.tok = r.set_tok ? r.set_tok : ps.tok;
+        take_opt = (r.flags & OPF_CLS_D) ? (g && opt.tail == r.out_tail) : g;
+        if (take_opt || ((r.flags & OPF_CLS_I) && g)) opt.hash = fold_hashes_blk(ps.hash, p.pool + r.hash_off, r.hash_cnt);
+        if (r.flags & OPF_CLS_I) take_id = (!idefer || r.ret_ev == pmin) && !(g && state_eq(opt, ps));
+      }
+      const uint32_t fl2 = pc ? rl((take_opt ? 1u : 0u) | (take_id ? 2u : 0u), src) : 1u;
+      const State so{rl64(opt.tail, src), rl64(opt.hash, src), rl(opt.tok, src)};
+      const uint32_t j = (uint32_t)src + 64u * q_cur;
+      LV_LAP(2);
+#pragma unroll 1
+      for (int w = 0; w < 2; ++w) {
+        if (!((fl2 >> w) & 1u)) continue;
+        const State cs_ = w == 0 ? so : ps;
+        const uint32_t mv = !pc ? LV_NONE : (w == 0 ? j : (j | MOVE_IDENT));
+        if (pc) {
+          kids++;
 #pragma unroll
-      for (int q = 0; q < NQ; ++q) {
-        const uint32_t j = (uint32_t)lane + 64u * q;
-        if (j < K) {
-          if ((need >> q) & 1u) {
-            const OpRec* r = p.recs + csj[q] + cnt[q];
-            const uint4 obs = ld16(r, 16);
-            const uint4 mid = ld16(r, 32);
-            flv[q] = r->flags;
-            otl[q] = (uint64_t)obs.x | ((uint64_t)obs.y << 32);
-            ohs[q] = (uint64_t)obs.z | ((uint64_t)obs.w << 32);
-            callv[q] = mid.z;
-            retv[q] = mid.w;
-            smv[q] = (uint64_t)mid.x | ((uint64_t)mid.y << 32);
+          for (int q = 0; q < NQ; ++q)
+            if ((uint32_t)q == q_cur && lane == src) {
+              d[q] = 1;
+              H[q].suf = (uint64_t)nx_mid.x | ((uint64_t)nx_mid.y << 32);
+              H[q].call = nx_mid.z;
+              H[q].ret = nx_mid.w;
+              H[q].fl = nx_fl | HB_KNOWN |
+                        lv_legal_bits(nx_fl, (uint64_t)nx_obs.x | ((uint64_t)nx_obs.y << 32),
+                                      (uint64_t)nx_obs.z | ((uint64_t)nx_obs.w << 32), cs_);
+            }
+        }
+        uint32_t mr = 0;
+        LV_LAP(4);
+        LV_ADD(6, 1);
+        const int cr = lv_closure<NQ>(H, d, cnt, s_cs, PL, lane, cs_, p.hflags, pmin, p.recs, mr);
+        LV_LAP(3);
+        if (cr == CL_COMPLETE || cr == CL_P4) {
+          if (lane == 0 && atomicCAS(&p.ctl->found, 0u, 1u) == 0u) {
+            atomicExch(&p.ctl->found_parent, ptrace);
+            atomicExch(&p.ctl->found_move, mv);
+            atomicExch(&p.ctl->found_p4, cr == CL_P4 ? 1u : 0u);
           }
-          mr = min(mr, retv[q]);
-          bd = smv[q] < bd ? smv[q] : bd;
-        } else {
-          flv[q] = OPF_SENTINEL; otl[q] = 0; ohs[q] = 0; callv[q] = EV_INF; retv[q] = EV_INF; smv[q] = REQ_NONE;
+        } else if (cr == CL_ALIVE) {
+          uint64_t dx = 0;
+#pragma unroll
+          for (int q = 0; q < NQ; ++q) {
+            const uint32_t jj = (uint32_t)lane + 64u * q;
+            if (d[q]) dx ^= lv_chain_term(jj, cnt[q]) ^ lv_chain_term(jj, cnt[q] + d[q]);
+          }
+          const uint64_t fp = mix64(parent_chx ^ wave_xor_u64(dx) ^ lv_state_term(cs_.tail, cs_.hash, cs_.tok));
+          lv_stage<NQ>(p, stripe, rk, rleft, cs_, fp, mr, ptrace, mv, cnt, d);
         }
-      }
-      minret = wave_min_u32(mr);
-      const uint64_t bound = wave_min_u64(bd);
-      uint32_t adv = 0;
-      bool dead = false;
+        // back to the parent's heads on the chains this child advanced
 #pragma unroll
-      for (int q = 0; q < NQ; ++q) {
-        const uint32_t f = flv[q];
-        if (!(f & OPF_CLS_E) || callv[q] >= minret) continue;
-        bool legal = true;
-        if ((f & OPF_KIND_MASK) != 0) {
-          const bool hash_bad = (f & OPF_HAS_HASH) && s.hash != ohs[q];
-          const bool tail_bad = !(f & OPF_FAIL) && s.tail != otl[q];
-          legal = !hash_bad && !tail_bad;
-          // P2: a minimal successful read at this tail with another hash can never pass
-          if (p2 && hash_bad && !(f & OPF_FAIL) && otl[q] == s.tail) dead = true;
-        }
-        if (legal) adv |= 1u << q;
+        for (int q = 0; q < NQ; ++q)
+          if (d[q]) {
+            d[q] = 0;
+            H[q] = lv_parent_hot<NQ>(PL, q, lane);
+          }
       }
-      if (__ballot(dead) || (nowrap && s.tail > bound)) { res = CL_DEAD; break; }
-      if (!__ballot(adv != 0)) {
-        res = minret == EV_INF ? CL_COMPLETE : ((p4 && bound == REQ_NONE) ? CL_P4 : CL_ALIVE);
-        break;
-      }
-#pragma unroll
-      for (int q = 0; q < NQ; ++q) cnt[q] += (adv >> q) & 1u;
-      need = adv;
-    }
-    if (res == CL_DEAD) continue;
-    const uint32_t ptrace = pc ? pc->trace : TRACE_NONE;
-    if (res != CL_ALIVE) {
-      if (lane == 0 && atomicCAS(&p.ctl->found, 0u, 1u) == 0u) {
-        p.ctl->found_parent = ptrace;
-        p.ctl->found_move = ch.move;
-        p.ctl->found_p4 = res == CL_P4;
-      }
-      continue;
-    }
-    uint64_t h = 0;
-#pragma unroll
-    for (int q = 0; q < NQ; ++q) {
-      const uint32_t j = (uint32_t)lane + 64u * q;
-      if (j < K) h ^= lv_chain_term(j, cnt[q]);
-    }
-    const uint64_t fp = mix64(wave_xor_u64(h) ^ lv_state_term(s.tail, s.hash, s.tok));
-    uint32_t k = 0;
-    if (lane == 0) k = atomicAdd(&p.ctl->nstage, 1u);
-    k = (uint32_t)__shfl((int)k, 0, 64);
-    if (k >= p.scap) {
-      if (lane == 0) p.ctl->overflow = 2;
-      continue;
-    }
-    LCfg<KMAX>* o = lv_cfg<KMAX>(p.stg, k);
-    if (lane == 0) {
-      o->tail = s.tail; o->hash = s.hash; o->fp = fp; o->tok = s.tok;
-      o->minret = minret; o->ptrace = ptrace; o->move = ch.move;
-      o->trace = TRACE_NONE; o->slot = LV_NONE;
-    }
-#pragma unroll
-    for (int q = 0; q < NQ; ++q) {
-      const uint32_t j = (uint32_t)lane + 64u * q;
-      o->cnt[j] = j < K ? (uint16_t)cnt[q] : (uint16_t)0;
     }
   }
+#ifdef S2LC_PROF
+  if (lane == 0 && p.prof)
+    for (int i_ = 0; i_ < 8; ++i_) atomicAdd(&p.prof[i_], lv_acc[i_]);
+#endif
+  if (rleft) lv_release<NQ>(p, stripe, rk, rleft);
+  if (lane == 0 && kids) atomicAdd(&p.ctl->children, kids);
 }
 
-template <int KMAX>
-__device__ __forceinline__ bool lv_eq(const LCfg<KMAX>* a, const LCfg<KMAX>* b, uint32_t K) {
+template <int NQ>
+__device__ __forceinline__ bool lv_eq(const LCfg<NQ>* a, const LCfg<NQ>* b, uint32_t K) {
   if (a->tail != b->tail || a->hash != b->hash || a->tok != b->tok) return false;
   const uint4* x = reinterpret_cast<const uint4*>(a->cnt);
   const uint4* y = reinterpret_cast<const uint4*>(b->cnt);
@@ -362,56 +606,155 @@ __device__ __forceinline__ bool lv_eq(const LCfg<KMAX>* a, const LCfg<KMAX>* b, 
   return true;
 }
 
+// The last block of lv_insert closes the round on the device: per-round
+// count, run counters, and the decision (found / empty / budget / overflow /
+// witness off), then publishes the run state to the host-mapped mirror.
+__device__ __forceinline__ void lv_close_round(const LvParams& p) {
+  // every counter of the round was written by device-scope atomics: read them
+  // as such (no fence needed between the blocks and this closer); the loads
+  // are independent and issued together
+  LvRun* R = p.run;
+  LvCtl* c = p.ctl;
+  const uint32_t nn = ld_agent(&c->nnext);
+  const uint32_t ovf = ld_agent(&c->overflow);
+  const uint32_t fnd = ld_agent(&c->found);
+  const uint32_t fpar = ld_agent(&c->found_parent), fmov = ld_agent(&c->found_move), fp4 = ld_agent(&c->found_p4);
+  const unsigned long long ch = ld_agent64(&c->children);
+  const uint32_t rnd = p.round;
+  R->children += ch;
+  R->last_nf = rnd == 0 ? 0u : R->nf;
+  R->last_children = ch;
+  if (ovf) {
+    R->done = LVR_OVERFLOW;  // the host re-runs this round in frontier chunks
+  } else if (fnd) {
+    R->done = LVR_FOUND;
+    R->round = rnd;
+    R->found_parent = R->witness ? fpar : TRACE_NONE;
+    R->found_move = fmov;
+    R->found_p4 = fp4;
+  } else {
+    if (p.rcounts) p.rcounts[rnd] = nn;
+    R->round = rnd;
+    if (nn == 0) {
+      R->done = LVR_EMPTY;
+      if (rnd > 0 && R->witness) { R->deep_trace = R->last_tbase; R->deep_len = rnd - 1; }
+    } else {
+      R->nf = nn;
+      R->max_frontier = max(R->max_frontier, nn);
+      R->configs += nn;
+      if (R->witness) {
+        R->last_tbase = (uint32_t)R->tnext;
+        R->tnext += nn;
+        if (R->tnext + p.scap > p.trace_cap) R->witness = 0;
+      }
+      if (R->max_configs && R->configs > R->max_configs) R->done = LVR_BUDGET;
+    }
+  }
+  // host-mapped mirror: only when the host will look (the last round of a
+  // batch, or the end of the search) -- every word is a write over the link
+  if (p.publish && (p.publish_always || R->done)) {
+    const uint32_t* src = reinterpret_cast<const uint32_t*>(R);
+    volatile uint32_t* dst = reinterpret_cast<volatile uint32_t*>(p.publish);
+    for (uint32_t i = 0; i < sizeof(LvRun) / 4; ++i) dst[i] = src[i];
+    __threadfence_system();
+  }
+}
+
 // ---- insert: one lane per staged configuration -----------------------------
-template <int KMAX>
+// Striped staging: lane l of every wave walks stripe l (slot l * scs + i for
+// i = lo[l] .. cnt[l]); the grid strides over i. Winners take next-frontier
+// positions with one atomic per block.
+template <int NQ>
 __global__ __launch_bounds__(LV_BLOCK) void lv_insert(LvParams p) {
-  const uint32_t hi = p.ctl->overflow ? 0u : min(p.ctl->nstage, p.scap);
-  const uint32_t stride = gridDim.x * LV_BLOCK;
-  for (uint32_t b0 = p.st_lo + blockIdx.x * LV_BLOCK; b0 < hi; b0 += stride) {
-    const uint32_t k = b0 + threadIdx.x;
+  if (p.run && p.run->done) return;
+  __shared__ uint32_t s_wcnt[LV_BLOCK / 64], s_base, s_hi, s_last;
+  const int lane = (int)(threadIdx.x & 63), wv = (int)(threadIdx.x >> 6);
+  const bool wit = p.run ? p.run->witness != 0 : p.witness_host != 0;
+  const uint32_t tbase = p.run ? (uint32_t)p.run->tnext : p.tbase_host;
+  uint32_t lo = 0, hi = 0;  // this lane's stripe range (striped mode)
+  if (p.dense) {
+    hi = p.dense;
+  } else if (!ld_agent(&p.ctl->overflow)) {
+    lo = p.ctl->lo[lane];
+    hi = min(ld_agent(&p.ctl->cnt[16 * lane]), p.scs);
+  }
+  // iterations: the longest stripe (striped) / the dense range, block-uniform
+  uint32_t n_it;
+  if (p.dense) {
+    n_it = (p.dense + LV_BLOCK - 1) / LV_BLOCK;
+  } else {
+    const uint32_t m = wave_max_u32(hi);
+    n_it = (m + LV_BLOCK / 64 - 1) / (LV_BLOCK / 64);  // rows of 4 slots per stripe per block iteration
+  }
+  for (uint32_t itb = blockIdx.x; itb < n_it; itb += gridDim.x) {
     bool win = false;
-    uint32_t slot = 0;
-    LCfg<KMAX>* c = nullptr;
-    if (k < hi) {
-      c = lv_cfg<KMAX>(p.stg, k);
-      const uint64_t fp = c->fp;
-      const uint32_t tag = (uint32_t)(fp >> 32);
-      const unsigned long long mine = ((unsigned long long)tag << 32) | k;
-      slot = (uint32_t)fp & p.ht_mask;
-      for (;;) {
-        const unsigned long long prev = atomicCAS(&p.ht[slot], HT_EMPTY, mine);
-        if (prev == HT_EMPTY) { win = true; break; }
-        if ((uint32_t)(prev >> 32) == tag && lv_eq<KMAX>(lv_cfg<KMAX>(p.stg, (uint32_t)prev), c, p.K)) break;
-        slot = (slot + 1) & p.ht_mask;
+    uint32_t slot = 0, k = 0;
+    LCfg<NQ>* c = nullptr;
+    bool valid;
+    if (p.dense) {
+      k = itb * LV_BLOCK + threadIdx.x;
+      valid = k < p.dense;
+    } else {
+      const uint32_t i = itb * (LV_BLOCK / 64) + (uint32_t)wv;
+      valid = i >= lo && i < hi;
+      k = (uint32_t)lane * p.scs + i;
+    }
+    if (valid) {
+      c = lv_cfg<NQ>(p.stg, k);
+      if (c->move != LV_HOLE) {
+        const uint64_t fp = c->fp;
+        const uint32_t tag = (uint32_t)(fp >> 32);
+        const unsigned long long mine = ((unsigned long long)tag << 32) | k;
+        slot = (uint32_t)fp & p.ht_mask;
+        for (;;) {
+          const unsigned long long prev = atomicCAS(&p.ht[slot], HT_EMPTY, mine);
+          if (prev == HT_EMPTY) { win = true; break; }
+          if ((uint32_t)(prev >> 32) == tag && lv_eq<NQ>(lv_cfg<NQ>(p.stg, (uint32_t)prev), c, p.K)) break;
+          slot = (slot + 1) & p.ht_mask;
+        }
       }
     }
-    const uint32_t n = wave_alloc(&p.ctl->nnext, win ? 1u : 0u);
+    // next-frontier positions: one atomic per block
+    const uint64_t bw = __ballot(win);
+    if (lane == 0) s_wcnt[wv] = (uint32_t)__popcll(bw);
+    __syncthreads();
+    if (threadIdx.x == 0) {
+      uint32_t t = 0;
+      for (int w = 0; w < LV_BLOCK / 64; ++w) t += s_wcnt[w];
+      s_base = t ? atomicAdd(&p.ctl->nnext, t) : 0u;
+    }
+    __syncthreads();
+    uint32_t n = s_base;
+    for (int w = 0; w < wv; ++w) n += s_wcnt[w];
+    n += (uint32_t)__popcll(bw & ((1ull << lane) - 1));
+    __syncthreads();  // s_wcnt / s_base are rewritten next iteration
     if (win) {
       p.nxt_idx[n] = k;
       c->slot = slot;
-      if (p.witness) {
-        c->trace = p.tgid + p.tbase + n;
-        p.trace[p.tbase + n] = TraceEnt{c->ptrace, c->move};
+      if (wit) {
+        c->trace = p.tgid + tbase + n;
+        p.trace[tbase + n] = TraceEnt{c->ptrace, c->move};
       }
     }
   }
-  // the last block to finish copies the control block to the host-mapped
-  // mirror: the host then needs no copy, only the stream sync
-  if (p.publish) {
-    __syncthreads();
-    __shared__ uint32_t s_last;
-    if (threadIdx.x == 0) {
-      __threadfence();
-      s_last = atomicAdd(&p.ctl->done_blocks, 1u) == gridDim.x - 1;
-    }
-    __syncthreads();
-    if (s_last && threadIdx.x < sizeof(LvCtl) / 4) {
-      __threadfence();
-      const uint32_t v = atomicAdd(reinterpret_cast<uint32_t*>(p.ctl) + threadIdx.x, 0u);
-      reinterpret_cast<volatile uint32_t*>(p.publish)[threadIdx.x] = v;
-      __threadfence_system();
-    }
-  }
+  (void)s_hi;
+  if (!p.close_round) return;
+  // the last block to finish closes the round (it only reads atomics: no fence)
+  __syncthreads();
+  if (threadIdx.x == 0) s_last = atomicAdd(&p.ctl->done_blocks, 1u) == gridDim.x - 1;
+  __syncthreads();
+  if (s_last && threadIdx.x == 0) lv_close_round(p);
+}
+
+// Round 0 setup on the device: the run state of a fresh search.
+__global__ __attribute__((unused)) void lv_run_init(LvRun* R, unsigned long long tnext, uint32_t witness,
+                                                    unsigned long long max_configs) {
+  if (threadIdx.x != 0 || blockIdx.x != 0) return;
+  R->done = LVR_RUNNING; R->round = 0; R->nf = 0; R->max_frontier = 0;
+  R->configs = 0; R->children = 0; R->tnext = tnext; R->max_configs = max_configs;
+  R->found_parent = TRACE_NONE; R->found_move = LV_NONE; R->found_p4 = 0;
+  R->witness = witness; R->deep_trace = TRACE_NONE; R->deep_len = 0; R->last_tbase = TRACE_NONE;
+  R->last_nf = 0; R->last_children = 0;
 }
 
 // ---- distributed: owner of a configuration ---------------------------------
@@ -420,34 +763,41 @@ __host__ __device__ __forceinline__ uint32_t lv_owner(uint64_t fp, uint32_t worl
   return (uint32_t)(((fp * 0xD6E8FEB86659FD93ull) >> 40) % world);
 }
 
-// one lane per staged configuration: owner bucket and position within it
-template <int KMAX>
+// Distributed staging walk: k -> stripe k & 63, index k >> 6, for k below
+// p.dense = 64 * (the longest stripe) (set by the host from the round's counters).
+// one lane per staging slot: owner bucket and position within it (LV_NONE for holes)
+template <int NQ>
 __global__ __launch_bounds__(LV_BLOCK) void lv_bucket(LvParams p) {
-  const uint32_t n = min(p.ctl->nstage, p.scap);
-  for (uint32_t k = blockIdx.x * LV_BLOCK + threadIdx.x; k < n; k += gridDim.x * LV_BLOCK) {
-    const uint32_t o = lv_owner(lv_cfg<KMAX>(p.stg, k)->fp, p.world);
+  for (uint32_t k = blockIdx.x * LV_BLOCK + threadIdx.x; k < p.dense; k += gridDim.x * LV_BLOCK) {
+    const uint32_t st = k & (LV_STRIPES - 1), i = k / LV_STRIPES, slot = st * p.scs + i;
+    if (i >= min(p.ctl->cnt[16 * st], p.scs)) continue;
+    const LCfg<NQ>* c = lv_cfg<NQ>(p.stg, slot);
+    if (c->move == LV_HOLE) { p.own_pos[slot] = LV_NONE; continue; }
+    const uint32_t o = lv_owner(c->fp, p.world);
     const uint32_t pos = atomicAdd(&p.own_cnt[o], 1u);
-    p.own_pos[k] = (o << 27) | pos;
+    p.own_pos[slot] = (o << 27) | pos;
   }
 }
 
 // one lane per 16-byte piece: copy staged configurations into their owner's bucket
-template <int KMAX>
+template <int NQ>
 __global__ __launch_bounds__(LV_BLOCK) void lv_scatter(LvParams p) {
-  constexpr uint32_t PER = sizeof(LCfg<KMAX>) / 16;
-  const uint32_t n = min(p.ctl->nstage, p.scap);
-  const uint64_t total = (uint64_t)n * PER;
-  for (uint64_t i = (uint64_t)blockIdx.x * LV_BLOCK + threadIdx.x; i < total; i += (uint64_t)gridDim.x * LV_BLOCK) {
-    const uint32_t k = (uint32_t)(i / PER), c = (uint32_t)(i % PER);
-    const uint32_t op = p.own_pos[k];
+  constexpr uint32_t PER = sizeof(LCfg<NQ>) / 16;
+  const uint64_t total = (uint64_t)p.dense * PER;
+  for (uint64_t x = (uint64_t)blockIdx.x * LV_BLOCK + threadIdx.x; x < total; x += (uint64_t)gridDim.x * LV_BLOCK) {
+    const uint32_t k = (uint32_t)(x / PER), c = (uint32_t)(x % PER);
+    const uint32_t st = k & (LV_STRIPES - 1), i = k / LV_STRIPES, slot = st * p.scs + i;
+    if (i >= min(p.ctl->cnt[16 * st], p.scs)) continue;
+    const uint32_t op = p.own_pos[slot];
+    if (op == LV_NONE) continue;
     const uint64_t dst = p.own_off[op >> 27] + (op & ((1u << 27) - 1));
-    const uint4* src = reinterpret_cast<const uint4*>(lv_cfg<KMAX>(p.stg, k));
-    reinterpret_cast<uint4*>(p.send + dst * sizeof(LCfg<KMAX>))[c] = src[c];
+    const uint4* src = reinterpret_cast<const uint4*>(lv_cfg<NQ>(p.stg, slot));
+    reinterpret_cast<uint4*>(p.send + dst * sizeof(LCfg<NQ>))[c] = src[c];
   }
 }
 
 // keep the frontier configurations this rank owns (replicated -> partitioned)
-template <int KMAX>
+template <int NQ>
 __global__ __launch_bounds__(LV_BLOCK) void lv_keep(LvParams p, uint32_t rank) {
   const uint32_t nf = p.f1;
   for (uint32_t b0 = blockIdx.x * LV_BLOCK; b0 < nf; b0 += gridDim.x * LV_BLOCK) {
@@ -456,7 +806,7 @@ __global__ __launch_bounds__(LV_BLOCK) void lv_keep(LvParams p, uint32_t rank) {
     bool mine = false;
     if (i < nf) {
       k = p.cur_idx[i];
-      mine = lv_owner(lv_cfg<KMAX>(p.cur, k)->fp, p.world) == rank;
+      mine = lv_owner(lv_cfg<NQ>(p.cur, k)->fp, p.world) == rank;
     }
     const uint32_t n = wave_alloc(&p.ctl->nnext, mine ? 1u : 0u);
     if (mine) p.nxt_idx[n] = k;
@@ -464,18 +814,18 @@ __global__ __launch_bounds__(LV_BLOCK) void lv_keep(LvParams p, uint32_t rank) {
 }
 
 // copy the frontier's configurations contiguously into p.send (16 B per lane)
-template <int KMAX>
+template <int NQ>
 __global__ __launch_bounds__(LV_BLOCK) void lv_gather_frontier(LvParams p) {
-  constexpr uint32_t PER = sizeof(LCfg<KMAX>) / 16;
+  constexpr uint32_t PER = sizeof(LCfg<NQ>) / 16;
   const uint64_t total = (uint64_t)p.f1 * PER;
   for (uint64_t i = (uint64_t)blockIdx.x * LV_BLOCK + threadIdx.x; i < total; i += (uint64_t)gridDim.x * LV_BLOCK) {
     const uint32_t f = (uint32_t)(i / PER), c = (uint32_t)(i % PER);
-    const uint4* src = reinterpret_cast<const uint4*>(lv_cfg<KMAX>(p.cur, p.cur_idx[f]));
-    reinterpret_cast<uint4*>(p.send + (uint64_t)f * sizeof(LCfg<KMAX>))[c] = src[c];
+    const uint4* src = reinterpret_cast<const uint4*>(lv_cfg<NQ>(p.cur, p.cur_idx[f]));
+    reinterpret_cast<uint4*>(p.send + (uint64_t)f * sizeof(LCfg<NQ>))[c] = src[c];
   }
 }
 
-__global__ void lv_iota(uint32_t* out, uint32_t n) {
+__global__ __attribute__((unused)) void lv_iota(uint32_t* out, uint32_t n) {
   for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) out[i] = i;
 }
 

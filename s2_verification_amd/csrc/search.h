@@ -62,20 +62,24 @@ struct SearchGeom {
 
 // Buffers of the device-wide level search (level.hip), reused across histories.
 struct LevelBufs {
-  uint32_t kmax = 0, scap = 0, ccap = 0, ht_mask = 0;
-  void* child = nullptr;
-  uint8_t* stg[2] = {nullptr, nullptr};
-  uint32_t* idx[2] = {nullptr, nullptr};
-  unsigned long long* ht = nullptr;
-  void* ctl = nullptr;
-  void* h_ctl = nullptr;  // pinned host mirror of the control block
-  size_t child_bytes = 0, stg_bytes[2] = {0, 0}, idx_bytes[2] = {0, 0}, ht_bytes = 0;
+  uint32_t nq = 0, scap = 0, ht_mask = 0;
+  uint8_t* stg[2] = {nullptr, nullptr};     // staging arrays (frontier of round r = staging of round r-1)
+  uint32_t* idx[2] = {nullptr, nullptr};    // frontier index lists
+  unsigned long long* ht = nullptr;         // dedupe table
+  void* ctl = nullptr;                      // LvCtl[2], double buffered by round
+  void* run = nullptr;                      // LvRun (device)
+  void* h_run = nullptr;                    // pinned host-mapped mirror of the run state
+  void* h_ctl = nullptr;                    // pinned host copy of a control block (chunked rounds)
+  hipEvent_t ev[2] = {nullptr, nullptr};
+  size_t stg_bytes[2] = {0, 0}, idx_bytes[2] = {0, 0}, ht_bytes = 0;
+  uint32_t grid_round = 0, grid_insert = 0, grid_nq = 0;  // persistent grids (for grid_nq)
 };
 
 struct LevelStats {
   double ms = 0;
   uint64_t rounds = 0, configs = 0, children = 0;
   uint32_t max_frontier = 0, histories = 0, chunk_retries = 0;
+  uint32_t syncs = 0;  // host synchronizations (one per batch of device-driven rounds)
 };
 
 // A batch of histories resident on one device. Every buffer is grown on
@@ -159,7 +163,7 @@ int device_fold(const uint64_t* seeds, const uint64_t* pool, size_t pool_len, co
 int batch_run(DevBatch& b, hipStream_t stream, const RunOpts& ro, RunStats& st, std::string& err);
 
 constexpr uint32_t LEVEL_KMAX = 512;  // most chains the level search handles
-uint32_t level_kmax(uint32_t K);
+uint32_t level_nq(uint32_t K);  // register slots per lane: ceil(K / 64)
 // deadline: steady-clock time in ns since epoch after which the search gives
 // Unknown (S2LC_R_TIMEOUT); 0 = none.
 int level_search(DevBatch& b, uint32_t h, hipStream_t st, const RunOpts& ro, int64_t deadline_ns, LevelStats& ls,
@@ -170,7 +174,7 @@ int64_t steady_ns();
 // One rank's part of the distributed level search of a single history.
 struct DistLevel {
   DevBatch b;                    // the history (one entry) + level buffers
-  uint32_t rank = 0, world = 1, K = 0, kmax = 0;
+  uint32_t rank = 0, world = 1, K = 0, nq = 0;
   size_t cb = 0;                 // bytes per configuration on the wire
   uint32_t* own_cnt = nullptr;
   uint32_t* own_pos = nullptr;
@@ -179,7 +183,7 @@ struct DistLevel {
   hipStream_t stream = nullptr;
   const uint8_t* cur = nullptr;  // current frontier: received buffer (caller-owned)
   int cur_sel = 0;               // index list of the current frontier: b.lv.idx[cur_sel]
-  uint32_t nf = 0, nstage = 0, round = 0;
+  uint32_t nf = 0, slot_hi = 0, round = 0;  // slot_hi: staging walk bound (64 x longest stripe)
   uint32_t found_parent = TRACE_NONE, found_move = TRACE_NONE, found_p4 = 0;
   uint64_t configs = 0, children = 0, max_frontier = 0;
   double ms = 0;

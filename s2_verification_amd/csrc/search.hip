@@ -500,11 +500,6 @@ int batch_run(DevBatch& b, hipStream_t stream, const RunOpts& ro, RunStats& st, 
     else st.n_overflow2 += (uint32_t)next.size();
     todo.swap(next);
   }
-  if (ro.round_counts) {
-    b.h_rcounts.resize(std::max<uint64_t>(b.moves_cap, 1));
-    HIPCHK(hipMemcpyAsync(b.h_rcounts.data(), b.rcounts, b.moves_cap * sizeof(uint32_t), hipMemcpyDeviceToHost, stream));
-    HIPCHK(hipStreamSynchronize(stream));
-  }
   // the device-wide level search, one history at a time: histories with more
   // than 128 chains and those whose frontier outgrew the workgroup passes
   todo.insert(todo.end(), level.begin(), level.end());
@@ -523,6 +518,10 @@ int batch_run(DevBatch& b, hipStream_t stream, const RunOpts& ro, RunStats& st, 
   }
   if (b.n_hist && (other_work || !(b.n_pack16 + b.n_pack32)))
     HIPCHK(hipMemcpyAsync(b.h_res, b.res, b.n_hist * sizeof(HistResult), hipMemcpyDeviceToHost, stream));
+  if (ro.round_counts) {  // every engine wrote its rounds' counts on the device
+    b.h_rcounts.resize(std::max<uint64_t>(b.moves_cap, 1));
+    HIPCHK(hipMemcpyAsync(b.h_rcounts.data(), b.rcounts, b.moves_cap * sizeof(uint32_t), hipMemcpyDeviceToHost, stream));
+  }
   HIPCHK(hipStreamSynchronize(stream));
   for (uint32_t i = 0; i < b.n_hist; ++i) {
     if (b.forced[i]) {
