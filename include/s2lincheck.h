@@ -265,6 +265,13 @@ typedef struct s2lc_batch_stats {
   uint64_t pack16_algo_bytes;/* algorithmic bytes of the histories it settled */
   uint32_t pack16_histories;
   uint32_t _pad1;
+  /* level search round modes: rounds run inside the persistent kernel, its
+   * launches, frontier-chunk re-runs after a staging overflow, host syncs */
+  uint64_t level_persist_rounds;
+  uint32_t level_persist_launches;
+  uint32_t level_chunk_retries;
+  uint32_t level_syncs;
+  uint32_t _pad2;
 } s2lc_batch_stats;
 int s2lc_batch_stats_get(const s2lc_batch* b, s2lc_batch_stats* out);
 /* With S2LC_F_ROUND_COUNTS: the unique-configuration count of each completed

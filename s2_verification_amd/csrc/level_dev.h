@@ -39,9 +39,14 @@ constexpr uint32_t LV_HOLE = 0xFFFFFFFEu;  // LCfg::move of a reserved, unused s
 constexpr int LV_BLOCK = 256;
 constexpr uint32_t LV_RESERVE = 8;          // staging slots a wave reserves per atomic
 
-// A staged / frontier configuration: 48 + 128 * NQ bytes.
+// A staged / frontier configuration: 128 + 128 * NQ bytes. The header fills
+// one 128-byte line and every 64-counter block another, so no two
+// configurations share a line: the persistent kernel hands a freshly staged
+// configuration to another workgroup inside the launch (write-through stores,
+// then the table CAS), and a reader must never have pulled a neighbour's
+// not-yet-written bytes into its caches.
 template <int NQ>
-struct __attribute__((aligned(16))) LCfg {
+struct __attribute__((aligned(128))) LCfg {
   uint64_t tail;
   uint64_t hash;
   uint64_t fp;      // fingerprint (dedupe / ownership)
@@ -51,9 +56,11 @@ struct __attribute__((aligned(16))) LCfg {
   uint32_t move;    // chain | MOVE_IDENT; LV_NONE initial configuration; LV_HOLE unused slot
   uint32_t trace;   // own trace id once in a frontier
   uint32_t slot;    // table slot (cleared when this configuration is expanded)
+  uint32_t _pad[20];
   uint16_t cnt[64 * NQ];
 };
 static_assert(offsetof(LCfg<1>, trace) == 40, "LCfg::trace offset");
+static_assert(offsetof(LCfg<1>, cnt) == 128 && sizeof(LCfg<5>) == 128 * 6, "LCfg line layout");
 
 // Per-round device counters (double buffered by round parity). Staging is
 // split into LV_STRIPES stripes with a counter each, 64 bytes apart: a single
@@ -67,7 +74,8 @@ struct LvCtl {
   uint32_t done_blocks;  // lv_insert blocks finished (the last one closes the round)
   uint32_t found_parent, found_move, found_p4, _p0;
   unsigned long long children;  // children generated this round
-  uint32_t _pad[6];
+  unsigned long long prof_end;  // S2LC_PROF: latest expansion end of the round (wall clock)
+  uint32_t _pad[4];
   uint32_t lo[LV_STRIPES];        // lv_insert: first slot of each stripe not inserted yet (chunked rounds)
   uint32_t cnt[LV_STRIPES * 16];  // stripe s reserves slots at cnt[16 s] (holes included)
 };
@@ -82,7 +90,7 @@ __device__ __forceinline__ unsigned long long ld_agent64(const unsigned long lon
 
 // State of one level search, kept on the device across rounds and published
 // to host-mapped memory by the last lv_insert block of every round.
-enum : uint32_t { LVR_RUNNING = 0, LVR_FOUND = 1, LVR_EMPTY = 2, LVR_BUDGET = 3, LVR_OVERFLOW = 4 };
+enum : uint32_t { LVR_RUNNING = 0, LVR_FOUND = 1, LVR_EMPTY = 2, LVR_BUDGET = 3, LVR_OVERFLOW = 4, LVR_ABORT = 5 };
 struct LvRun {
   uint32_t done;           // LVR_*
   uint32_t round;          // expansion rounds completed (round 0 = the initial closure)
@@ -119,7 +127,8 @@ struct LvParams {
   uint32_t scap;
   uint32_t scs;          // staging slots per stripe (scap / LV_STRIPES); slot = stripe * scs + index
   uint32_t dense;        // lv_insert: a dense input of this many configurations (distributed receive), else striped
-  unsigned long long* ht;
+  unsigned long long* ht;        // this round's table (the staged configurations are inserted here)
+  unsigned long long* ht_clear;  // the table holding the expanded frontier's slots (round parity)
   uint32_t ht_mask;
   uint32_t clear_slots;  // lv_round clears the table slots of the frontier it expands
   uint32_t init;         // lv_round: round 0 (close the initial configuration)
@@ -393,12 +402,15 @@ __device__ __forceinline__ void lv_release(const LvParams& p, uint32_t st, uint3
     if (rk + i < p.scs) lv_cfg<NQ>(p.stg, st * p.scs + rk + i)->move = LV_HOLE;
 }
 
-// S2LC_PROF: per-phase cycle counts of lv_round (lane 0 of every wave, summed
-// into g_lvprof): [0] parent load, [1] heads + fingerprint, [2] move states,
-// [3] closures, [4] stage + restore, [5] items, [6] children, [7] closure passes
+// S2LC_PROF: per-phase cycle counts of lv_expand (lane 0 of every wave, summed
+// into p.prof by the waves that had items; every lap first waits for the
+// wave's outstanding loads): [0] parent load, [1] heads + fingerprint, [2]
+// move states, [3] closures, [4] stage (+ insert) + restore, [5] items, [6]
+// children, [12] move selection, [13] move record loads (the rest of [2] is
+// the hash fold). [9..11]: persistent round timing (lv_persist).
 #ifdef S2LC_PROF
 #define LV_T0() lv_t = clock64()
-#define LV_LAP(i) do { const unsigned long long t_ = clock64(); lv_acc[i] += t_ - lv_t; lv_t = t_; } while (0)
+#define LV_LAP(i) do { asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); const unsigned long long t_ = clock64(); lv_acc[i] += t_ - lv_t; lv_t = t_; } while (0)
 #define LV_ADD(i, v) lv_acc[i] += (v)
 #else
 #define LV_T0() do { } while (0)
@@ -415,31 +427,127 @@ __device__ __forceinline__ uint32_t sel_cnt(const uint32_t (&cnt)[NQ], uint32_t 
   return v;
 }
 
-// ---- round: one wave per (frontier configuration, slice of its candidates) --
+typedef __attribute__((address_space(1))) uint16_t lv_g16;
+typedef __attribute__((address_space(1))) uint32_t lv_g32;
+typedef __attribute__((address_space(1))) unsigned long long lv_g64;
+// write-through (agent-scope) stores and loads: the hand-off forms of the
+// persistent kernel (a configuration staged by one workgroup is compared by
+// another inside the same round)
+__device__ __forceinline__ void st_wt16(uint16_t* p, uint16_t v) {
+  __hip_atomic_store((lv_g16*)p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ void st_wt32(uint32_t* p, uint32_t v) {
+  __hip_atomic_store((lv_g32*)p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ void st_wt64(void* p, unsigned long long v) {
+  __hip_atomic_store((lv_g64*)p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ uint16_t ld_wt16(const uint16_t* p) {
+  return __hip_atomic_load((lv_g16*)p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ unsigned long long ld_wt64(const void* p) {
+  return __hip_atomic_load((lv_g64*)p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ void lv_drain() { asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); }
+
+// What one round's expansion takes besides LvParams: the frontier range, the
+// slices per configuration, and (fused insert) the round's trace base.
+struct LvRoundIn {
+  uint32_t f0, nf;  // frontier positions [f0, f0 + nf) of cur_idx (init: the initial configuration)
+  uint32_t S;       // slices per configuration
+  uint32_t tbase;   // trace index of the round's first winner (fused insert)
+  uint32_t wit;     // record trace entries (fused insert)
+};
+
+// Slices per configuration: narrow frontiers spread a configuration's moves
+// over several waves (down to about one child per wave), wide ones give a wave
+// whole configurations. The expected moves per configuration come from the
+// previous round.
+__device__ __forceinline__ uint32_t lv_slices(uint32_t K, uint32_t nf, uint32_t nwaves, uint32_t last_nf,
+                                              unsigned long long last_children) {
+  uint32_t c_est = K;
+  if (last_nf) c_est = (uint32_t)min<unsigned long long>(K, last_children / last_nf + 1);
+  return max(1u, min(c_est + (c_est >> 2) + 1, (2u * nwaves + nf - 1) / max(nf, 1u)));
+}
+
+// Persistent kernel: stage one closed child with write-through stores and
+// insert it at once (the producing wave deduplicates its own child: a 64-bit
+// CAS, and on a tag hit a wave-parallel compare against the resident entry).
 template <int NQ>
-__global__ __launch_bounds__(LV_BLOCK) void lv_round(LvParams p) {
-  if (p.run && p.run->done) return;  // the search ended in an earlier round of this batch
-  if (p.ctl_next && blockIdx.x == 0)
-    for (uint32_t i = threadIdx.x; i < sizeof(LvCtl) / 4; i += LV_BLOCK) reinterpret_cast<uint32_t*>(p.ctl_next)[i] = 0;
-  __shared__ LvHeadsLds<NQ> s_heads[LV_BLOCK / 64];
-  __shared__ uint32_t s_cs[64 * NQ];  // chain starts (slot q of lane l = chain l + 64 q), shared by the block
-  LvHeadsLds<NQ>& PL = s_heads[threadIdx.x >> 6];
+__device__ __forceinline__ void lv_stage_insert(const LvParams& p, const LvRoundIn& in, uint32_t st, uint32_t& rk,
+                                                uint32_t& rleft, const State& s, uint64_t fp, uint32_t minret,
+                                                uint32_t ptrace, uint32_t move, const uint32_t (&cnt)[NQ],
+                                                const uint32_t (&d)[NQ]) {
+  const int lane = (int)(threadIdx.x & 63);
+  if (rleft == 0) {
+    uint32_t b = 0;
+    if (lane == 0) b = atomicAdd(&p.ctl->cnt[16 * st], LV_RESERVE);
+    rk = rl(b, 0);
+    rleft = LV_RESERVE;
+  }
+  const uint32_t i = rk++;
+  rleft--;
+  if (i >= p.scs) {
+    if (lane == 0) atomicExch(&p.ctl->overflow, 1u);
+    return;
+  }
+  const uint32_t k = st * p.scs + i;
+  LCfg<NQ>* o = lv_cfg<NQ>(p.stg, k);
+  // the header line: lanes 0..15 store one 8-byte word each (one whole-line store)
+  const unsigned long long w = lane == 0 ? s.tail
+                             : lane == 1 ? s.hash
+                             : lane == 2 ? fp
+                             : lane == 3 ? ((unsigned long long)minret << 32 | s.tok)
+                             : lane == 4 ? ((unsigned long long)move << 32 | ptrace)
+                             : lane == 5 ? ((unsigned long long)LV_NONE << 32 | TRACE_NONE)
+                                         : 0ull;
+  if (lane < 16) st_wt64(reinterpret_cast<unsigned long long*>(o) + lane, w);
+#pragma unroll
+  for (int q = 0; q < NQ; ++q) st_wt16(&o->cnt[lane + 64 * q], (uint16_t)(cnt[q] + d[q]));
+  lv_drain();  // the child is in memory before the CAS can hand it to another wave
+  const uint32_t tag = (uint32_t)(fp >> 32);
+  const unsigned long long mine = ((unsigned long long)tag << 32) | k;
+  uint32_t slot = (uint32_t)fp & p.ht_mask;
+  for (;;) {
+    unsigned long long prev = 0;
+    if (lane == 0) prev = atomicCAS(&p.ht[slot], HT_EMPTY, mine);
+    prev = rl64(prev, 0);
+    if (prev == HT_EMPTY) break;
+    if ((uint32_t)(prev >> 32) == tag) {
+      const LCfg<NQ>* e = lv_cfg<NQ>(p.stg, (uint32_t)prev);
+      const unsigned long long et = ld_wt64(&e->tail), eh = ld_wt64(&e->hash), ek = ld_wt64(&e->tok);
+      bool ne = et != s.tail || eh != s.hash || (uint32_t)ek != s.tok;
+#pragma unroll
+      for (int q = 0; q < NQ; ++q) ne |= ld_wt16(&e->cnt[lane + 64 * q]) != (uint16_t)(cnt[q] + d[q]);
+      if (__ballot(ne) == 0) return;  // an equal configuration is already in the round
+    }
+    slot = (slot + 1) & p.ht_mask;
+  }
+  // the winner: next-frontier position, table slot, trace entry
+  uint32_t n = 0;
+  if (lane == 0) n = atomicAdd(&p.ctl->nnext, 1u);
+  n = rl(n, 0);
+  if (lane == 0) {
+    st_wt32(&p.nxt_idx[n], k);
+    st_wt32(&o->slot, slot);
+    if (in.wit) {
+      st_wt32(&o->trace, p.tgid + in.tbase + n);
+      p.trace[in.tbase + n] = TraceEnt{ptrace, move};
+    }
+  }
+}
+
+// ---- expansion: one wave per (frontier configuration, slice of its candidates)
+// FUSED = false: stage into the striped staging array (lv_insert deduplicates);
+// FUSED = true: the persistent kernel's stage-and-insert.
+template <int NQ, bool FUSED>
+__device__ __forceinline__ bool lv_expand(const LvParams& p, const LvRoundIn& in, LvHeadsLds<NQ>& PL,
+                                          const uint32_t* s_cs) {
   const int lane = (int)(threadIdx.x & 63);
   const uint32_t K = p.K;
   const bool idefer = p.hflags & H_IDEFER;
-  for (uint32_t x = threadIdx.x; x < 64u * NQ; x += LV_BLOCK) s_cs[x] = x < K ? p.cs[x] : 0u;
-  __syncthreads();
-  uint32_t f0 = p.f0, f1 = p.f1;
-  if (f1 == LV_NONE) { f0 = 0; f1 = p.run->nf; }
-  const uint32_t nf = p.init ? 1u : f1 - f0;
+  const uint32_t f0 = in.f0, nf = in.nf, S = in.S;
   const uint32_t nwaves = gridDim.x * (LV_BLOCK / 64);
-  // Slices per configuration: narrow frontiers spread a configuration's moves
-  // over several waves (down to about one child per wave), wide ones give a
-  // wave whole configurations (the chip is full either way). The expected
-  // moves per configuration come from the previous round.
-  uint32_t c_est = p.K;
-  if (p.run && p.run->last_nf) c_est = (uint32_t)min<unsigned long long>(p.K, p.run->last_children / p.run->last_nf + 1);
-  const uint32_t S = p.init ? 1u : max(1u, min(c_est + (c_est >> 2) + 1, (2u * nwaves + nf - 1) / max(nf, 1u)));
   const uint32_t items = nf * S;
   uint32_t rk = 0, rleft = 0;  // reserved staging slots (wave-uniform)
   const uint32_t wave_id = blockIdx.x * (LV_BLOCK / 64) + (threadIdx.x >> 6);
@@ -447,14 +555,14 @@ __global__ __launch_bounds__(LV_BLOCK) void lv_round(LvParams p) {
   if (wave_id < items) {  // the first reservation, in flight with the first item's loads
     uint32_t b0 = 0;
     if (lane == 0) b0 = atomicAdd(&p.ctl->cnt[16 * stripe], LV_RESERVE);
-    rk = (uint32_t)__shfl((int)b0, 0, 64);
+    rk = rl(b0, 0);
     rleft = LV_RESERVE;
   }
   unsigned long long kids = 0;
 #ifdef S2LC_PROF
-  unsigned long long lv_acc[8] = {0, 0, 0, 0, 0, 0, 0, 0}, lv_t = 0;
+  unsigned long long lv_acc[10] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0}, lv_t = 0;
 #endif
-  for (uint32_t it = blockIdx.x * (LV_BLOCK / 64) + (threadIdx.x >> 6); it < items; it += nwaves) {
+  for (uint32_t it = wave_id; it < items; it += nwaves) {
     LV_T0();
     LV_ADD(5, 1);
     const uint32_t f = f0 + it / S;
@@ -467,7 +575,8 @@ __global__ __launch_bounds__(LV_BLOCK) void lv_round(LvParams p) {
       ps = State{pc->tail, pc->hash, pc->tok};
       pmin = pc->minret;
       ptrace = pc->trace;
-      if (slice == 0 && lane == 0 && p.clear_slots && pc->slot <= p.ht_mask) p.ht[pc->slot] = HT_EMPTY;
+      if (slice == 0 && lane == 0 && p.clear_slots && pc->slot <= p.ht_mask)
+        st_wt64(&p.ht_clear[pc->slot], HT_EMPTY);
     }
     uint32_t cnt[NQ], d[NQ];
     LvHot H[NQ];
@@ -516,6 +625,7 @@ __global__ __launch_bounds__(LV_BLOCK) void lv_round(LvParams p) {
       State opt = ps;
       uint4 nx_obs = make_uint4(0, 0, 0, 0), nx_mid = make_uint4(0, 0, 0, 0);
       uint32_t nx_fl = 0;
+      LV_LAP(7);
       if (pc && lane == src) {
         // the move's record, and the chain's next head (the child's first new head) with it
         const OpRec* mrec = p.recs + s_cs[64 * q_cur + lane] + sel_cnt<NQ>(cnt, q_cur);
@@ -525,6 +635,7 @@ __global__ __launch_bounds__(LV_BLOCK) void lv_round(LvParams p) {
         nx_fl = nx->flags;
         const OpRec r = load_rec(mrec);
         const bool g = append_guards_ok(r, ps);
+        LV_LAP(8);
         opt.tail = ps.tail + r.num_records;
         opt.tok = r.set_tok ? r.set_tok : ps.tok;
         take_opt = (r.flags & OPF_CLS_D) ? (g && opt.tail == r.out_tail) : g;
@@ -573,7 +684,10 @@ __global__ __launch_bounds__(LV_BLOCK) void lv_round(LvParams p) {
             if (d[q]) dx ^= lv_chain_term(jj, cnt[q]) ^ lv_chain_term(jj, cnt[q] + d[q]);
           }
           const uint64_t fp = mix64(parent_chx ^ wave_xor_u64(dx) ^ lv_state_term(cs_.tail, cs_.hash, cs_.tok));
-          lv_stage<NQ>(p, stripe, rk, rleft, cs_, fp, mr, ptrace, mv, cnt, d);
+          if (FUSED)
+            lv_stage_insert<NQ>(p, in, stripe, rk, rleft, cs_, fp, mr, ptrace, mv, cnt, d);
+          else
+            lv_stage<NQ>(p, stripe, rk, rleft, cs_, fp, mr, ptrace, mv, cnt, d);
         }
         // back to the parent's heads on the chains this child advanced
 #pragma unroll
@@ -586,11 +700,34 @@ __global__ __launch_bounds__(LV_BLOCK) void lv_round(LvParams p) {
     }
   }
 #ifdef S2LC_PROF
-  if (lane == 0 && p.prof)
-    for (int i_ = 0; i_ < 8; ++i_) atomicAdd(&p.prof[i_], lv_acc[i_]);
+  if (lane == 0 && p.prof && lv_acc[5])  // only waves that had work (idle waves would swamp the counters)
+    for (int i_ = 0; i_ < 9; ++i_) atomicAdd(&p.prof[i_ < 7 ? i_ : i_ + 5], lv_acc[i_]);
 #endif
-  if (rleft) lv_release<NQ>(p, stripe, rk, rleft);
+  if (!FUSED && rleft) lv_release<NQ>(p, stripe, rk, rleft);
   if (lane == 0 && kids) atomicAdd(&p.ctl->children, kids);
+  return wave_id < items;
+}
+
+// ---- round kernel (host-enqueued rounds): expand + close + stage ----------
+template <int NQ>
+__global__ __launch_bounds__(LV_BLOCK) void lv_round(LvParams p) {
+  if (p.run && p.run->done) return;  // the search ended in an earlier round of this batch
+  if (p.ctl_next && blockIdx.x == 0)
+    for (uint32_t i = threadIdx.x; i < sizeof(LvCtl) / 4; i += LV_BLOCK) reinterpret_cast<uint32_t*>(p.ctl_next)[i] = 0;
+  __shared__ LvHeadsLds<NQ> s_heads[LV_BLOCK / 64];
+  __shared__ uint32_t s_cs[64 * NQ];  // chain starts (slot q of lane l = chain l + 64 q), shared by the block
+  for (uint32_t x = threadIdx.x; x < 64u * NQ; x += LV_BLOCK) s_cs[x] = x < p.K ? p.cs[x] : 0u;
+  __syncthreads();
+  LvRoundIn in;
+  in.f0 = p.f0;
+  in.nf = p.f1 == LV_NONE ? p.run->nf : p.f1 - p.f0;
+  if (p.f1 == LV_NONE) in.f0 = 0;
+  if (p.init) in.nf = 1;
+  const uint32_t nwaves = gridDim.x * (LV_BLOCK / 64);
+  in.S = p.init ? 1u : lv_slices(p.K, in.nf, nwaves, p.run ? p.run->last_nf : 0u, p.run ? p.run->last_children : 0ull);
+  in.tbase = 0;
+  in.wit = 0;
+  lv_expand<NQ, false>(p, in, s_heads[threadIdx.x >> 6], s_cs);
 }
 
 template <int NQ>
@@ -606,58 +743,74 @@ __device__ __forceinline__ bool lv_eq(const LCfg<NQ>* a, const LCfg<NQ>* b, uint
   return true;
 }
 
-// The last block of lv_insert closes the round on the device: per-round
-// count, run counters, and the decision (found / empty / budget / overflow /
-// witness off), then publishes the run state to the host-mapped mirror.
-__device__ __forceinline__ void lv_close_round(const LvParams& p) {
-  // every counter of the round was written by device-scope atomics: read them
-  // as such (no fence needed between the blocks and this closer); the loads
-  // are independent and issued together
-  LvRun* R = p.run;
-  LvCtl* c = p.ctl;
-  const uint32_t nn = ld_agent(&c->nnext);
-  const uint32_t ovf = ld_agent(&c->overflow);
-  const uint32_t fnd = ld_agent(&c->found);
-  const uint32_t fpar = ld_agent(&c->found_parent), fmov = ld_agent(&c->found_move), fp4 = ld_agent(&c->found_p4);
-  const unsigned long long ch = ld_agent64(&c->children);
-  const uint32_t rnd = p.round;
-  R->children += ch;
-  R->last_nf = rnd == 0 ? 0u : R->nf;
-  R->last_children = ch;
-  if (ovf) {
-    R->done = LVR_OVERFLOW;  // the host re-runs this round in frontier chunks
-  } else if (fnd) {
-    R->done = LVR_FOUND;
-    R->round = rnd;
-    R->found_parent = R->witness ? fpar : TRACE_NONE;
-    R->found_move = fmov;
-    R->found_p4 = fp4;
+// A round's counters, read by the closer (every word was written by
+// device-scope atomics: read as such, issued together).
+struct LvCounts {
+  uint32_t nn, ovf, fnd, fpar, fmov, fp4;
+  unsigned long long ch;
+};
+__device__ __forceinline__ LvCounts lv_read_counts(LvCtl* c) {
+  LvCounts k;
+  k.nn = ld_agent(&c->nnext);
+  k.ovf = ld_agent(&c->overflow);
+  k.fnd = ld_agent(&c->found);
+  k.fpar = ld_agent(&c->found_parent);
+  k.fmov = ld_agent(&c->found_move);
+  k.fp4 = ld_agent(&c->found_p4);
+  k.ch = ld_agent64(&c->children);
+  return k;
+}
+
+// Close round `rnd` on the run state R: per-round count, run counters, and
+// the decision (found / empty / budget / overflow / witness off).
+__device__ __forceinline__ void lv_close_state(LvRun& R, const LvCounts& k, uint32_t rnd, uint32_t* rcounts,
+                                               uint32_t scap, uint64_t trace_cap) {
+  R.children += k.ch;
+  R.last_nf = rnd == 0 ? 0u : R.nf;
+  R.last_children = k.ch;
+  if (k.ovf) {
+    R.done = LVR_OVERFLOW;  // the host re-runs this round in frontier chunks
+  } else if (k.fnd) {
+    R.done = LVR_FOUND;
+    R.round = rnd;
+    R.found_parent = R.witness ? k.fpar : TRACE_NONE;
+    R.found_move = k.fmov;
+    R.found_p4 = k.fp4;
   } else {
-    if (p.rcounts) p.rcounts[rnd] = nn;
-    R->round = rnd;
-    if (nn == 0) {
-      R->done = LVR_EMPTY;
-      if (rnd > 0 && R->witness) { R->deep_trace = R->last_tbase; R->deep_len = rnd - 1; }
+    if (rcounts) rcounts[rnd] = k.nn;
+    R.round = rnd;
+    if (k.nn == 0) {
+      R.done = LVR_EMPTY;
+      if (rnd > 0 && R.witness) { R.deep_trace = R.last_tbase; R.deep_len = rnd - 1; }
     } else {
-      R->nf = nn;
-      R->max_frontier = max(R->max_frontier, nn);
-      R->configs += nn;
-      if (R->witness) {
-        R->last_tbase = (uint32_t)R->tnext;
-        R->tnext += nn;
-        if (R->tnext + p.scap > p.trace_cap) R->witness = 0;
+      R.nf = k.nn;
+      R.max_frontier = max(R.max_frontier, k.nn);
+      R.configs += k.nn;
+      if (R.witness) {
+        R.last_tbase = (uint32_t)R.tnext;
+        R.tnext += k.nn;
+        if (R.tnext + scap > trace_cap) R.witness = 0;
       }
-      if (R->max_configs && R->configs > R->max_configs) R->done = LVR_BUDGET;
+      if (R.max_configs && R.configs > R.max_configs) R.done = LVR_BUDGET;
     }
   }
-  // host-mapped mirror: only when the host will look (the last round of a
-  // batch, or the end of the search) -- every word is a write over the link
-  if (p.publish && (p.publish_always || R->done)) {
-    const uint32_t* src = reinterpret_cast<const uint32_t*>(R);
-    volatile uint32_t* dst = reinterpret_cast<volatile uint32_t*>(p.publish);
-    for (uint32_t i = 0; i < sizeof(LvRun) / 4; ++i) dst[i] = src[i];
-    __threadfence_system();
-  }
+}
+
+__device__ __forceinline__ void lv_publish(const LvRun& R, LvRun* pub) {
+  const uint32_t* src = reinterpret_cast<const uint32_t*>(&R);
+  volatile uint32_t* dst = reinterpret_cast<volatile uint32_t*>(pub);
+  for (uint32_t i = 0; i < sizeof(LvRun) / 4; ++i) dst[i] = src[i];
+  __threadfence_system();
+}
+
+// The last block of lv_insert closes the round on the device, then publishes
+// the run state to the host-mapped mirror when the host will look (the last
+// round of a batch, or the end of the search): every word is a write over the link.
+__device__ __forceinline__ void lv_close_round(const LvParams& p) {
+  const LvCounts k = lv_read_counts(p.ctl);
+  LvRun& R = *p.run;
+  lv_close_state(R, k, p.round, p.rcounts, p.scap, p.trace_cap);
+  if (p.publish && (p.publish_always || R.done)) lv_publish(R, p.publish);
 }
 
 // ---- insert: one lane per staged configuration -----------------------------
@@ -744,6 +897,148 @@ __global__ __launch_bounds__(LV_BLOCK) void lv_insert(LvParams p) {
   if (threadIdx.x == 0) s_last = atomicAdd(&p.ctl->done_blocks, 1u) == gridDim.x - 1;
   __syncthreads();
   if (s_last && threadIdx.x == 0) lv_close_round(p);
+}
+
+// ---- persistent narrow rounds ---------------------------------------------
+// While the frontier is narrow, a round's work is a few microseconds of
+// dependent loads per wave, and two kernel launches per round (each starting
+// with cold instruction / scalar / data caches on every CU) cost far more than
+// the work. lv_persist keeps one resident workgroup per CU and runs round
+// after round: lv_expand<FUSED> stages every closed child with write-through
+// stores and inserts it at once, then a grid barrier ends the round, and
+// every workgroup closes it identically from the round's atomic counters (its
+// own copy of the run state, in LDS). It stops when the search ends, the
+// frontier outgrows it (the host goes on with lv_round / lv_insert), or after
+// max_rounds rounds (the host checks its deadline between launches).
+//
+// Memory protocol (inter-workgroup hand-offs inside one launch): everything a
+// workgroup writes that another reads in this launch is stored write-through
+// (agent-scope stores) and drained (vmcnt(0)) before the atomic that
+// publishes it; inside a round, staged configurations are read back only with
+// agent-scope loads; across rounds, every workgroup runs one agent-scope
+// acquire after the barrier before any plain load. Counters and the tables are
+// atomics only.
+
+// Barrier words (zeroed by the host before every launch), one per 128-byte line.
+struct LvBar {
+  uint32_t grp[8][32];  // arrivals of blocks b with b % 8 == g (block-to-XCD placement is only a speed hint)
+  uint32_t top[32];     // arrivals of the group leaders
+  uint32_t gen[32];     // the last completed barrier epoch
+  uint32_t abort[32];   // set by a block whose wait timed out: every block leaves
+};
+
+struct LvPersist {
+  LvCtl* ctl3;                // round r counts in ctl3[r % 3]
+  LvBar* bar;
+  uint8_t* stg[2];            // round r stages into stg[r & 1]; its frontier is stg[(r + 1) & 1]
+  uint32_t* idx[2];
+  unsigned long long* ht[2];  // round r inserts into ht[r & 1]
+  uint32_t max_rounds;        // rounds per launch
+  uint32_t nf_max;            // leave when the frontier is wider
+  unsigned long long spin_ticks;  // barrier wait limit (wall-clock ticks)
+};
+
+// Grid barrier for epoch e = 1, 2, ... (monotonic counters: no reset inside a
+// launch). Returns false when the wait timed out or another block gave up.
+__device__ __forceinline__ bool lv_grid_sync(LvBar* B, uint32_t e, unsigned long long spin_ticks) {
+  __shared__ uint32_t s_ok;
+  lv_drain();  // this wave's write-through stores have landed
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    const uint32_t G = gridDim.x, g = blockIdx.x & 7u;
+    const uint32_t ng = min(G, 8u);
+    const uint32_t gsz = G / 8u + (g < G % 8u ? 1u : 0u);
+    const uint32_t v = atomicAdd(&B->grp[g][0], 1u) + 1u;
+    if (v == e * gsz) {
+      const uint32_t t = atomicAdd(&B->top[0], 1u) + 1u;
+      if (t == e * ng) st_wt32(&B->gen[0], e);
+    }
+    uint32_t ok = 1;
+    const unsigned long long t0 = wall_clock64();
+    while (ld_agent(&B->gen[0]) < e) {
+      if (ld_agent(&B->abort[0])) { ok = 0; break; }
+      __builtin_amdgcn_s_sleep(2);
+      if (wall_clock64() - t0 > spin_ticks) {
+        atomicExch(&B->abort[0], 1u);
+        ok = 0;
+        break;
+      }
+    }
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");  // this CU's stale lines go
+    lv_drain();                                        // ... before any wave of the block loads
+    s_ok = ok;
+  }
+  __syncthreads();
+  return s_ok != 0;
+}
+
+template <int NQ>
+__global__ __launch_bounds__(LV_BLOCK) void lv_persist(LvParams p, LvPersist q) {
+  __shared__ LvHeadsLds<NQ> s_heads[LV_BLOCK / 64];
+  __shared__ uint32_t s_cs[64 * NQ];
+  __shared__ LvRun s_run;
+  for (uint32_t x = threadIdx.x; x < 64u * NQ; x += LV_BLOCK) s_cs[x] = x < p.K ? p.cs[x] : 0u;
+  if (threadIdx.x == 0) s_run = *p.run;  // written by an earlier launch
+  __syncthreads();
+  if (s_run.done != LVR_RUNNING) return;
+  const uint32_t nwaves = gridDim.x * (LV_BLOCK / 64);
+  bool ok = true;
+#ifdef S2LC_PROF
+  unsigned long long t_round = wall_clock64();
+#endif
+  for (uint32_t it = 0; ok; ++it) {
+    const uint32_t r = s_run.round + 1;  // the round this iteration expands
+    LvParams rp = p;
+    rp.round = r;
+    rp.cur = q.stg[(r + 1) & 1]; rp.cur_idx = q.idx[(r + 1) & 1];
+    rp.stg = q.stg[r & 1]; rp.nxt_idx = q.idx[r & 1];
+    rp.ht = q.ht[r & 1]; rp.ht_clear = q.ht[(r + 1) & 1];
+    rp.ctl = q.ctl3 + (r % 3);
+    rp.clear_slots = 1;
+    rp.init = 0;
+    if (blockIdx.x == 0) {  // the counters of round r + 1 (last read in round r - 2's close)
+      uint32_t* z = reinterpret_cast<uint32_t*>(q.ctl3 + ((r + 1) % 3));
+      for (uint32_t i = threadIdx.x; i < sizeof(LvCtl) / 4; i += LV_BLOCK) st_wt32(z + i, 0u);
+    }
+    LvRoundIn in;
+    in.f0 = 0;
+    in.nf = s_run.nf;
+    in.S = lv_slices(p.K, in.nf, nwaves, s_run.last_nf, s_run.last_children);
+    in.tbase = (uint32_t)s_run.tnext;
+    in.wit = s_run.witness;
+    const bool worked = lv_expand<NQ, true>(rp, in, s_heads[threadIdx.x >> 6], s_cs);
+#ifdef S2LC_PROF
+    if (worked && (threadIdx.x & 63) == 0 && p.prof) atomicMax(&rp.ctl->prof_end, wall_clock64());
+#else
+    (void)worked;
+#endif
+    ok = lv_grid_sync(q.bar, it + 1, q.spin_ticks);
+#ifdef S2LC_PROF
+    if (blockIdx.x == 0 && threadIdx.x == 0 && p.prof) {
+      // [9] round time, [10] expansion critical path, [11] rounds (wall-clock ticks)
+      const unsigned long long t_b = wall_clock64(), e = ld_agent64(&rp.ctl->prof_end);
+      atomicAdd(&p.prof[9], t_b - t_round);
+      atomicAdd(&p.prof[10], e > t_round ? e - t_round : 0ull);
+      atomicAdd(&p.prof[11], 1ull);
+      t_round = t_b;
+    }
+#endif
+    if (threadIdx.x == 0) {
+      if (ok) {
+        const LvCounts k = lv_read_counts(rp.ctl);
+        lv_close_state(s_run, k, r, blockIdx.x == 0 ? p.rcounts : nullptr, p.scap, p.trace_cap);
+      } else {
+        s_run.done = LVR_ABORT;
+      }
+    }
+    __syncthreads();
+    if (s_run.done != LVR_RUNNING || it + 1 >= q.max_rounds || s_run.nf > q.nf_max) break;
+  }
+  if (blockIdx.x == 0 && threadIdx.x == 0) {
+    if (ld_agent(&q.bar->abort[0])) s_run.done = LVR_ABORT;  // some block left early: nothing here is valid
+    *p.run = s_run;
+    if (p.publish) lv_publish(s_run, p.publish);
+  }
 }
 
 // Round 0 setup on the device: the run state of a fresh search.

@@ -65,14 +65,16 @@ struct LevelBufs {
   uint32_t nq = 0, scap = 0, ht_mask = 0;
   uint8_t* stg[2] = {nullptr, nullptr};     // staging arrays (frontier of round r = staging of round r-1)
   uint32_t* idx[2] = {nullptr, nullptr};    // frontier index lists
-  unsigned long long* ht = nullptr;         // dedupe table
-  void* ctl = nullptr;                      // LvCtl[2], double buffered by round
+  unsigned long long* ht[2] = {nullptr, nullptr};  // dedupe tables: round r inserts into ht[r & 1]
+  void* ctl = nullptr;                      // LvCtl[3] (host-enqueued rounds: ctl[r & 1]; persistent: ctl[r % 3])
+  void* bar = nullptr;                      // LvBar (persistent rounds)
   void* run = nullptr;                      // LvRun (device)
   void* h_run = nullptr;                    // pinned host-mapped mirror of the run state
   void* h_ctl = nullptr;                    // pinned host copy of a control block (chunked rounds)
   hipEvent_t ev[2] = {nullptr, nullptr};
-  size_t stg_bytes[2] = {0, 0}, idx_bytes[2] = {0, 0}, ht_bytes = 0;
-  uint32_t grid_round = 0, grid_insert = 0, grid_nq = 0;  // persistent grids (for grid_nq)
+  size_t stg_bytes[2] = {0, 0}, idx_bytes[2] = {0, 0}, ht_bytes[2] = {0, 0};
+  uint32_t grid_round = 0, grid_insert = 0, grid_nq = 0;  // resident grids (for grid_nq)
+  uint32_t grid_persist = 0;                // lv_persist: one workgroup per CU
 };
 
 struct LevelStats {
@@ -80,6 +82,7 @@ struct LevelStats {
   uint64_t rounds = 0, configs = 0, children = 0;
   uint32_t max_frontier = 0, histories = 0, chunk_retries = 0;
   uint32_t syncs = 0;  // host synchronizations (one per batch of device-driven rounds)
+  uint64_t persist_rounds = 0, persist_launches = 0;  // rounds run inside lv_persist
 };
 
 // A batch of histories resident on one device. Every buffer is grown on

@@ -155,25 +155,88 @@ def test_round_counts_match_reduced_search(engine, abl):
                                                              if x != y][:5])
 
 
+# level-search round modes: narrow rounds inside the persistent kernel
+# (default), host-enqueued lv_round / lv_insert only, or every round inside
+# the persistent kernel (fused stage-and-insert also on wide frontiers)
+LEVEL_MODES = {"default": {}, "no_persist": {"S2LC_NO_PERSIST": "1"}, "all_persist": {"S2LC_PERSIST_NF": "4294967295"}}
+
+
+def _set_mode(monkeypatch, mode):
+    for k, v in LEVEL_MODES[mode].items():
+        monkeypatch.setenv(k, v)
+
+
+@pytest.mark.parametrize("mode", list(LEVEL_MODES))
 @pytest.mark.parametrize("name,off", [("H174", 0), ("H174", 2), ("H212", 0), ("H212", 2), ("C5bad", 0),
                                       ("C5bad", 2), ("C5bad", 4)])
-def test_hard_round_counts(name, off):
+def test_hard_round_counts(name, off, mode, monkeypatch):
     """Hard single histories (> 128 chains, the level search): per-round counts
-    against the committed CPU reduced-search counts."""
+    against the committed CPU reduced-search counts, in every round mode."""
     from s2_verification_amd import workloads as W
+    _set_mode(monkeypatch, mode)
     ref = golden("hard_round_counts.json")[name]
     assert config_digest(name) == ref["digest"], "simulator output changed: regenerate the fixture"
     want = ref[str(off)]
     h = W.config_history(name)
     b, res = run(checker_for(s2.ENGINE_AUTO, off, rc=True), [h])
     r = res[0]
-    assert r.verdict == want["verdict"], (name, off, r)
+    st = b.stats()
+    assert r.verdict == want["verdict"], (name, off, mode, r)
     assert r.rounds == want["rounds"]
     got = b.round_counts(0)
     bad = [k for k, (x, y) in enumerate(zip(got, want["counts"])) if x != y]
-    assert got == want["counts"], (name, off, bad[:5])
+    assert got == want["counts"], (name, off, mode, bad[:5])
     if r.verdict == s2.Ok:
         assert r.witness is not None
+    if mode == "no_persist":
+        assert st["level_persist_rounds"] == 0, st
+    else:
+        assert st["level_persist_rounds"] > 0, st
+    if mode == "all_persist":
+        assert st["level_persist_rounds"] == r.rounds, st
+
+
+@pytest.mark.parametrize("mode", ["default", "all_persist"])
+@pytest.mark.parametrize("abl", ["all_on", "no_p2", "no_idefer"])
+def test_level_persist_round_counts_match_reduced_search(mode, abl, monkeypatch):
+    """The persistent rounds against oracle/reduced.c, round by round, on the
+    small cases (level engine forced)."""
+    _set_mode(monkeypatch, mode)
+    red = ABLATIONS[abl]
+    hs = _round_cases()
+    b, res = run(checker_for(s2.ENGINE_LEVEL, red, rc=True), hs)
+    for i, (h, r) in enumerate(zip(hs, res)):
+        v, st = orc.check_reduced(orc.from_s2lc_numpy(h.events_numpy()), reductions_off=red, round_counts=True)
+        assert r.verdict == v, (mode, abl, i, r, v)
+        assert r.rounds == st["rounds"], (mode, abl, i, r.rounds, st["rounds"])
+        assert b.round_counts(i) == st["round_counts"], (mode, abl, i)
+        if r.verdict == s2.Ok:
+            assert r.witness is not None
+
+
+@pytest.mark.parametrize("mode", ["default", "all_persist"])
+def test_level_staging_overflow_is_unknown_with_exact_prefix(mode, monkeypatch):
+    """A staging array too small for H174's widest rounds (4,096 slots): the
+    round that overflows (inside the persistent kernel or
+    not) is re-run over frontier chunks, and when the round still does not fit
+    the verdict is Unknown / frontier. Every round completed before it keeps
+    the exact unique-configuration count of the CPU reduced search."""
+    from s2_verification_amd import workloads as W
+    _set_mode(monkeypatch, mode)
+    monkeypatch.setenv("S2LC_LEVEL_SCAP", "4096")
+    ref = golden("hard_round_counts.json")["H174"]["0"]
+    h = W.config_history("H174")
+    c = s2.Checker(round_counts=True)
+    b = c.batch([h])
+    r = b.check()[0]
+    st = b.stats()
+    assert r.verdict == s2.Unknown and r.reason == "frontier", (r, st)
+    got = b.round_counts(0)
+    assert 100 < len(got) < ref["rounds"]
+    assert got[:-1] == ref["counts"][:len(got) - 1]  # the last (overflowing) round has no count
+    assert st["level_chunk_retries"] > 0, st
+    if mode == "all_persist":
+        assert st["level_persist_rounds"] > 0, st
 
 
 def test_rerun_does_not_reuse_stale_results(monkeypatch):
