@@ -240,6 +240,17 @@ int s2lc_batch_run(s2lc_ctx* ctx, s2lc_batch* b);
 /* Results of the last run; with_witness expands and replay-verifies witnesses
  * on the host (CPU model, powerset semantics). */
 int s2lc_batch_results(s2lc_ctx* ctx, s2lc_batch* b, s2lc_result* out /* [n] */, int with_witness);
+/* The same results as flat arrays, for bulk callers (no per-history
+ * allocation crosses the boundary): per history verdict, reason, configs and
+ * rounds; the Ok witnesses (certified exactly as by s2lc_batch_results)
+ * concatenated into witness_ids, history i's at [witness_offs[i],
+ * witness_offs[i+1]) (empty unless Ok). witness_offs has n + 1 entries;
+ * with witness_ids NULL no witness is rebuilt (every range empty), else it
+ * must hold ids_cap >= the total (the sum of the histories' n_ops always
+ * suffices). Any output pointer but witness_offs may be NULL. Returns
+ * S2LC_EWITNESS like s2lc_batch_results. */
+int s2lc_batch_results_flat(s2lc_ctx* ctx, s2lc_batch* b, int32_t* verdicts, int32_t* reasons, uint64_t* configs,
+                            uint64_t* rounds, int64_t* witness_ids, size_t ids_cap, uint64_t* witness_offs);
 void s2lc_batch_free(s2lc_batch* b);
 
 typedef struct s2lc_batch_stats {
@@ -272,6 +283,7 @@ typedef struct s2lc_batch_stats {
   uint32_t level_chunk_retries;
   uint32_t level_syncs;
   uint32_t _pad2;
+  uint64_t n_ops_total;      /* ops over the batch's histories (sizes s2lc_batch_results_flat's ids) */
 } s2lc_batch_stats;
 int s2lc_batch_stats_get(const s2lc_batch* b, s2lc_batch_stats* out);
 /* With S2LC_F_ROUND_COUNTS: the unique-configuration count of each completed

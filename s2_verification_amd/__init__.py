@@ -106,7 +106,8 @@ class c_batch_stats(ctypes.Structure):
                 ("pack16_ms", ctypes.c_double), ("pack16_algo_bytes", ctypes.c_uint64),
                 ("pack16_histories", ctypes.c_uint32), ("_pad1", ctypes.c_uint32),
                 ("level_persist_rounds", ctypes.c_uint64), ("level_persist_launches", ctypes.c_uint32),
-                ("level_chunk_retries", ctypes.c_uint32), ("level_syncs", ctypes.c_uint32), ("_pad2", ctypes.c_uint32)]
+                ("level_chunk_retries", ctypes.c_uint32), ("level_syncs", ctypes.c_uint32), ("_pad2", ctypes.c_uint32),
+                ("n_ops_total", ctypes.c_uint64)]
 
 
 class c_sim_params(ctypes.Structure):
@@ -162,6 +163,7 @@ SIGNATURES = [
     ("s2lc_batch_load", ctypes.c_int, [_P, _P, ctypes.POINTER(_P), ctypes.c_size_t]),
     ("s2lc_batch_run", ctypes.c_int, [_P, _P]),
     ("s2lc_batch_results", ctypes.c_int, [_P, _P, ctypes.POINTER(c_result), ctypes.c_int]),
+    ("s2lc_batch_results_flat", ctypes.c_int, [_P, _P, _P, _P, _P, _P, _P, ctypes.c_size_t, _P]),
     ("s2lc_batch_free", None, [_P]),
     ("s2lc_batch_stats_get", ctypes.c_int, [_P, ctypes.POINTER(c_batch_stats)]),
     ("s2lc_batch_round_counts", ctypes.c_int, [_P, ctypes.c_size_t, ctypes.POINTER(ctypes.c_uint32), ctypes.c_size_t,
@@ -477,6 +479,27 @@ class Batch:
         out = [_convert(res[i], as_numpy) for i in range(n)] if rc in (0, EWITNESS) else None
         for i in range(n):
             lib().s2lc_result_free(ctypes.byref(res[i]))
+        if rc:
+            raise S2LCError(rc, self.checker.last_error())
+        return out
+
+    def results_flat(self, with_witness=True) -> dict:
+        """s2lc_batch_results_flat: numpy arrays (verdict, reason, configs,
+        rounds per history; certified Ok witnesses as one int64 array of op ids
+        with offsets: history i's witness = witness_ids[offs[i]:offs[i+1]])."""
+        n = len(self.histories)
+        out = {"verdict": np.zeros(n, np.int32), "reason": np.zeros(n, np.int32),
+               "configs": np.zeros(n, np.uint64), "rounds": np.zeros(n, np.uint64),
+               "witness_offs": np.zeros(n + 1, np.uint64)}
+        cap = self.stats()["n_ops_total"] if with_witness else 0
+        ids = np.zeros(max(1, cap), np.int64)
+        p = lambda a: a.ctypes.data
+        rc = lib().s2lc_batch_results_flat(self.checker._ctx, self._b, p(out["verdict"]), p(out["reason"]),
+                                           p(out["configs"]), p(out["rounds"]), p(ids) if with_witness else None,
+                                           cap, p(out["witness_offs"]))
+        if rc and rc != EWITNESS:
+            raise S2LCError(rc, self.checker.last_error())
+        out["witness_ids"] = ids[:int(out["witness_offs"][-1])]
         if rc:
             raise S2LCError(rc, self.checker.last_error())
         return out

@@ -18,6 +18,7 @@
 #include "history.h"
 #include "s2lincheck.h"
 #include "search.h"
+#include "host_par.h"
 
 namespace s2lc {
 int simulate(const s2lc_sim_params& p, History* h, std::string* jsonl);
@@ -543,6 +544,47 @@ int s2lc_batch_run(s2lc_ctx* c, s2lc_batch* b) {
   }
 }
 
+int s2lc_batch_results_flat(s2lc_ctx* c, s2lc_batch* b, int32_t* verdicts, int32_t* reasons, uint64_t* configs,
+                            uint64_t* rounds, int64_t* witness_ids, size_t ids_cap, uint64_t* witness_offs) {
+  if (!c || !b || !witness_offs) return S2LC_EINVAL;
+  if (!b->ran) { c->err = "batch has not been run"; return S2LC_EINVAL; }
+  try {
+    if (hipSetDevice(b->b.device) != hipSuccess) { c->err = "hipSetDevice failed"; return S2LC_EHIP; }
+    const size_t n = b->b.n_hist;
+    std::vector<s2lc_result> res(std::max<size_t>(n, 1));
+    const int rc = collect_results(b->b, b->stats, b->witness, res.data(), witness_ids != nullptr, c->err);
+    if (rc && rc != S2LC_EWITNESS) return rc;
+    uint64_t total = 0;
+    for (size_t i = 0; i < n; ++i) {
+      witness_offs[i] = total;
+      total += res[i].witness ? res[i].witness_len : 0;
+    }
+    witness_offs[n] = total;
+    int out_rc = rc;
+    if (witness_ids && total > ids_cap) {
+      c->err = "witness buffer too small";
+      out_rc = S2LC_EINVAL;
+    }
+    parallel_for(n, 256, [&](size_t i) {
+      s2lc_result& r = res[i];
+      if (verdicts) verdicts[i] = r.verdict;
+      if (reasons) reasons[i] = r.reason;
+      if (configs) configs[i] = r.configs_explored;
+      if (rounds) rounds[i] = r.rounds;
+      if (witness_ids && out_rc != S2LC_EINVAL && r.witness)
+        memcpy(witness_ids + witness_offs[i], r.witness, sizeof(int64_t) * r.witness_len);
+      s2lc_result_free(&r);
+    });
+    return out_rc;
+  } catch (const std::bad_alloc&) {
+    c->err = "out of memory";
+    return S2LC_ENOMEM;
+  } catch (...) {
+    c->err = "internal error";
+    return S2LC_EINVAL;
+  }
+}
+
 int s2lc_batch_results(s2lc_ctx* c, s2lc_batch* b, s2lc_result* out, int with_witness) {
   if (!c || !b || (!out && b->b.n_hist)) return S2LC_EINVAL;
   if (!b->ran) { c->err = "batch has not been run"; return S2LC_EINVAL; }
@@ -587,6 +629,9 @@ int s2lc_batch_stats_get(const s2lc_batch* b, s2lc_batch_stats* out) {
   out->level_persist_launches = (uint32_t)b->stats.level.persist_launches;
   out->level_chunk_retries = b->stats.level.chunk_retries;
   out->level_syncs = b->stats.level.syncs;
+  uint64_t ops = 0;
+  for (const History* h : b->b.src) ops += h->n_ops;
+  out->n_ops_total = ops;
   return 0;
 }
 

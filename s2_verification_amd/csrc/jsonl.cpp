@@ -13,6 +13,7 @@
 //     ParseInt), strings are UTF-8-sanitised (invalid bytes -> U+FFFD);
 //   * len(record_hashes) != num_records is an error (main.go:62-64).
 #include <stdio.h>
+#include <stdlib.h>
 #include <string.h>
 
 #include <string>
@@ -454,6 +455,157 @@ struct Dec {
   }
 };
 
+
+// ------------------------------------------------------------ fast path ---
+// The collector's own serialisation (serde, history.rs; the simulator writes
+// the same bytes): fixed key order, no whitespace inside a record, integers
+// as plain digits, token strings without escapes. A record in exactly that
+// form is decoded here without building a JSON tree; any byte that deviates
+// sends the record to the general parser above (which also owns every error
+// message), so the result is the same History either way (tests/test_jsonl.py
+// compares both paths).
+struct Fast {
+  const uint8_t* p;
+  const uint8_t* end;
+  template <size_t N>
+  bool lit(const char (&w)[N]) {
+    const size_t n = N - 1;
+    if ((size_t)(end - p) < n || memcmp(p, w, n) != 0) return false;
+    p += n;
+    return true;
+  }
+  bool peek(char c) const { return p < end && *p == (uint8_t)c; }
+  // a non-negative integer literal in uint64 range, not followed by a
+  // fraction or exponent (those are type errors: the general parser reports them)
+  bool u64(uint64_t& v) {
+    if (p >= end || *p < '0' || *p > '9') return false;
+    if (*p == '0') {
+      ++p;
+      v = 0;
+    } else {
+      uint64_t r = 0;
+      while (p < end && *p >= '0' && *p <= '9') {
+        const uint32_t d = *p - '0';
+        if (r > (~0ull - d) / 10) return false;
+        r = r * 10 + d;
+        ++p;
+      }
+      v = r;
+    }
+    return !(p < end && (*p == '.' || *p == 'e' || *p == 'E' || (*p >= '0' && *p <= '9')));
+  }
+  bool i64(int64_t& v) {
+    uint64_t u;
+    if (!u64(u) || u > (uint64_t)INT64_MAX) return false;
+    v = (int64_t)u;
+    return true;
+  }
+  // "..." of printable ASCII without escapes; s/n = the contents
+  bool plain_str(const char*& s, size_t& n) {
+    if (!peek('"')) return false;
+    const uint8_t* q = ++p;
+    while (p < end && *p != '"') {
+      if (*p < 0x20 || *p >= 0x80 || *p == '\\') return false;
+      ++p;
+    }
+    if (p >= end) return false;
+    s = (const char*)q;
+    n = (size_t)(p - q);
+    ++p;
+    return true;
+  }
+  // null | "token"
+  bool opt_tok(bool& has, const char*& s, size_t& n) {
+    if (lit("null")) { has = false; return true; }
+    has = true;
+    return plain_str(s, n);
+  }
+};
+
+// One record at buf[off..]; returns the bytes consumed (0: not in the
+// collector's form, nothing was changed).
+size_t fast_record(const uint8_t* base, const uint8_t* end, History& h) {
+  Fast F{base, end};
+  Event e;
+  size_t pool0 = h.pool.size();
+  bool set_has = false, tok_has = false;
+  const char *set_s = nullptr, *tok_s = nullptr;
+  size_t set_n = 0, tok_n = 0;
+  auto undo = [&]() { h.pool.resize(pool0); return (size_t)0; };
+  if (!F.lit("{\"event\":{\"")) return 0;
+  if (F.lit("Start\":")) {
+    e.kind = 0;
+    if (F.lit("\"Read\"")) {
+      e.input_type = S2LC_INPUT_READ;
+    } else if (F.lit("\"CheckTail\"")) {
+      e.input_type = S2LC_INPUT_CHECK_TAIL;
+    } else {
+      if (!F.lit("{\"Append\":{\"num_records\":")) return 0;
+      e.input_type = S2LC_INPUT_APPEND;
+      e.has_num_records = 1;
+      if (!F.u64(e.num_records) || !F.lit(",\"record_hashes\":[")) return 0;
+      if (!F.peek(']')) {
+        for (;;) {
+          uint64_t v;
+          if (!F.u64(v)) return undo();
+          h.pool.push_back(v);
+          if (F.peek(',')) { ++F.p; continue; }
+          break;
+        }
+      }
+      if (!F.lit("],\"set_fencing_token\":") || !F.opt_tok(set_has, set_s, set_n)) return undo();
+      if (!F.lit(",\"fencing_token\":") || !F.opt_tok(tok_has, tok_s, tok_n)) return undo();
+      if (!F.lit(",\"match_seq_num\":")) return undo();
+      if (F.lit("null")) {
+        e.has_msn = 0;
+        e.msn = 0;
+      } else {
+        if (!F.u64(e.msn)) return undo();
+        e.has_msn = 1;
+      }
+      if (!F.lit("}}")) return undo();
+      e.hash_off = pool0;
+      e.hash_cnt = h.pool.size() - pool0;
+      if (e.hash_cnt != e.num_records) return undo();  // the general parser reports the mismatch
+    }
+  } else if (F.lit("Finish\":")) {
+    e.kind = 1;
+    if (F.peek('"')) {
+      e.failure = 1;
+      e.has_tail = 0;
+      e.has_hash = 0;
+      if (F.lit("\"AppendDefiniteFailure\"")) e.definite = 1;
+      else if (F.lit("\"AppendIndefiniteFailure\"")) e.definite = 0;
+      else if (F.lit("\"ReadFailure\"") || F.lit("\"CheckTailFailure\"")) e.definite = 1;
+      else return 0;
+    } else {
+      e.failure = 0;
+      e.definite = 0;
+      e.has_tail = 1;
+      if (F.lit("{\"AppendSuccess\":{\"tail\":") || F.lit("{\"CheckTailSuccess\":{\"tail\":")) {
+        if (!F.u64(e.tail)) return 0;
+      } else if (F.lit("{\"ReadSuccess\":{\"tail\":")) {
+        e.has_hash = 1;
+        if (!F.u64(e.tail) || !F.lit(",\"stream_hash\":") || !F.u64(e.stream_hash)) return 0;
+      } else {
+        return 0;
+      }
+      if (!F.lit("}}")) return 0;
+    }
+  } else {
+    return 0;
+  }
+  if (!F.lit("},\"client_id\":") || !F.i64(e.client_id) || !F.lit(",\"op_id\":") || !F.i64(e.op_id) ||
+      !F.lit("}"))
+    return undo();
+  // the next byte must end the value (whitespace, end of input, or the next record)
+  if (F.p < end && !(*F.p == ' ' || *F.p == '\t' || *F.p == '\n' || *F.p == '\r' || *F.p == '{')) return undo();
+  if (set_has) e.set_tok = h.intern(std::string(set_s, set_n));
+  if (tok_has) e.batch_tok = h.intern(std::string(tok_s, tok_n));
+  h.events.push_back(e);
+  return (size_t)(F.p - base);
+}
+
 }  // namespace
 
 int load_jsonl(const uint8_t* buf, size_t len, History& h, std::string& err) {
@@ -462,9 +614,26 @@ int load_jsonl(const uint8_t* buf, size_t len, History& h, std::string& err) {
   P.p = buf;
   P.end = buf + len;
   std::vector<uint64_t> hashes;
+  const bool fast = getenv("S2LC_JSONL_GENERAL") == nullptr;  // tests: the general parser only
+  {
+    // size the event / hash arrays once (a record per line in the collector's
+    // output): growing them record by record re-maps large blocks, which
+    // serialises parallel decoders on the process's address-space lock
+    size_t lines = 0;
+    for (const uint8_t* q = buf; (q = (const uint8_t*)memchr(q, '\n', (size_t)(buf + len - q))) != nullptr; ++q) ++lines;
+    h.events.reserve(h.events.size() + lines + 1);
+    h.pool.reserve(h.pool.size() + len / 24);
+  }
   while (true) {
     P.ws();
     if (P.p >= P.end) return 0;  // io.EOF
+    if (fast) {
+      const size_t used = fast_record(P.p, P.end, h);
+      if (used) {
+        P.p += used;
+        continue;
+      }
+    }
     const size_t rec_off = (size_t)(P.p - buf);
     P.reset();
     uint32_t root;

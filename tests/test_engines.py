@@ -341,3 +341,26 @@ def test_check_reuses_scratch_and_matches_batch():
     want = [r.verdict for r in s2.Checker().check_batch(hs)]
     got = [c.check(h).verdict for h in hs]
     assert got == want
+
+
+def test_results_flat_matches_results():
+    """s2lc_batch_results_flat: the same verdicts, counts and certified
+    witnesses as s2lc_batch_results, as flat arrays."""
+    from s2_verification_amd import workloads as W
+    import numpy as np
+    hs = W.c4_histories(300, first_seed=4200) + [W.config_history("C3")]
+    c = s2.Checker()
+    b = c.batch(hs)
+    b.run()
+    res = b.results(with_witness=True)
+    flat = b.results_flat(with_witness=True)
+    offs = flat["witness_offs"].astype(np.int64)
+    assert offs[-1] == len(flat["witness_ids"])
+    for i, r in enumerate(res):
+        assert s2._VERDICT[int(flat["verdict"][i])] == r.verdict
+        assert int(flat["configs"][i]) == r.configs_explored and int(flat["rounds"][i]) == r.rounds
+        w = flat["witness_ids"][offs[i]:offs[i + 1]].tolist()
+        assert w == (list(r.witness) if r.verdict == s2.Ok else []), i
+    assert any(r.verdict == s2.Illegal for r in res) and any(r.verdict == s2.Ok for r in res)
+    nw = b.results_flat(with_witness=False)
+    assert (nw["witness_offs"] == 0).all() and (nw["verdict"] == flat["verdict"]).all()

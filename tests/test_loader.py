@@ -174,3 +174,54 @@ def test_load_many_reports_first_bad_buffer():
     with pytest.raises(s2.S2LCError) as e:
         s2.load_many(blobs, threads=3)
     assert "history 2:" in str(e.value)
+
+
+def _canon_or_error(data):
+    try:
+        h = load(data)
+    except s2.S2LCError as e:
+        return ("error", e.status, str(e))
+    return ("ok", h.info()["n_events"], [(e.Kind, e.Id, e.ClientId, repr(e.Value)) for e in h.events()])
+
+
+def _perturbations(text):
+    """Variants of a collector-format blob that leave the fast path's form
+    (the general parser takes those records) or are invalid."""
+    lines = text.splitlines(keepends=True)
+    out = []
+    for i in range(0, min(len(lines), 40), 7):
+        ln = lines[i]
+        for a, b in (('":', '": '), ('"event"', '"Event"'), ('"client_id":', '"client_id":-'),
+                     ('"op_id":', '"op_id":0'), ('"tail":', '"tail":1.5e'), ('"num_records":', '"num_records":1'),
+                     ('"set_fencing_token":null', '"set_fencing_token":"t\\u00e9"'),
+                     ('"fencing_token":null', '"fencing_token":"éx"'), (',"op_id"', ',"x":[1,2],"op_id"'),
+                     ('}\n', '}  '), ('{"event"', '\t{"event"'), ('"Read"', '"Re\\u0061d"'),
+                     ('"match_seq_num":null', '"match_seq_num":7'), ('[', '[ ')):
+            if a in ln:
+                out.append("".join(lines[:i] + [ln.replace(a, b, 1)] + lines[i + 1:]))
+    return out
+
+
+def test_fast_path_decodes_like_the_general_parser(monkeypatch):
+    """jsonl.cpp decodes records in the collector's exact serialisation without
+    a JSON tree and hands every other record to the general (Go encoding/json)
+    parser: same events, tokens and errors either way (S2LC_JSONL_GENERAL=1
+    forces the general parser)."""
+    from s2_verification_amd import workloads as W
+    blobs = [open(os.path.join(GOLDEN, f), "rb").read().decode() for f in sorted(os.listdir(GOLDEN))
+             if f.endswith(".jsonl")]
+    blobs += [s2.simulate_jsonl(**W.c4_params(sd)).decode() for sd in range(0, 30)]
+    blobs.append(W.config_jsonl("C3").decode())
+    cases = list(blobs)
+    for b in blobs[:12] + blobs[-3:]:
+        cases += _perturbations(b)
+    assert len(cases) > 150
+    n_err = 0
+    for data in cases:
+        monkeypatch.delenv("S2LC_JSONL_GENERAL", raising=False)
+        fast = _canon_or_error(data.encode("utf-8"))
+        monkeypatch.setenv("S2LC_JSONL_GENERAL", "1")
+        general = _canon_or_error(data.encode("utf-8"))
+        assert fast == general, data[:300]
+        n_err += fast[0] == "error"
+    assert 0 < n_err < len(cases)
