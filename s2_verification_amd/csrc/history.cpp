@@ -6,7 +6,6 @@
 //   s2Model.Step                                main.go:264-335
 #include <algorithm>
 #include <queue>
-#include <unordered_map>
 
 #include "history.h"
 #include "s2lincheck.h"
@@ -64,18 +63,29 @@ int History::finalize() {
   const size_t E = events.size();
   if (E >= (size_t)EV_INF) { status = S2LC_EUNSUPPORTED; error = "too many events"; return status; }
 
-  // porcupine renumber(): ids -> 0..m-1 in order of first appearance.
-  std::unordered_map<int64_t, uint32_t> idmap;
-  idmap.reserve(E);
+  // porcupine renumber(): ids -> 0..m-1 in order of first appearance
+  // (an open-addressing map: one allocation, no per-id nodes)
   std::vector<uint32_t> dense(E);
   std::vector<int64_t> ids;
-  for (size_t i = 0; i < E; ++i) {
-    auto it = idmap.find(events[i].op_id);
-    if (it == idmap.end()) {
-      it = idmap.emplace(events[i].op_id, (uint32_t)ids.size()).first;
-      ids.push_back(events[i].op_id);
+  ids.reserve(E / 2 + 1);
+  {
+    size_t cap = 16;
+    while (cap < 2 * E) cap <<= 1;
+    std::vector<int64_t> key(cap);
+    std::vector<uint32_t> val(cap, EV_INF);
+    const size_t mask = cap - 1;
+    for (size_t i = 0; i < E; ++i) {
+      const int64_t id = events[i].op_id;
+      uint64_t x = (uint64_t)id * 0x9E3779B97F4A7C15ull;
+      size_t s_ = (size_t)(x ^ (x >> 29)) & mask;
+      while (val[s_] != EV_INF && key[s_] != id) s_ = (s_ + 1) & mask;
+      if (val[s_] == EV_INF) {
+        key[s_] = id;
+        val[s_] = (uint32_t)ids.size();
+        ids.push_back(id);
+      }
+      dense[i] = val[s_];
     }
-    dense[i] = it->second;
   }
   const uint32_t m = (uint32_t)ids.size();
   std::vector<uint32_t> ncall(m, 0), nret(m, 0), call(m, EV_INF), ret(m, EV_INF);
@@ -131,37 +141,45 @@ int History::finalize() {
 
   // Greedy interval colouring (ops by call order; reuse the chain that
   // finished earliest if it finished before this call): K = max overlap.
-  std::vector<std::vector<uint32_t>> chains;
-  using P = std::pair<uint32_t, uint32_t>;  // (last ret, chain)
-  std::priority_queue<P, std::vector<P>, std::greater<P>> heap;
-  for (uint32_t d = 0; d < m; ++d) {
-    uint32_t c;
-    if (!heap.empty() && heap.top().first < call[d]) { c = heap.top().second; heap.pop(); }
-    else { c = (uint32_t)chains.size(); chains.emplace_back(); }
-    chains[c].push_back(d);
-    heap.push({ret[d], c});
+  std::vector<uint32_t> chain_of(m), chain_len;
+  {
+    using P = std::pair<uint32_t, uint32_t>;  // (last ret, chain)
+    std::vector<P> hv;
+    hv.reserve(64);
+    std::priority_queue<P, std::vector<P>, std::greater<P>> heap(std::greater<P>(), std::move(hv));
+    for (uint32_t d = 0; d < m; ++d) {
+      uint32_t c;
+      if (!heap.empty() && heap.top().first < call[d]) { c = heap.top().second; heap.pop(); }
+      else { c = (uint32_t)chain_len.size(); chain_len.push_back(0); }
+      chain_of[d] = c;
+      chain_len[c]++;
+      heap.push({ret[d], c});
+    }
   }
-  K = (uint32_t)chains.size();
+  K = (uint32_t)chain_len.size();
   chain_start.resize(K + 1);
   uint32_t pos = 0;
   for (uint32_t c = 0; c < K; ++c) {
     chain_start[c] = pos;
-    pos += (uint32_t)chains[c].size() + 1;
-    max_chain_len = std::max<uint32_t>(max_chain_len, (uint32_t)chains[c].size());
+    pos += chain_len[c] + 1;
+    max_chain_len = std::max<uint32_t>(max_chain_len, chain_len[c]);
   }
   chain_start[K] = pos;
   recs.assign(pos, OpRec{});
   rec_op.assign(pos, EV_INF);
-  for (uint32_t c = 0; c < K; ++c) {
-    uint32_t p = chain_start[c];
-    for (uint32_t d : chains[c]) {
+  {
+    std::vector<uint32_t> fill(chain_start.begin(), chain_start.end() - 1);  // next slot of each chain
+    for (uint32_t d = 0; d < m; ++d) {  // call order within every chain
+      const uint32_t p = fill[chain_of[d]]++;
       OpRec& r = recs[p];
       r = rec_of(d);
       if (r.flags & OPF_CLS_E) n_ident++;
       rec_op[p] = d;
       op_rec[d] = p;
-      ++p;
     }
+  }
+  for (uint32_t c = 0; c < K; ++c) {
+    const uint32_t p = chain_start[c + 1] - 1;
     OpRec& s = recs[p];  // sentinel
     s.call_ev = EV_INF;
     s.ret_ev = EV_INF;

@@ -477,22 +477,29 @@ struct Fast {
   bool peek(char c) const { return p < end && *p == (uint8_t)c; }
   // a non-negative integer literal in uint64 range, not followed by a
   // fraction or exponent (those are type errors: the general parser reports them)
+  static bool is_digit(uint8_t c) { return c >= '0' && c <= '9'; }
+  // eight ASCII digits -> value (little-endian SWAR)
+  static uint32_t eight(const uint8_t* q) {
+    uint64_t v;
+    memcpy(&v, q, 8);
+    v -= 0x3030303030303030ull;
+    v = v * 10 + (v >> 8);
+    v = (((v & 0x000000FF000000FFull) * 0x000F424000000064ull) +
+         (((v >> 16) & 0x000000FF000000FFull) * 0x0000271000000001ull)) >> 32;
+    return (uint32_t)v;
+  }
   bool u64(uint64_t& v) {
-    if (p >= end || *p < '0' || *p > '9') return false;
-    if (*p == '0') {
-      ++p;
-      v = 0;
-    } else {
-      uint64_t r = 0;
-      while (p < end && *p >= '0' && *p <= '9') {
-        const uint32_t d = *p - '0';
-        if (r > (~0ull - d) / 10) return false;
-        r = r * 10 + d;
-        ++p;
-      }
-      v = r;
-    }
-    return !(p < end && (*p == '.' || *p == 'e' || *p == 'E' || (*p >= '0' && *p <= '9')));
+    const uint8_t* s = p;
+    while (p < end && is_digit(*p)) ++p;
+    const size_t n = (size_t)(p - s);
+    if (n == 0 || n > 20 || (n > 1 && s[0] == '0')) return false;
+    if (n == 20 && memcmp(s, "18446744073709551615", 20) > 0) return false;  // beyond uint64
+    uint64_t r = 0;
+    size_t k = 0;
+    for (; k + 8 <= n; k += 8) r = r * 100000000ull + eight(s + k);
+    for (; k < n; ++k) r = r * 10 + (uint64_t)(s[k] - '0');
+    v = r;
+    return !(p < end && (*p == '.' || *p == 'e' || *p == 'E'));
   }
   bool i64(int64_t& v) {
     uint64_t u;
