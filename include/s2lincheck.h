@@ -284,6 +284,12 @@ typedef struct s2lc_batch_stats {
   uint32_t level_syncs;
   uint32_t _pad2;
   uint64_t n_ops_total;      /* ops over the batch's histories (sizes s2lc_batch_results_flat's ids) */
+  /* pack_kernel<8>: histories with at most 8 chains (every C4 history), one
+   * 8-lane group each */
+  double pack8_ms;
+  uint64_t pack8_algo_bytes;
+  uint32_t pack8_histories;
+  uint32_t _pad3;
 } s2lc_batch_stats;
 int s2lc_batch_stats_get(const s2lc_batch* b, s2lc_batch_stats* out);
 /* With S2LC_F_ROUND_COUNTS: the unique-configuration count of each completed

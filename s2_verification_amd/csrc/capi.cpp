@@ -632,6 +632,9 @@ int s2lc_batch_stats_get(const s2lc_batch* b, s2lc_batch_stats* out) {
   uint64_t ops = 0;
   for (const History* h : b->b.src) ops += h->n_ops;
   out->n_ops_total = ops;
+  out->pack8_ms = b->stats.pack8_ms;
+  out->pack8_algo_bytes = b->stats.pack8_algo_bytes;
+  out->pack8_histories = b->stats.pack8_histories;
   return 0;
 }
 

@@ -5,9 +5,9 @@
 // configuration in 93 % of histories, at most 4 in 99.8 %), so a workgroup- or
 // wave-per-history kernel leaves 60+ of 64 lanes idle and is VALU-issue bound
 // (round-1 PROF build: ~38k cycles per round, 64 % of them in a one-lane
-// closure). Here a GROUP of L lanes (L = 16 or 32, a power of two >= K) owns
-// one history, so a wave checks 64/L histories at once, and inside a group
-// lane l owns chain l:
+// closure). Here a GROUP of L lanes (L = 8, 16 or 32, a power of two >= K)
+// owns one history, so a wave checks 64/L histories at once (C4: K <= 8, eight
+// histories per wave), and inside a group lane l owns chain l:
 //   - expand: lane l tries the head of chain l as the next non-identity op
 //     (the candidates of porcupine's checkSingle loop, upstream checker.go),
 //     folding the record hashes (main.go:227-244) only when the tail matches;
@@ -61,7 +61,8 @@ __device__ __forceinline__ void wave_lds_sync() {
 // Group min-reductions. A 16-lane group is one DPP row: quad_perm [1,0,3,2],
 // quad_perm [2,3,0,1], row_ror:4, row_ror:8 leave the row minimum in every
 // lane with VALU data-parallel moves (no LDS round trip, unlike ds_bpermute,
-// which __shfl_xor compiles to). A 32-lane group adds one bpermute (lane ^ 16).
+// which __shfl_xor compiles to). An 8-lane group (half a row) ends with
+// row_half_mirror; a 32-lane group adds one bpermute (lane ^ 16).
 template <int CTRL>
 __device__ __forceinline__ uint32_t dpp_u32(uint32_t v) {
   return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, CTRL, 0xF, 0xF, false);
@@ -76,6 +77,7 @@ template <int L>
 __device__ __forceinline__ uint32_t gmin_u32(uint32_t v) {
   v = min(v, dpp_u32<0xB1>(v));
   v = min(v, dpp_u32<0x4E>(v));
+  if (L == 8) return min(v, dpp_u32<0x141>(v));  // row_half_mirror: the other quad of the 8-lane group
   v = min(v, dpp_u32<0x124>(v));
   v = min(v, dpp_u32<0x128>(v));
   if (L == 32) v = min(v, (uint32_t)__shfl_xor((int)v, 16, 64));
@@ -86,6 +88,7 @@ template <int L>
 __device__ __forceinline__ uint64_t gmin_u64(uint64_t v) {
   v = dpp_min_u64<0xB1>(v);
   v = dpp_min_u64<0x4E>(v);
+  if (L == 8) return dpp_min_u64<0x141>(v);
   v = dpp_min_u64<0x124>(v);
   v = dpp_min_u64<0x128>(v);
   if (L == 32) {
@@ -206,8 +209,11 @@ __device__ __forceinline__ int pack_closure(ChainLane& ch, const uint64_t* __res
 #define PK_LAP(i) do { } while (0)
 #endif
 
+#ifndef S2LC_PACK_MINW
+#define S2LC_PACK_MINW 1
+#endif
 template <int L>
-__global__ __launch_bounds__(PACK_BLOCK) void pack_kernel(Params p) {
+__global__ __launch_bounds__(PACK_BLOCK, S2LC_PACK_MINW) void pack_kernel(Params p) {
 #ifdef S2LC_PROF
   unsigned long long pk_acc[6] = {0, 0, 0, 0, 0, 0};
   unsigned long long pk_t = 0;

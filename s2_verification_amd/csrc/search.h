@@ -108,7 +108,8 @@ struct DevBatch {
   uint32_t* moves = nullptr;        // witness moves (per history at witness_off)
   uint32_t* rcounts = nullptr;      // per-round unique configurations (same offsets as moves)
   uint32_t* list = nullptr;         // histories of a workgroup pass
-  uint32_t n_pack16 = 0, n_pack32 = 0;
+  uint32_t n_pack8 = 0, n_pack16 = 0, n_pack32 = 0;  // packed-kernel lists (order[]: pack8 | pack16 | pack32)
+  uint32_t pack8_kmax = 8;                            // K bound of the pack8 list (0: none)
   std::vector<uint32_t> lpt;        // searchable histories, longest (n_ops x K) first
   std::vector<uint64_t> h_in_bytes; // per history: input SoA bytes (48 per op + 8 per record hash)
   LevelBufs lv;
@@ -118,7 +119,7 @@ struct DevBatch {
   uint64_t trace_cap = 0;
   uint8_t* slab = nullptr;
   size_t slab_cap = 0;
-  hipEvent_t ev[6] = {nullptr, nullptr, nullptr, nullptr, nullptr, nullptr};
+  hipEvent_t ev[8] = {nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr};
   // host views
   HistDesc* h_hist = nullptr;        // in stage
   HistResult* h_res = nullptr;       // in stage (pinned: the per-run read-back is a direct DMA)
@@ -152,6 +153,9 @@ struct RunStats {
   double pack16_ms = 0;              // pack_kernel<16> launch (HIP events)
   uint64_t pack16_algo_bytes = 0;    // algorithmic bytes of the histories it settled
   uint32_t pack16_histories = 0;
+  double pack8_ms = 0;               // pack_kernel<8> (K <= 8: every C4 history)
+  uint64_t pack8_algo_bytes = 0;
+  uint32_t pack8_histories = 0;
   LevelStats level;
 };
 

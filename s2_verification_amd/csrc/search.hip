@@ -257,12 +257,22 @@ int batch_upload(DevBatch& b, const std::vector<const History*>& hs, uint32_t re
   std::stable_sort(b.lpt.begin(), b.lpt.end(), [&](uint32_t x, uint32_t y) {
     return (uint64_t)b.h_hist[x].n_ops * b.h_hist[x].K > (uint64_t)b.h_hist[y].n_ops * b.h_hist[y].K;
   });
-  // the packed-kernel lists (engine AUTO): K <= 16, then 16 < K <= 32
+  // the packed-kernel lists (engine AUTO): K <= 16, 16 < K <= 32, and with
+  // S2LC_PACK8=1 the K <= 8 histories in 8-lane groups first. Off by default:
+  // at C4's 10k histories a launch lasts about one history's chain of rounds
+  // (~2.3 ms either way), and the 8-lane launch runs before the
+  // 16-lane one for the rest; 8-lane groups pay off only on batches several
+  // times larger (twice the histories per wave).
+  const char* e8 = getenv("S2LC_PACK8");
+  const uint32_t k8 = (e8 && e8[0] == '1') ? 8u : 0u;
+  b.pack8_kmax = k8;
   uint32_t no = 0;
-  for (uint32_t i : b.lpt) if (b.h_hist[i].K <= 16) s_order[no++] = i;
-  b.n_pack16 = no;
+  for (uint32_t i : b.lpt) if (b.h_hist[i].K <= k8) s_order[no++] = i;
+  b.n_pack8 = no;
+  for (uint32_t i : b.lpt) if (b.h_hist[i].K > k8 && b.h_hist[i].K <= 16) s_order[no++] = i;
+  b.n_pack16 = no - b.n_pack8;
   for (uint32_t i : b.lpt) if (b.h_hist[i].K > 16 && b.h_hist[i].K <= 32) s_order[no++] = i;
-  b.n_pack32 = no - b.n_pack16;
+  b.n_pack32 = no - b.n_pack8 - b.n_pack16;
   HIPCHK(hipMemcpy(b.arena, b.stage, stage_bytes, hipMemcpyHostToDevice));
   return 0;
 }
@@ -353,37 +363,43 @@ int batch_run(DevBatch& b, hipStream_t stream, const RunOpts& ro, RunStats& st, 
     if (engine == S2LC_ENGINE_LEVEL || K > 128) level.push_back(i);
     else if (!use_pack || K > 32) todo.push_back(i);
   }
-  // histories settled by pack_kernel<16> (roofline accounting of that kernel)
-  std::vector<uint8_t> pack16_done(b.n_hist, 0);
-  if (use_pack && b.n_pack16 + b.n_pack32) {
+  // histories settled by pack_kernel<8> / <16> (roofline accounting of those kernels)
+  std::vector<uint8_t> pack_done(b.n_hist, 0);  // 8 or 16: the kernel that settled it
+  const uint32_t n_packed = b.n_pack8 + b.n_pack16 + b.n_pack32;
+  if (use_pack && n_packed) {
 #ifdef S2LC_PROF
     {
       unsigned long long z[16] = {0};
       HIPCHK(hipMemcpyToSymbol(HIP_SYMBOL(g_prof), z, sizeof z));
     }
 #endif
-    // Packed passes: one L-lane group per history (K <= 16: L = 16, K <= 32:
-    // L = 32), frontier <= PACK_F. Both launches, then (witness on) the walk of
-    // the histories they settled, then one results read-back: a batch that
-    // needs no other pass (all of C4) costs a single host sync per run.
-    bool launched[2] = {false, false};
-    for (int li = 0; li < 2; ++li) {
-      const uint32_t n_l = li == 0 ? b.n_pack16 : b.n_pack32;
+    // Packed passes: one L-lane group per history (K <= 8: L = 8, K <= 16:
+    // L = 16, K <= 32: L = 32), frontier <= PACK_F. All launches, then
+    // (witness on) the walk of the histories they settled, then one results
+    // read-back: a batch that needs no other pass (all of C4) costs a single
+    // host sync per run.
+    bool launched[3] = {false, false, false};
+    const uint32_t n_list[3] = {b.n_pack8, b.n_pack16, b.n_pack32};
+    const uint32_t first[3] = {0, b.n_pack8, b.n_pack8 + b.n_pack16};
+    for (int li = 0; li < 3; ++li) {
+      const uint32_t n_l = n_list[li];
       if (n_l == 0) continue;
       Params pp = prm;
-      pp.order = b.order + (li == 0 ? 0 : b.n_pack16);
+      pp.order = b.order + first[li];
       pp.n_hist = n_l;
       pp.counter = b.counter + 12 + li;
-      const uint32_t L = li == 0 ? 16 : 32;
-      const size_t smem = li == 0 ? pack_smem_bytes<16>() : pack_smem_bytes<32>();
+      const uint32_t L = 8u << li;
+      const size_t smem = li == 0 ? pack_smem_bytes<8>() : li == 1 ? pack_smem_bytes<16>() : pack_smem_bytes<32>();
       int bpc = 1;
-      if (li == 0) HIPCHK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&bpc, pack_kernel<16>, PACK_BLOCK, smem));
+      if (li == 0) HIPCHK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&bpc, pack_kernel<8>, PACK_BLOCK, smem));
+      else if (li == 1) HIPCHK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&bpc, pack_kernel<16>, PACK_BLOCK, smem));
       else HIPCHK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&bpc, pack_kernel<32>, PACK_BLOCK, smem));
       const uint32_t groups = PACK_BLOCK / L;
       const uint32_t grid = std::max<uint32_t>(
           1, std::min<uint32_t>((n_l + groups - 1) / groups, (uint32_t)n_cu * (uint32_t)std::max(1, bpc)));
       HIPCHK(hipEventRecord(b.ev[2 * li], stream));
-      if (li == 0) hipLaunchKernelGGL(pack_kernel<16>, dim3(grid), dim3(PACK_BLOCK), smem, stream, pp);
+      if (li == 0) hipLaunchKernelGGL(pack_kernel<8>, dim3(grid), dim3(PACK_BLOCK), smem, stream, pp);
+      else if (li == 1) hipLaunchKernelGGL(pack_kernel<16>, dim3(grid), dim3(PACK_BLOCK), smem, stream, pp);
       else hipLaunchKernelGGL(pack_kernel<32>, dim3(grid), dim3(PACK_BLOCK), smem, stream, pp);
       HIPCHK(hipGetLastError());
       HIPCHK(hipEventRecord(b.ev[2 * li + 1], stream));
@@ -397,13 +413,14 @@ int batch_run(DevBatch& b, hipStream_t stream, const RunOpts& ro, RunStats& st, 
     }
     HIPCHK(hipMemcpyAsync(b.h_res, b.res, b.n_hist * sizeof(HistResult), hipMemcpyDeviceToHost, stream));
     HIPCHK(hipStreamSynchronize(stream));
-    for (int li = 0; li < 2; ++li) {
+    for (int li = 0; li < 3; ++li) {
       if (!launched[li]) continue;
       float ms = 0;
       HIPCHK(hipEventElapsedTime(&ms, b.ev[2 * li], b.ev[2 * li + 1]));
       st.kernel_ms += ms;
       st.pack_ms += ms;
-      if (li == 0) st.pack16_ms = ms;
+      if (li == 0) st.pack8_ms = ms;
+      if (li == 1) st.pack16_ms = ms;
     }
 #ifdef S2LC_PROF
     {
@@ -420,7 +437,8 @@ int batch_run(DevBatch& b, hipStream_t stream, const RunOpts& ro, RunStats& st, 
       const uint32_t K = b.h_hist[i].K;
       if (K > 32) continue;
       if (b.h_res[i].verdict == V_UNKNOWN && b.h_res[i].reason == S2LC_R_FRONTIER) over.push_back(i);
-      else if (K <= 16) pack16_done[i] = 1;
+      else if (K <= b.pack8_kmax) pack_done[i] = 8;
+      else if (K <= 16) pack_done[i] = 16;
     }
     st.n_overflow = (uint32_t)over.size();
     over.insert(over.end(), todo.begin(), todo.end());
@@ -524,7 +542,7 @@ int batch_run(DevBatch& b, hipStream_t stream, const RunOpts& ro, RunStats& st, 
                        (const TraceEnt*)b.trace, b.moves);
     HIPCHK(hipGetLastError());
   }
-  if (b.n_hist && (other_work || !(b.n_pack16 + b.n_pack32)))
+  if (b.n_hist && (other_work || !(b.n_pack8 + b.n_pack16 + b.n_pack32)))
     HIPCHK(hipMemcpyAsync(b.h_res, b.res, b.n_hist * sizeof(HistResult), hipMemcpyDeviceToHost, stream));
   if (ro.round_counts) {  // every engine wrote its rounds' counts on the device
     b.h_rcounts.resize(std::max<uint64_t>(b.moves_cap, 1));
@@ -545,10 +563,13 @@ int batch_run(DevBatch& b, hipStream_t stream, const RunOpts& ro, RunStats& st, 
     st.rounds += r.rounds;
     const uint64_t S = 8 * ((2 * (uint64_t)b.h_hist[i].K + 20 + 7) / 8);
     st.algo_bytes += 2 * S * r.configs + 8 * r.children;
-    if (pack16_done[i]) {
+    if (pack_done[i] == 16) {
       // pack_kernel<16> alone: its histories' search bytes + their input SoA
       st.pack16_algo_bytes += 2 * S * r.configs + 8 * r.children + b.h_in_bytes[i];
       st.pack16_histories++;
+    } else if (pack_done[i] == 8) {
+      st.pack8_algo_bytes += 2 * S * r.configs + 8 * r.children + b.h_in_bytes[i];
+      st.pack8_histories++;
     }
   }
   b.rc_valid = ro.round_counts;

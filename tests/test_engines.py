@@ -120,10 +120,33 @@ def test_mid_k_histories_take_search_kernel(name):
     b, res = run(checker_for(), [h])
     r = res[0]
     st = b.stats()
-    assert st["pack16_histories"] == 0 and st["level_histories"] == 0, st
+    assert st["pack8_histories"] == 0 and st["pack16_histories"] == 0 and st["level_histories"] == 0, st
     assert r.verdict == v, (name, r)
     if r.verdict == s2.Ok:
         assert r.witness is not None and len(r.witness) == h.info()["n_ops"]
+
+
+@pytest.mark.parametrize("pack8", [True, False])
+def test_packed_kernels_round_counts(pack8, monkeypatch):
+    """The packed kernels (16-lane groups for K <= 16, or with S2LC_PACK8=1
+    8-lane groups for K <= 8 first): verdicts and per-round unique-configuration
+    counts equal the CPU reduced search."""
+    from s2_verification_amd import workloads as W
+    if pack8:
+        monkeypatch.setenv("S2LC_PACK8", "1")
+    hs = W.c4_histories(120, first_seed=8100) + [W.config_history(n) for n in ("C1", "C2", "C3")]
+    c = s2.Checker(round_counts=True)
+    b = c.batch(hs)
+    res = b.check()
+    st = b.stats()
+    n8 = sum(1 for h in hs if h.info()["n_chains"] <= 8)
+    assert (st["pack8_histories"] >= n8 - st["n_overflow"] and n8 > 0) if pack8 else st["pack8_histories"] == 0, st
+    for i, (h, r) in enumerate(zip(hs, res)):
+        v, ost = orc.check_reduced(orc.from_s2lc_numpy(h.events_numpy()), round_counts=True)
+        assert r.verdict == v, (pack8, i, r, v)
+        assert b.round_counts(i) == ost["round_counts"], (pack8, i)
+        if r.verdict == s2.Ok:
+            assert r.witness is not None and len(r.witness) == h.info()["n_ops"]
 
 
 ABLATIONS = {"all_on": 0, "no_p1": s2.RED_P1, "no_p2": s2.RED_P2, "no_p4": s2.RED_P4, "no_idefer": s2.RED_IDEFER}
@@ -254,8 +277,12 @@ def test_rerun_does_not_reuse_stale_results(monkeypatch):
     r2 = b.check()
     st2 = b.stats()
     assert r1[0].verdict == s2.Unknown and r1[0].reason == "frontier", r1[0]
-    assert [(r.verdict, r.reason, r.configs_explored) for r in r1] == [(r.verdict, r.reason, r.configs_explored)
-                                                                      for r in r2]
+    # the overflowing history: same verdict and reason (where in the search the
+    # tiny staging array overflows depends on which waves reserve slots first);
+    # every other history: identical results
+    assert (r1[0].verdict, r1[0].reason) == (r2[0].verdict, r2[0].reason)
+    assert [(r.verdict, r.reason, r.configs_explored) for r in r1[1:]] == [(r.verdict, r.reason, r.configs_explored)
+                                                                          for r in r2[1:]]
     assert st1["level_histories"] == st2["level_histories"] == 1
     assert st2["n_overflow"] == 0
     expect = [orc.check_wgl(orc.from_s2lc_numpy(h.events_numpy()))[0] for h in hs[1:]]
