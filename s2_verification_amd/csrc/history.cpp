@@ -143,17 +143,35 @@ int History::finalize() {
   // finished earliest if it finished before this call): K = max overlap.
   std::vector<uint32_t> chain_of(m), chain_len;
   {
-    using P = std::pair<uint32_t, uint32_t>;  // (last ret, chain)
-    std::vector<P> hv;
-    hv.reserve(64);
-    std::priority_queue<P, std::vector<P>, std::greater<P>> heap(std::greater<P>(), std::move(hv));
+    // the chain with the smallest (last ret, index) that ended before the call
+    std::vector<uint32_t> last;  // last ret of each chain
+    using P = std::pair<uint32_t, uint32_t>;  // (last ret, chain), for wide histories
+    std::priority_queue<P, std::vector<P>, std::greater<P>> heap;
+    bool use_heap = false;
     for (uint32_t d = 0; d < m; ++d) {
-      uint32_t c;
-      if (!heap.empty() && heap.top().first < call[d]) { c = heap.top().second; heap.pop(); }
-      else { c = (uint32_t)chain_len.size(); chain_len.push_back(0); }
+      uint32_t c = EV_INF;
+      if (!use_heap) {
+        uint32_t best = EV_INF;
+        for (uint32_t k = 0; k < (uint32_t)last.size(); ++k)
+          if (last[k] < best) { best = last[k]; c = k; }
+        if (best >= call[d]) c = EV_INF;
+      } else if (!heap.empty() && heap.top().first < call[d]) {
+        c = heap.top().second;
+        heap.pop();
+      }
+      if (c == EV_INF) {
+        c = (uint32_t)chain_len.size();
+        chain_len.push_back(0);
+        last.push_back(0);
+      }
       chain_of[d] = c;
       chain_len[c]++;
-      heap.push({ret[d], c});
+      last[c] = ret[d];
+      if (use_heap) heap.push({ret[d], c});
+      if (!use_heap && last.size() > 32) {  // many chains: switch to the heap (same choices)
+        use_heap = true;
+        for (uint32_t k = 0; k < (uint32_t)last.size(); ++k) heap.push({last[k], k});
+      }
     }
   }
   K = (uint32_t)chain_len.size();

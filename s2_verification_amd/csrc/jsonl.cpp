@@ -467,10 +467,20 @@ struct Dec {
 struct Fast {
   const uint8_t* p;
   const uint8_t* end;
+  // the literal w at p (eight bytes per compare; w is a compile-time constant)
   template <size_t N>
   bool lit(const char (&w)[N]) {
-    const size_t n = N - 1;
-    if ((size_t)(end - p) < n || memcmp(p, w, n) != 0) return false;
+    constexpr size_t n = N - 1;
+    if ((size_t)(end - p) < n) return false;
+    size_t i = 0;
+    for (; i + 8 <= n; i += 8) {
+      uint64_t a, b;
+      memcpy(&a, p + i, 8);
+      memcpy(&b, w + i, 8);
+      if (a != b) return false;
+    }
+    for (; i < n; ++i)
+      if (p[i] != (uint8_t)w[i]) return false;
     p += n;
     return true;
   }
@@ -488,9 +498,25 @@ struct Fast {
          (((v >> 16) & 0x000000FF000000FFull) * 0x0000271000000001ull)) >> 32;
     return (uint32_t)v;
   }
+  // length of the digit run at s (eight bytes per step: the first byte whose
+  // high nibble is not 3, or whose value + 6 leaves the 0x3_ range, ends it)
+  size_t digits(const uint8_t* s) const {
+    size_t n = 0;
+    while (s + n + 8 <= end) {
+      uint64_t v;
+      memcpy(&v, s + n, 8);
+      const uint64_t a = (v & 0xF0F0F0F0F0F0F0F0ull) ^ 0x3030303030303030ull;
+      const uint64_t b = ((v + 0x0606060606060606ull) & 0xF0F0F0F0F0F0F0F0ull) ^ 0x3030303030303030ull;
+      const uint64_t m = a | b;
+      if (m) return n + (size_t)(__builtin_ctzll(m) >> 3);
+      n += 8;
+    }
+    while (s + n < end && is_digit(s[n])) ++n;
+    return n;
+  }
   bool u64(uint64_t& v) {
     const uint8_t* s = p;
-    while (p < end && is_digit(*p)) ++p;
+    p += digits(s);
     const size_t n = (size_t)(p - s);
     if (n == 0 || n > 20 || (n > 1 && s[0] == '0')) return false;
     if (n == 20 && memcmp(s, "18446744073709551615", 20) > 0) return false;  // beyond uint64
@@ -533,13 +559,18 @@ struct Fast {
 // collector's form, nothing was changed).
 size_t fast_record(const uint8_t* base, const uint8_t* end, History& h) {
   Fast F{base, end};
-  Event e;
+  h.events.emplace_back();  // decoded in place; dropped again if the record is not in the collector's form
+  Event& e = h.events.back();
   size_t pool0 = h.pool.size();
   bool set_has = false, tok_has = false;
   const char *set_s = nullptr, *tok_s = nullptr;
   size_t set_n = 0, tok_n = 0;
-  auto undo = [&]() { h.pool.resize(pool0); return (size_t)0; };
-  if (!F.lit("{\"event\":{\"")) return 0;
+  auto undo = [&]() {
+    h.pool.resize(pool0);
+    h.events.pop_back();
+    return (size_t)0;
+  };
+  if (!F.lit("{\"event\":{\"")) return undo();
   if (F.lit("Start\":")) {
     e.kind = 0;
     if (F.lit("\"Read\"")) {
@@ -547,10 +578,10 @@ size_t fast_record(const uint8_t* base, const uint8_t* end, History& h) {
     } else if (F.lit("\"CheckTail\"")) {
       e.input_type = S2LC_INPUT_CHECK_TAIL;
     } else {
-      if (!F.lit("{\"Append\":{\"num_records\":")) return 0;
+      if (!F.lit("{\"Append\":{\"num_records\":")) return undo();
       e.input_type = S2LC_INPUT_APPEND;
       e.has_num_records = 1;
-      if (!F.u64(e.num_records) || !F.lit(",\"record_hashes\":[")) return 0;
+      if (!F.u64(e.num_records) || !F.lit(",\"record_hashes\":[")) return undo();
       if (!F.peek(']')) {
         for (;;) {
           uint64_t v;
@@ -584,23 +615,23 @@ size_t fast_record(const uint8_t* base, const uint8_t* end, History& h) {
       if (F.lit("\"AppendDefiniteFailure\"")) e.definite = 1;
       else if (F.lit("\"AppendIndefiniteFailure\"")) e.definite = 0;
       else if (F.lit("\"ReadFailure\"") || F.lit("\"CheckTailFailure\"")) e.definite = 1;
-      else return 0;
+      else return undo();
     } else {
       e.failure = 0;
       e.definite = 0;
       e.has_tail = 1;
       if (F.lit("{\"AppendSuccess\":{\"tail\":") || F.lit("{\"CheckTailSuccess\":{\"tail\":")) {
-        if (!F.u64(e.tail)) return 0;
+        if (!F.u64(e.tail)) return undo();
       } else if (F.lit("{\"ReadSuccess\":{\"tail\":")) {
         e.has_hash = 1;
-        if (!F.u64(e.tail) || !F.lit(",\"stream_hash\":") || !F.u64(e.stream_hash)) return 0;
+        if (!F.u64(e.tail) || !F.lit(",\"stream_hash\":") || !F.u64(e.stream_hash)) return undo();
       } else {
-        return 0;
+        return undo();
       }
-      if (!F.lit("}}")) return 0;
+      if (!F.lit("}}")) return undo();
     }
   } else {
-    return 0;
+    return undo();
   }
   if (!F.lit("},\"client_id\":") || !F.i64(e.client_id) || !F.lit(",\"op_id\":") || !F.i64(e.op_id) ||
       !F.lit("}"))
@@ -609,7 +640,6 @@ size_t fast_record(const uint8_t* base, const uint8_t* end, History& h) {
   if (F.p < end && !(*F.p == ' ' || *F.p == '\t' || *F.p == '\n' || *F.p == '\r' || *F.p == '{')) return undo();
   if (set_has) e.set_tok = h.intern(std::string(set_s, set_n));
   if (tok_has) e.batch_tok = h.intern(std::string(tok_s, tok_n));
-  h.events.push_back(e);
   return (size_t)(F.p - base);
 }
 
