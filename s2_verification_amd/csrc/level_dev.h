@@ -38,6 +38,7 @@ constexpr uint32_t LV_NONE = 0xFFFFFFFFu;
 constexpr uint32_t LV_HOLE = 0xFFFFFFFEu;  // LCfg::move of a reserved, unused staging slot
 constexpr int LV_BLOCK = 256;
 constexpr uint32_t LV_RESERVE = 8;          // staging slots a wave reserves per atomic
+constexpr unsigned long long LV_PENDING = 1ull << 31;  // table entry whose configuration is still landing (lv_persist)
 
 // A staged / frontier configuration: 128 + 128 * NQ bytes. The header fills
 // one 128-byte line and every 64-counter block another, so no two
@@ -504,16 +505,25 @@ __device__ __forceinline__ void lv_stage_insert(const LvParams& p, const LvRound
   if (lane < 16) st_wt64(reinterpret_cast<unsigned long long*>(o) + lane, w);
 #pragma unroll
   for (int q = 0; q < NQ; ++q) st_wt16(&o->cnt[lane + 64 * q], (uint16_t)(cnt[q] + d[q]));
-  lv_drain();  // the child is in memory before the CAS can hand it to another wave
+  // The CAS goes out with the stores: the entry is published PENDING (bit 31
+  // of the index) and made final once this wave's stores have landed. A wave
+  // that meets a pending entry with its tag waits for the final form before
+  // it reads the configuration. A duplicate never waits for its own stores.
   const uint32_t tag = (uint32_t)(fp >> 32);
   const unsigned long long mine = ((unsigned long long)tag << 32) | k;
   uint32_t slot = (uint32_t)fp & p.ht_mask;
   for (;;) {
     unsigned long long prev = 0;
-    if (lane == 0) prev = atomicCAS(&p.ht[slot], HT_EMPTY, mine);
+    if (lane == 0) prev = atomicCAS(&p.ht[slot], HT_EMPTY, mine | LV_PENDING);
     prev = rl64(prev, 0);
     if (prev == HT_EMPTY) break;
     if ((uint32_t)(prev >> 32) == tag) {
+      while (prev & LV_PENDING) {  // its producer is between its CAS and its final store
+        __builtin_amdgcn_s_sleep(1);
+        unsigned long long x = 0;
+        if (lane == 0) x = ld_agent64(&p.ht[slot]);
+        prev = rl64(x, 0);
+      }
       const LCfg<NQ>* e = lv_cfg<NQ>(p.stg, (uint32_t)prev);
       const unsigned long long et = ld_wt64(&e->tail), eh = ld_wt64(&e->hash), ek = ld_wt64(&e->tok);
       bool ne = et != s.tail || eh != s.hash || (uint32_t)ek != s.tok;
@@ -523,7 +533,10 @@ __device__ __forceinline__ void lv_stage_insert(const LvParams& p, const LvRound
     }
     slot = (slot + 1) & p.ht_mask;
   }
-  // the winner: next-frontier position, table slot, trace entry
+  // the winner: its stores land, then the entry loses its PENDING bit
+  lv_drain();
+  if (lane == 0) atomicExch(&p.ht[slot], mine);
+  // next-frontier position, table slot, trace entry
   uint32_t n = 0;
   if (lane == 0) n = atomicAdd(&p.ctl->nnext, 1u);
   n = rl(n, 0);
