@@ -4,7 +4,7 @@
 # One rocprofv3 --pmc run per counter group (gfx950 slot limits: 8 SQ, 4 TCC
 # with FETCH_SIZE = 3 and WRITE_SIZE = 2, 1 GRBM here). Workloads:
 #   C4 (bench.py, C4 leg only)  -> pack_kernel<16>
-#   C5 (tools/c5run.py C5)      -> lv_persist / lv_round / lv_insert
+#   C5 (tools/c5run.py C5: cold + warm run) -> lv_persist / lv_round / lv_insert
 # Summaries: python3 profiles/pmc_sq.py gpurun_out/<tag> > profiles/<round>/pmc_sq.json
 set -euo pipefail
 TAG=${1:-pmc}
@@ -27,3 +27,4 @@ pmc c4_sq_b c4 SQ_INSTS_SALU SQ_INSTS_SMEM SQ_INSTS_LDS SQ_INSTS_BRANCH SQ_ACTIV
 pmc c5_sq_a c5 SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_INSTS_VALU SQ_INSTS_VMEM GRBM_GUI_ACTIVE
 pmc c5_fetch c5 FETCH_SIZE TCC_ATOMIC
 pmc c5_write c5 WRITE_SIZE TCC_ATOMIC
+pmc c5_atomic c5 TCC_ATOMIC TCC_EA0_ATOMIC

@@ -46,6 +46,7 @@ def load(d):
         for c, v in cs.items():
             out[k][c].append(v)
     return {k: {c: sum(v) / len(v) for c, v in cs.items()} | {"dispatches": max(len(v) for v in cs.values())}
+            | {c + "_total": sum(v) for c, v in cs.items() if c.startswith("TCC_")}
             for k, cs in out.items()}
 
 
@@ -75,6 +76,13 @@ def main():
             continue
         res[os.path.basename(d)] = {k: {**{c: round(v, 1) for c, v in cs.items()}, **derive(cs)}
                                     for k, cs in stats.items() if k in KERNELS}
+        tot = {}
+        for k, cs in stats.items():
+            for c, v in cs.items():
+                if c.endswith("_total") and k.startswith("lv_"):
+                    tot[c] = tot.get(c, 0.0) + v
+        if tot:
+            res[os.path.basename(d)]["level_search_totals"] = {c: round(v, 1) for c, v in tot.items()}
     print(json.dumps(res, indent=1))
 
 
