@@ -30,6 +30,16 @@ namespace s2lc {
 namespace {
 
 constexpr int PACK_F = 8;       // frontier capacity per group (configurations)
+constexpr int PACK_PF = 8;      // record hashes prefetched per lane for the next round's first expansion
+
+// fold with the first PACK_PF hashes already in registers
+__device__ __forceinline__ uint64_t fold_hashes_pf(uint64_t h, const uint64_t (&pf)[PACK_PF],
+                                                   const uint64_t* __restrict__ rs, uint32_t n) {
+#pragma unroll
+  for (int q = 0; q < PACK_PF; ++q)
+    if ((uint32_t)q < n) h = chain_hash(h, pf[q]);
+  return n > (uint32_t)PACK_PF ? fold_hashes_blk(h, rs + PACK_PF, n - PACK_PF) : h;
+}
 constexpr int PACK_BLOCK = 256; // threads per workgroup
 
 template <int L>
@@ -248,6 +258,17 @@ __global__ __launch_bounds__(PACK_BLOCK, S2LC_PACK_MINW) void pack_kernel(Params
     ChainLane ch;
     ch.reset(p.recs + cs, on, ce - cs);
     bool witness_ok = p.witness != 0;
+    // the first record hashes of this lane's head in the next round's first
+    // configuration, loaded right after that configuration's closure so the
+    // load overlaps the round's dedupe / insert / bookkeeping (pf_cc: the count
+    // they belong to; PACK_PF hashes)
+    uint64_t pf[PACK_PF];
+    uint32_t pf_cc = 0xFFFFFFFFu;
+    // witness moves: while every round leaves exactly one configuration the
+    // path is the sequence of those configurations' moves, written as the
+    // rounds go; otherwise lane 0 walks the parent chain at the end
+    uint32_t* const wout = p.moves ? p.moves + p.res[h].witness_off : nullptr;
+    bool linear = wout != nullptr;
 
     uint32_t verdict = V_ILLEGAL, reason = S2LC_R_SEARCH_EXHAUSTED;
     uint32_t found_parent = TRACE_NONE, found_move = TRACE_NONE, found_p4 = 0;
@@ -312,7 +333,10 @@ __global__ __launch_bounds__(PACK_BLOCK, S2LC_PACK_MINW) void pack_kernel(Params
             take_opt = g;
           }
           if (take_opt) {
-            opt.hash = fold_hashes_blk(s.hash, p.pool + r.hash_off, r.hash_cnt);
+            if (f == 0 && pcnt == pf_cc)
+              opt.hash = fold_hashes_pf(s.hash, pf, p.pool + r.hash_off, r.hash_cnt);
+            else
+              opt.hash = fold_hashes_blk(s.hash, p.pool + r.hash_off, r.hash_cnt);
           }
           if (r.flags & OPF_CLS_I) take_id = (!idefer || r.ret_ev == pmin) && !(g && state_eq(opt, s));
         }
@@ -335,6 +359,18 @@ __global__ __launch_bounds__(PACK_BLOCK, S2LC_PACK_MINW) void pack_kernel(Params
           uint32_t mr = 0;
           PK_LAP(2);
           const int cr = pack_closure<L>(ch, p.pool, cnt, ks, hd.flags, gmask, mr);
+          if (cr == CL_ALIVE && nn == 0) {
+            // this child becomes the next round's first configuration: start
+            // loading its candidate heads' record hashes now
+            const OpRec& hr = ch.r;  // the head at cnt (the closure's last pass selected it)
+            pf_cc = 0xFFFFFFFFu;
+            if (on && !(hr.flags & (OPF_SENTINEL | OPF_CLS_E)) && hr.call_ev < mr) {
+              const uint64_t* src = p.pool + hr.hash_off;
+#pragma unroll
+              for (int q = 0; q < PACK_PF; ++q) pf[q] = (uint32_t)q < hr.hash_cnt ? src[q] : 0ull;
+              pf_cc = cnt;
+            }
+          }
           PK_LAP(1);
           const uint32_t mv = is_id ? ((uint32_t)j | MOVE_IDENT) : (uint32_t)j;
           if (cr == CL_COMPLETE || cr == CL_P4) {
@@ -368,6 +404,8 @@ __global__ __launch_bounds__(PACK_BLOCK, S2LC_PACK_MINW) void pack_kernel(Params
       if (overflow) { verdict = V_UNKNOWN; reason = S2LC_R_FRONTIER; break; }
       rounds++;
       if (rc && gl == 0) rc[rounds] = nn;
+      if (linear && nn == 1 && gl == 0) wout[rounds - 1] = nxt[0].move;
+      if (nn > 1) linear = false;
       if (nn == 0) {
         verdict = V_ILLEGAL; reason = S2LC_R_SEARCH_EXHAUSTED;
         deep_trace = curf[0].trace;  // a configuration of the deepest non-empty round
@@ -421,7 +459,38 @@ __global__ __launch_bounds__(PACK_BLOCK, S2LC_PACK_MINW) void pack_kernel(Params
       R.witness_len = 0;
       R.deep_trace = (verdict == V_ILLEGAL && witness_ok) ? deep_trace : TRACE_NONE;
       R.deep_len = deep_len;
-      R.has_witness = ((verdict == V_OK || R.deep_trace != TRACE_NONE) && witness_ok) ? 2u : 0u;  // resolved by walk_kernel
+      const bool want = (verdict == V_OK || R.deep_trace != TRACE_NONE) && witness_ok;
+      uint32_t hw = 0;
+      if (want && wout) {
+        // Ok: the completing move after the path to its parent; Illegal: the
+        // path to a configuration of the deepest non-empty round (walk_kernel's
+        // output, produced here)
+        uint32_t len, pos, idx;
+        if (verdict == V_OK) {
+          len = found_move == TRACE_NONE ? 0u : rounds;
+          if (len) wout[len - 1] = found_move;
+          pos = len ? len - 1 : 0;
+          idx = found_parent;
+        } else {
+          len = deep_len;
+          pos = len;
+          idx = deep_trace;
+        }
+        if (linear) {
+          pos = 0;  // rounds 1 .. len-1 (Ok) / 1 .. len (Illegal) were written as they closed
+        } else {
+          while (pos > 0 && idx != TRACE_NONE) {
+            const TraceEnt e = p.trace[idx];
+            wout[--pos] = e.move;
+            idx = e.parent;
+          }
+        }
+        hw = pos == 0 ? 1u : 0u;
+        R.witness_len = hw ? len : 0u;
+      } else if (want) {
+        hw = 2u;  // no move buffer: resolved by walk_kernel
+      }
+      R.has_witness = hw;
     }
   }
 }

@@ -185,6 +185,7 @@ int batch_upload(DevBatch& b, const std::vector<const History*>& hs, uint32_t re
     b.h_moves_off[i] = (uint32_t)moves_total;
     moves_total += h.n_ops + 1;
   }
+  b.n_ops_total = moves_total - n;
   if (n_recs >= 0xFFFFFFFFull || n_pool >= 0xFFFFFFFFull || moves_total >= 0xFFFFFFFFull) {
     err = "batch too large for 32-bit indices";
     return S2LC_EUNSUPPORTED;
@@ -279,7 +280,7 @@ int batch_upload(DevBatch& b, const std::vector<const History*>& hs, uint32_t re
 
 void batch_release(DevBatch& b) {
   level_release(b);
-  void* dptrs[] = {b.arena, b.counter, b.trace, b.trace_head, b.slab};
+  void* dptrs[] = {b.arena, b.counter, b.trace, b.slab};  // trace_head lives inside counter
   for (void* q : dptrs) if (q) (void)hipFree(q);
   if (b.stage) (void)hipHostFree(b.stage);
   if (b.h_moves) (void)hipHostFree(b.h_moves);
@@ -306,8 +307,9 @@ int batch_run(DevBatch& b, hipStream_t stream, const RunOpts& ro, RunStats& st, 
   (void)hipDeviceGetAttribute(&n_cu, hipDeviceAttributeMultiprocessorCount, dev);
   b.rc_valid = false;
 
-  if (!b.counter) HIPCHK(hipMalloc(&b.counter, 32 * sizeof(uint32_t)));  // [0..15] work counters, [16..17] deadline
-  if (!b.trace_head) HIPCHK(hipMalloc(&b.trace_head, sizeof(unsigned long long)));
+  // [0..15] work counters, [16..17] deadline, [24..25] trace head (one memset clears them)
+  if (!b.counter) HIPCHK(hipMalloc(&b.counter, 32 * sizeof(uint32_t)));
+  b.trace_head = reinterpret_cast<unsigned long long*>(b.counter + 24);
   for (hipEvent_t& e : b.ev)
     if (!e) HIPCHK(hipEventCreate(&e));
   // trace pool: generous, allocated once per batch and reused across runs
@@ -334,11 +336,11 @@ int batch_run(DevBatch& b, hipStream_t stream, const RunOpts& ro, RunStats& st, 
   prm.recs = b.recs; prm.pool = b.pool; prm.chain_start = b.chain_start; prm.hist = b.hist;
   prm.trace = b.trace; prm.trace_head = b.trace_head; prm.trace_cap = witness ? b.trace_cap : 0;
   prm.res = b.res; prm.max_configs = ro.max_configs; prm.witness = witness ? 1 : 0;
+  prm.moves = b.moves;
   prm.n_recs = b.n_recs; prm.n_pool = b.n_pool; prm.n_res = b.n_hist;
   prm.rcounts = ro.round_counts ? b.rcounts : nullptr;
 
-  HIPCHK(hipMemsetAsync(b.counter, 0, 16 * sizeof(uint32_t), stream));
-  HIPCHK(hipMemsetAsync(b.trace_head, 0, sizeof(unsigned long long), stream));
+  HIPCHK(hipMemsetAsync(b.counter, 0, 32 * sizeof(uint32_t), stream));
   if (b.n_hist) {
     hipLaunchKernelGGL(reset_results_kernel, dim3((b.n_hist + 255) / 256), dim3(256), 0, stream, b.res, b.n_hist);
     HIPCHK(hipGetLastError());
@@ -390,10 +392,14 @@ int batch_run(DevBatch& b, hipStream_t stream, const RunOpts& ro, RunStats& st, 
       pp.counter = b.counter + 12 + li;
       const uint32_t L = 8u << li;
       const size_t smem = li == 0 ? pack_smem_bytes<8>() : li == 1 ? pack_smem_bytes<16>() : pack_smem_bytes<32>();
-      int bpc = 1;
-      if (li == 0) HIPCHK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&bpc, pack_kernel<8>, PACK_BLOCK, smem));
-      else if (li == 1) HIPCHK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&bpc, pack_kernel<16>, PACK_BLOCK, smem));
-      else HIPCHK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&bpc, pack_kernel<32>, PACK_BLOCK, smem));
+      int bpc = b.pack_bpc[li];  // resident blocks per CU (queried once per batch)
+      if (bpc == 0) {
+        if (li == 0) HIPCHK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&bpc, pack_kernel<8>, PACK_BLOCK, smem));
+        else if (li == 1) HIPCHK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&bpc, pack_kernel<16>, PACK_BLOCK, smem));
+        else HIPCHK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&bpc, pack_kernel<32>, PACK_BLOCK, smem));
+        bpc = std::max(1, bpc);
+        b.pack_bpc[li] = bpc;
+      }
       const uint32_t groups = PACK_BLOCK / L;
       const uint32_t grid = std::max<uint32_t>(
           1, std::min<uint32_t>((n_l + groups - 1) / groups, (uint32_t)n_cu * (uint32_t)std::max(1, bpc)));
@@ -406,11 +412,7 @@ int batch_run(DevBatch& b, hipStream_t stream, const RunOpts& ro, RunStats& st, 
       launched[li] = true;
       st.launches++;
     }
-    if (witness) {
-      hipLaunchKernelGGL(walk_kernel, dim3((b.n_hist + 255) / 256), dim3(256), 0, stream, b.n_hist, b.res,
-                         (const TraceEnt*)b.trace, b.moves);
-      HIPCHK(hipGetLastError());
-    }
+    // (pack_kernel resolves its histories' witnesses itself: no walk here)
     HIPCHK(hipMemcpyAsync(b.h_res, b.res, b.n_hist * sizeof(HistResult), hipMemcpyDeviceToHost, stream));
     HIPCHK(hipStreamSynchronize(stream));
     for (int li = 0; li < 3; ++li) {

@@ -96,6 +96,7 @@ struct Params {
   unsigned long long* trace_head;
   uint64_t trace_cap;
   HistResult* res;
+  uint32_t* moves;     // witness move lists (pack_kernel resolves its own; nullable)
   uint64_t max_configs;
   uint32_t witness;
   uint32_t n_recs, n_pool, n_res;  // buffer sizes (guard build checks)
