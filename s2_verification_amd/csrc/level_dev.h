@@ -428,6 +428,21 @@ __device__ __forceinline__ uint32_t sel_cnt(const uint32_t (&cnt)[NQ], uint32_t 
   return v;
 }
 
+template <int N>
+__device__ __forceinline__ uint32_t sel_u32(const uint32_t (&a)[N], uint32_t q) {
+  uint32_t v = a[0];
+#pragma unroll
+  for (int i = 1; i < N; ++i) v = q == (uint32_t)i ? a[i] : v;
+  return v;
+}
+template <int N>
+__device__ __forceinline__ uint64_t sel_u64(const uint64_t (&a)[N], uint32_t q) {
+  uint64_t v = a[0];
+#pragma unroll
+  for (int i = 1; i < N; ++i) v = q == (uint32_t)i ? a[i] : v;
+  return v;
+}
+
 typedef __attribute__((address_space(1))) uint16_t lv_g16;
 typedef __attribute__((address_space(1))) uint32_t lv_g32;
 typedef __attribute__((address_space(1))) unsigned long long lv_g64;
@@ -613,13 +628,47 @@ __device__ __forceinline__ bool lv_expand(const LvParams& p, const LvRoundIn& in
     }
     const uint64_t parent_chx = wave_xor_u64(chx);
     LV_LAP(1);
-    uint32_t n_cand = 0;
+    // candidate moves in (slot, lane) order; this slice takes moves [c0, c1)
+    uint32_t n_cand = 0, my_idx[NQ];
+    const uint64_t lt_mask = (1ull << lane) - 1;
 #pragma unroll
-    for (int q = 0; q < NQ; ++q) n_cand += (uint32_t)__popcll(__ballot((cand >> q) & 1u));
+    for (int q = 0; q < NQ; ++q) {
+      const uint64_t bq = __ballot((cand >> q) & 1u);
+      my_idx[q] = n_cand + (uint32_t)__popcll(bq & lt_mask);
+      n_cand += (uint32_t)__popcll(bq);
+    }
     // round 0 has one pseudo-move: the initial configuration itself
     const uint32_t n_moves = pc ? n_cand : 1u;
     const uint32_t c0 = (uint32_t)(((uint64_t)n_moves * slice) / S);
     const uint32_t c1 = (uint32_t)(((uint64_t)n_moves * (slice + 1)) / S);
+    // The outcome of every move of this slice at once (lane l, slot q: the
+    // append at the head of chain l + 64 q): the rest of its record, guards,
+    // outcome and hash fold, for those moves in parallel, so a move in the
+    // loop below costs only its next head's load. Registers: 5 per slot
+    // (NQ <= 6).
+    constexpr bool PRE = NQ <= 6;
+    constexpr int NP = PRE ? NQ : 1;
+    uint64_t mv_tail[NP], mv_hash[NP];
+    uint32_t mv_pk[NP];  // take_opt | take_id << 1 | token << 16
+#pragma unroll
+    for (int q = 0; q < NP; ++q) {
+      mv_tail[q] = ps.tail;
+      mv_hash[q] = ps.hash;
+      mv_pk[q] = ps.tok << 16;
+      if (PRE && ((cand >> q) & 1u) && my_idx[q] >= c0 && my_idx[q] < c1) {
+        const OpRec r = load_rec(p.recs + s_cs[64 * q + lane] + cnt[q]);  // the head: just loaded, cached
+        const bool g = append_guards_ok(r, ps);
+        State opt = ps;
+        opt.tail = ps.tail + r.num_records;
+        opt.tok = r.set_tok ? r.set_tok : ps.tok;
+        const bool to = (r.flags & OPF_CLS_D) ? (g && opt.tail == r.out_tail) : g;
+        if (to || ((r.flags & OPF_CLS_I) && g)) opt.hash = fold_hashes_blk(ps.hash, p.pool + r.hash_off, r.hash_cnt);
+        const bool ti = (r.flags & OPF_CLS_I) && (!idefer || r.ret_ev == pmin) && !(g && state_eq(opt, ps));
+        mv_tail[q] = opt.tail;
+        mv_hash[q] = opt.hash;
+        mv_pk[q] = (to ? 1u : 0u) | (ti ? 2u : 0u) | (opt.tok << 16);
+      }
+    }
     uint32_t ord = 0, q_cur = 0;
     uint64_t m = pc ? __ballot(cand & 1u) : 1ull;
     for (;;) {
@@ -639,24 +688,39 @@ __device__ __forceinline__ bool lv_expand(const LvParams& p, const LvRoundIn& in
       uint4 nx_obs = make_uint4(0, 0, 0, 0), nx_mid = make_uint4(0, 0, 0, 0);
       uint32_t nx_fl = 0;
       LV_LAP(7);
-      if (pc && lane == src) {
-        // the move's record, and the chain's next head (the child's first new head) with it
-        const OpRec* mrec = p.recs + s_cs[64 * q_cur + lane] + sel_cnt<NQ>(cnt, q_cur);
-        const OpRec* nx = mrec + 1;
-        nx_obs = ld16(nx, 16);
-        nx_mid = ld16(nx, 32);
-        nx_fl = nx->flags;
-        const OpRec r = load_rec(mrec);
-        const bool g = append_guards_ok(r, ps);
-        LV_LAP(8);
-        opt.tail = ps.tail + r.num_records;
-        opt.tok = r.set_tok ? r.set_tok : ps.tok;
-        take_opt = (r.flags & OPF_CLS_D) ? (g && opt.tail == r.out_tail) : g;
-        if (take_opt || ((r.flags & OPF_CLS_I) && g)) opt.hash = fold_hashes_blk(ps.hash, p.pool + r.hash_off, r.hash_cnt);
-        if (r.flags & OPF_CLS_I) take_id = (!idefer || r.ret_ev == pmin) && !(g && state_eq(opt, ps));
+      uint32_t fl2;
+      State so;
+      if (PRE) {
+        if (pc && lane == src) {
+          // the chain's next head (the child's first new head)
+          const OpRec* nx = p.recs + s_cs[64 * q_cur + lane] + sel_cnt<NQ>(cnt, q_cur) + 1;
+          nx_obs = ld16(nx, 16);
+          nx_mid = ld16(nx, 32);
+          nx_fl = nx->flags;
+        }
+        const uint32_t pk = rl(sel_u32<NP>(mv_pk, q_cur), src);
+        fl2 = pc ? (pk & 3u) : 1u;
+        so = pc ? State{rl64(sel_u64<NP>(mv_tail, q_cur), src), rl64(sel_u64<NP>(mv_hash, q_cur), src), pk >> 16} : ps;
+      } else {
+        if (pc && lane == src) {
+          // the move's record, and the chain's next head (the child's first new head) with it
+          const OpRec* mrec = p.recs + s_cs[64 * q_cur + lane] + sel_cnt<NQ>(cnt, q_cur);
+          const OpRec* nx = mrec + 1;
+          nx_obs = ld16(nx, 16);
+          nx_mid = ld16(nx, 32);
+          nx_fl = nx->flags;
+          const OpRec r = load_rec(mrec);
+          const bool g = append_guards_ok(r, ps);
+          LV_LAP(8);
+          opt.tail = ps.tail + r.num_records;
+          opt.tok = r.set_tok ? r.set_tok : ps.tok;
+          take_opt = (r.flags & OPF_CLS_D) ? (g && opt.tail == r.out_tail) : g;
+          if (take_opt || ((r.flags & OPF_CLS_I) && g)) opt.hash = fold_hashes_blk(ps.hash, p.pool + r.hash_off, r.hash_cnt);
+          if (r.flags & OPF_CLS_I) take_id = (!idefer || r.ret_ev == pmin) && !(g && state_eq(opt, ps));
+        }
+        fl2 = pc ? rl((take_opt ? 1u : 0u) | (take_id ? 2u : 0u), src) : 1u;
+        so = State{rl64(opt.tail, src), rl64(opt.hash, src), rl(opt.tok, src)};
       }
-      const uint32_t fl2 = pc ? rl((take_opt ? 1u : 0u) | (take_id ? 2u : 0u), src) : 1u;
-      const State so{rl64(opt.tail, src), rl64(opt.hash, src), rl(opt.tok, src)};
       const uint32_t j = (uint32_t)src + 64u * q_cur;
       LV_LAP(2);
 #pragma unroll 1
