@@ -250,13 +250,15 @@ def load_jsonl(text):
             events.append({"kind": "return", **base, **_finish_to_output(ev["Finish"])})
 
 
-def from_s2lc_numpy(ev):
+def from_s2lc_numpy(ev, owner=None):
     """Product-exported events (numpy array in the s2lc_event layout, see
     s2_verification_amd.History.events_numpy) -> EventArray for the oracle.
 
     Token ids are re-derived from the exported string pointers (one pointer per
-    distinct token string within a history); record-hash pointers are used as
-    they are, so the source history must outlive the returned array.
+    distinct token string within a history). The exported record-hash pointers
+    point into the source history: with `owner` (that history) the array keeps
+    it alive and uses them as they are; without it the hashes are copied into a
+    pool the array owns, so the source may be freed.
     """
     n = len(ev)
     arr = np.zeros(n, dtype=EVENT_DTYPE)
@@ -274,5 +276,16 @@ def from_s2lc_numpy(ev):
     arr["batch_tok"] = ids[n:]
     ea = EventArray.__new__(EventArray)
     ea.arr = arr
-    ea.pool = None
+    ea.pool = owner
+    if owner is None:
+        cnt = arr["n_hashes"].astype(np.int64)
+        has = np.nonzero(cnt)[0]
+        offs = np.zeros(n, dtype=np.int64)
+        offs[has] = np.cumsum(cnt[has]) - cnt[has]
+        pool = np.zeros(max(1, int(cnt.sum())), dtype=np.uint64)
+        base = pool.ctypes.data
+        for i in has.tolist():
+            ctypes.memmove(base + 8 * int(offs[i]), int(arr["hashes"][i]), 8 * int(cnt[i]))
+        arr["hashes"] = np.where(cnt > 0, base + offs * 8, 0).astype(arr["hashes"].dtype)
+        ea.pool = pool
     return ea
