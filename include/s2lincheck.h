@@ -282,7 +282,7 @@ typedef struct s2lc_batch_stats {
   uint32_t level_persist_launches;
   uint32_t level_chunk_retries;
   uint32_t level_syncs;
-  uint32_t _pad2;
+  uint32_t level_solo_rounds;/* one-configuration rounds run by one workgroup (LvSolo) */
   uint64_t n_ops_total;      /* ops over the batch's histories (sizes s2lc_batch_results_flat's ids) */
   /* pack_kernel<8>: histories with at most 8 chains (every C4 history), one
    * 8-lane group each */

@@ -629,6 +629,7 @@ int s2lc_batch_stats_get(const s2lc_batch* b, s2lc_batch_stats* out) {
   out->level_persist_launches = (uint32_t)b->stats.level.persist_launches;
   out->level_chunk_retries = b->stats.level.chunk_retries;
   out->level_syncs = b->stats.level.syncs;
+  out->level_solo_rounds = (uint32_t)b->stats.level.solo_rounds;
   out->n_ops_total = b->b.n_ops_total;
   out->pack8_ms = b->stats.pack8_ms;
   out->pack8_algo_bytes = b->stats.pack8_algo_bytes;

@@ -237,6 +237,7 @@ int level_search(DevBatch& b, uint32_t h, hipStream_t st, const RunOpts& ro, int
   for (int i = 0; i < 2; ++i) { pq.stg[i] = L.stg[i]; pq.idx[i] = L.idx[i]; pq.ht[i] = L.ht[i]; }
   pq.max_rounds = 4096;
   pq.nf_max = persist_nf;
+  pq.solo = getenv("S2LC_NO_SOLO") ? 0u : 1u;  // S2LC_NO_SOLO=1: one-configuration rounds on the grid too
   {
     int dev = 0, khz = 100000;
     LVCHK(hipGetDevice(&dev));
@@ -246,8 +247,8 @@ int level_search(DevBatch& b, uint32_t h, hipStream_t st, const RunOpts& ro, int
 
 #ifdef S2LC_PROF
   unsigned long long* d_prof = nullptr;
-  LVCHK(hipMalloc(&d_prof, 16 * sizeof(unsigned long long)));
-  LVCHK(hipMemset(d_prof, 0, 16 * sizeof(unsigned long long)));
+  LVCHK(hipMalloc(&d_prof, 32 * sizeof(unsigned long long)));
+  LVCHK(hipMemset(d_prof, 0, 32 * sizeof(unsigned long long)));
   p.prof = d_prof;
 #endif
   LVCHK(hipEventRecord(L.ev[0], st));
@@ -376,7 +377,7 @@ int level_search(DevBatch& b, uint32_t h, hipStream_t st, const RunOpts& ro, int
   const LvRun fin = *hr;
 #ifdef S2LC_PROF
   {
-    unsigned long long g[16];
+    unsigned long long g[32];
     LVCHK(hipMemcpy(g, d_prof, sizeof g, hipMemcpyDeviceToHost));
     (void)hipFree(d_prof);
     const double it = g[5] ? (double)g[5] : 1.0, ch = g[6] ? (double)g[6] : 1.0;
@@ -391,6 +392,13 @@ int level_search(DevBatch& b, uint32_t h, hipStream_t st, const RunOpts& ro, int
     fprintf(stderr, "[s2lc lvprof] persistent rounds %llu: %.2f us/round, expansion critical path %.2f us/round | "
             "cycles/item move selection %.0f move record loads %.0f\n",
             g[11], g[9] * us / nr, g[10] * us / nr, g[12] / it, g[13] / it);
+    fprintf(stderr, "[s2lc lvprof] solo rounds %llu: %.2f us/round | closures run %llu, opt children dropped by the P1 "
+            "precheck %llu\n", g[7], g[8] * us / (g[7] ? (double)g[7] : 1.0), g[14], g[15]);
+    const double ns = g[7] ? (double)g[7] : 1.0;
+    fprintf(stderr, "[s2lc lvprof] solo cycles/round (wave 0): start %.0f setup %.0f pre %.0f moves %.0f close %.0f next %.0f\n",
+            g[16] / ns, g[17] / ns, g[18] / ns, g[19] / ns, g[20] / ns, g[21] / ns);
+    fprintf(stderr, "[s2lc lvprof] solo closures: ALIVE %llu at %.0f cycles, others %.0f cycles/round; stage %.0f cycles per ALIVE\n",
+            g[24], g[22] / (g[24] ? (double)g[24] : 1.0), g[23] / ns, g[25] / (g[24] ? (double)g[24] : 1.0));
   }
 #endif
   if (aborted) {
@@ -442,6 +450,7 @@ int level_search(DevBatch& b, uint32_t h, hipStream_t st, const RunOpts& ro, int
   ls.max_frontier = std::max(ls.max_frontier, fin.max_frontier);
   ls.histories++;
   ls.syncs += syncs;
+  ls.solo_rounds += fin.solo_rounds;
   return 0;
 }
 

@@ -107,7 +107,8 @@ struct LvRun {
   uint32_t last_tbase;     // trace index of the first winner of the last non-empty round
   uint32_t last_nf;        // frontier expanded by the last round
   unsigned long long last_children;  // children it generated (slices per configuration)
-  uint32_t _pad[2];
+  uint32_t solo_rounds;    // rounds run as solo rounds (LvSolo)
+  uint32_t _pad;
 };
 static_assert(sizeof(LvRun) == 96, "LvRun layout");
 
@@ -326,7 +327,7 @@ template <int NQ>
 __device__ __forceinline__ int lv_closure(LvHot (&H)[NQ], uint32_t (&d)[NQ], const uint32_t (&cnt)[NQ],
                                           const uint32_t* s_cs, const LvHeadsLds<NQ>& PL, int lane, const State& s,
                                           uint32_t hflags, uint32_t minret_seed, const OpRec* __restrict__ recs,
-                                          uint32_t& minret_out) {
+                                          uint32_t& minret_out, const LvHeadsLds<NQ>* NX = nullptr) {
   const bool nowrap = hflags & H_NOWRAP;
   const bool p2 = hflags & H_P2OK;
   const bool p4 = hflags & H_P4;
@@ -359,7 +360,13 @@ __device__ __forceinline__ int lv_closure(LvHot (&H)[NQ], uint32_t (&d)[NQ], con
     for (int q = 0; q < NQ; ++q) {
       if ((adv >> q) & 1u) {
         d[q] += 1;
-        H[q] = lv_load_child_head(recs + s_cs[64 * q + lane] + cnt[q] + d[q], s);
+        if (NX && d[q] == 1) {  // solo rounds: the record after the parent's head is in LDS
+          H[q].suf = NX->suf[q][lane]; H[q].call = NX->call[q][lane]; H[q].ret = NX->ret[q][lane];
+          const uint32_t fl = NX->fl[q][lane];
+          H[q].fl = fl | HB_KNOWN | lv_legal_bits(fl, NX->otail[q][lane], NX->ohash[q][lane], s);
+        } else {
+          H[q] = lv_load_child_head(recs + s_cs[64 * q + lane] + cnt[q] + d[q], s);
+        }
       }
     }
     minret_prev = minret;
@@ -565,22 +572,122 @@ __device__ __forceinline__ void lv_stage_insert(const LvParams& p, const LvRound
   }
 }
 
+// ---- solo rounds: a frontier of ONE configuration ---------------------------
+// Most rounds of a hard history keep exactly one configuration (H174: 10,129
+// of its 10,285 rounds). The children of one configuration are pairwise
+// distinct (each linearizes a different durable / indefinite op, or the same
+// indefinite op with two different states), so such a round needs no dedupe
+// table and no grid: workgroup 0 of lv_persist runs it alone, its four waves
+// splitting the moves, with the configuration's heads kept in LDS from round
+// to round (only the chains the surviving child advanced are reloaded). Every
+// surviving child is written to the staging array exactly as a grid round
+// leaves its frontier (staging slot, next-frontier index, trace entry; no
+// table slot), so grid rounds and the host take over after any solo round.
+// Workgroup barrier over LDS only: waits for this wave's LDS operations, not
+// for its global loads and write-through stores (a __syncthreads release
+// would drain those too). Solo rounds share only LDS between their waves.
+__device__ __forceinline__ void lv_sync_lds() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); }
+
+constexpr int LV_SOLO_HP = 4;  // record hashes of each head kept in LDS
+template <int NQ>
+struct LvSolo {
+  uint64_t hp[LV_SOLO_HP][64 * NQ];  // the heads' first record hashes
+  uint32_t nx_hoff[64 * NQ], nx_hcnt[64 * NQ];  // record-hash range of each head's next record
+  uint16_t cnt[64 * NQ];   // the configuration's chain counts
+  uint16_t keep[64 * NQ];  // advance per chain of the child with staging index 0
+  uint64_t tail, hash, chx;        // the configuration: state, XOR of its chain terms
+  uint64_t ktail, khash, kchx;     // the kept child
+  uint32_t tok, pmin, ptrace, ktok, kmr, cs_end;
+  uint32_t alive, found, fpar, fmov, fp4, ovf, tbase, wit;
+  unsigned long long kids;
+  uint64_t wx[LV_BLOCK / 64];
+#ifdef S2LC_PROF
+  unsigned long long pt[8];  // wave 0 phase cycles: [0] start [1] setup [2] pre [3] moves [4] close [5] next; [7] last stamp
+  unsigned long long pc[4];  // closure cycles (ALIVE, other), ALIVE closures, stage cycles (all waves)
+#endif
+};
+
+// (smallest, second smallest) of the heads' P1 bounds over the wave's chains
+// (a value held by two chains is both), in every lane.
+template <int CTRL>
+__device__ __forceinline__ void lv_min2_step(uint64_t& a, uint64_t& b) {
+  const uint64_t oa = lv_dpp64<CTRL>(a), ob = lv_dpp64<CTRL>(b);
+  const uint64_t lo = lv_min64(a, oa), hi = a < oa ? oa : a;
+  b = lv_min64(hi, lv_min64(b, ob));
+  a = lo;
+}
+template <int NQ>
+__device__ __forceinline__ void wave_min2_hot(const LvHot (&H)[NQ], uint64_t& m1, uint64_t& m2) {
+  uint64_t a = REQ_NONE, b = REQ_NONE;
+#pragma unroll
+  for (int q = 0; q < NQ; ++q) {
+    const uint64_t v = H[q].suf;
+    if (v < a) { b = a; a = v; } else if (v < b) { b = v; }
+  }
+  lv_min2_step<0xB1>(a, b);
+  lv_min2_step<0x4E>(a, b);
+  lv_min2_step<0x124>(a, b);
+  lv_min2_step<0x128>(a, b);
+  m1 = REQ_NONE; m2 = REQ_NONE;
+#pragma unroll
+  for (int row = 0; row < 4; ++row) {
+    const uint64_t ra = rl64(a, 16 * row), rb = rl64(b, 16 * row);
+    const uint64_t lo = lv_min64(m1, ra), hi = m1 < ra ? ra : m1;
+    m2 = lv_min64(hi, lv_min64(m2, rb));
+    m1 = lo;
+  }
+}
+
+// Write one surviving solo child into staging slot k of round r (header line,
+// counters, next-frontier index, trace entry): the form lv_stage_insert leaves.
+template <int NQ>
+__device__ __forceinline__ void lv_solo_put(const LvParams& p, uint32_t k, const State& s, uint64_t fp,
+                                            uint32_t minret, uint32_t ptrace, uint32_t move, uint32_t tbase,
+                                            uint32_t wit, const uint32_t (&cnt)[NQ], const uint32_t (&d)[NQ]) {
+  const int lane = (int)(threadIdx.x & 63);
+  LCfg<NQ>* o = lv_cfg<NQ>(p.stg, k);
+  const uint32_t tr = wit ? p.tgid + tbase + k : TRACE_NONE;
+  const unsigned long long w = lane == 0 ? s.tail
+                             : lane == 1 ? s.hash
+                             : lane == 2 ? fp
+                             : lane == 3 ? ((unsigned long long)minret << 32 | s.tok)
+                             : lane == 4 ? ((unsigned long long)move << 32 | ptrace)
+                             : lane == 5 ? ((unsigned long long)LV_NONE << 32 | tr)
+                                         : 0ull;
+  if (lane < 16) st_wt64(reinterpret_cast<unsigned long long*>(o) + lane, w);
+#pragma unroll
+  for (int q = 0; q < NQ; ++q) st_wt16(&o->cnt[lane + 64 * q], (uint16_t)(cnt[q] + d[q]));
+  if (lane == 0) {
+    st_wt32(&p.nxt_idx[k], k);
+    if (wit) p.trace[tbase + k] = TraceEnt{ptrace, move};
+  }
+}
+
+// P1 bound (sufmin) of a record
+__device__ __forceinline__ uint64_t ld_suf(const OpRec* r) {
+  return *reinterpret_cast<const uint64_t*>(reinterpret_cast<const uint8_t*>(r) + 32);
+}
+
 // ---- expansion: one wave per (frontier configuration, slice of its candidates)
-// FUSED = false: stage into the striped staging array (lv_insert deduplicates);
-// FUSED = true: the persistent kernel's stage-and-insert.
-template <int NQ, bool FUSED>
+// MODE 0: stage into the striped staging array (lv_insert deduplicates);
+// MODE 1: the persistent kernel's stage-and-insert;
+// MODE 2: a solo round (one configuration, in LDS; the four waves of
+//         workgroup 0 take one slice of its moves each).
+template <int NQ, int MODE>
 __device__ __forceinline__ bool lv_expand(const LvParams& p, const LvRoundIn& in, LvHeadsLds<NQ>& PL,
-                                          const uint32_t* s_cs) {
+                                          const uint32_t* s_cs, LvSolo<NQ>* sol = nullptr,
+                                          LvHeadsLds<NQ>* NX = nullptr, const OpRec* FR = nullptr) {
+  constexpr bool FUSED = MODE == 1, SOLO = MODE == 2;
   const int lane = (int)(threadIdx.x & 63);
   const uint32_t K = p.K;
   const bool idefer = p.hflags & H_IDEFER;
   const uint32_t f0 = in.f0, nf = in.nf, S = in.S;
-  const uint32_t nwaves = gridDim.x * (LV_BLOCK / 64);
+  const uint32_t nwaves = SOLO ? LV_BLOCK / 64 : gridDim.x * (LV_BLOCK / 64);
   const uint32_t items = nf * S;
   uint32_t rk = 0, rleft = 0;  // reserved staging slots (wave-uniform)
-  const uint32_t wave_id = blockIdx.x * (LV_BLOCK / 64) + (threadIdx.x >> 6);
+  const uint32_t wave_id = SOLO ? (threadIdx.x >> 6) : blockIdx.x * (LV_BLOCK / 64) + (threadIdx.x >> 6);
   const uint32_t stripe = wave_id & (LV_STRIPES - 1);
-  if (wave_id < items) {  // the first reservation, in flight with the first item's loads
+  if (!SOLO && wave_id < items) {  // the first reservation, in flight with the first item's loads
     uint32_t b0 = 0;
     if (lane == 0) b0 = atomicAdd(&p.ctl->cnt[16 * stripe], LV_RESERVE);
     rk = rl(b0, 0);
@@ -595,11 +702,16 @@ __device__ __forceinline__ bool lv_expand(const LvParams& p, const LvRoundIn& in
     LV_ADD(5, 1);
     const uint32_t f = f0 + it / S;
     const uint32_t slice = it % S;
-    // parent configuration (round 0: the all-zero initial one)
-    const LCfg<NQ>* pc = p.init ? nullptr : lv_cfg<NQ>(p.cur, p.cur_idx[f]);
+    // parent configuration (round 0: the all-zero initial one; solo: in LDS)
+    const LCfg<NQ>* pc = (p.init || SOLO) ? nullptr : lv_cfg<NQ>(p.cur, p.cur_idx[f]);
+    const bool has_parent = SOLO || pc;
     State ps{0, 0, 0};
     uint32_t pmin = 0, ptrace = TRACE_NONE;
-    if (pc) {
+    if (SOLO) {
+      ps = State{sol->tail, sol->hash, sol->tok};
+      pmin = sol->pmin;
+      ptrace = sol->ptrace;
+    } else if (pc) {
       ps = State{pc->tail, pc->hash, pc->tok};
       pmin = pc->minret;
       ptrace = pc->trace;
@@ -614,19 +726,24 @@ __device__ __forceinline__ bool lv_expand(const LvParams& p, const LvRoundIn& in
 #pragma unroll
     for (int q = 0; q < NQ; ++q) {
       const uint32_t j = (uint32_t)lane + 64u * q;
-      cnt[q] = (j < K && pc) ? (uint32_t)pc->cnt[j] : 0u;
       d[q] = 0;
-      if (j < K) {
-        H[q] = lv_load_parent_head<NQ>(p.recs + s_cs[64 * q + lane] + cnt[q], PL, q, lane);
+      if (SOLO) {
+        cnt[q] = sol->cnt[j];
+        H[q] = lv_parent_hot<NQ>(PL, q, lane);
       } else {
-        H[q] = lv_hot_null();
-        PL.fl[q][lane] = OPF_SENTINEL; PL.call[q][lane] = EV_INF; PL.ret[q][lane] = EV_INF; PL.suf[q][lane] = REQ_NONE;
+        cnt[q] = (j < K && pc) ? (uint32_t)pc->cnt[j] : 0u;
+        if (j < K) {
+          H[q] = lv_load_parent_head<NQ>(p.recs + s_cs[64 * q + lane] + cnt[q], PL, q, lane);
+        } else {
+          H[q] = lv_hot_null();
+          PL.fl[q][lane] = OPF_SENTINEL; PL.call[q][lane] = EV_INF; PL.ret[q][lane] = EV_INF; PL.suf[q][lane] = REQ_NONE;
+        }
+        if (j < K) chx ^= lv_chain_term(j, cnt[q]);
       }
-      if (j < K) chx ^= lv_chain_term(j, cnt[q]);
       // candidate moves: minimal durable / indefinite appends at the chain heads
-      if (pc && !(H[q].fl & (OPF_SENTINEL | OPF_CLS_E)) && H[q].call < pmin) cand |= 1u << q;
+      if (has_parent && !(H[q].fl & (OPF_SENTINEL | OPF_CLS_E)) && H[q].call < pmin) cand |= 1u << q;
     }
-    const uint64_t parent_chx = wave_xor_u64(chx);
+    const uint64_t parent_chx = SOLO ? sol->chx : wave_xor_u64(chx);
     LV_LAP(1);
     // candidate moves in (slot, lane) order; this slice takes moves [c0, c1)
     uint32_t n_cand = 0, my_idx[NQ];
@@ -638,7 +755,7 @@ __device__ __forceinline__ bool lv_expand(const LvParams& p, const LvRoundIn& in
       n_cand += (uint32_t)__popcll(bq);
     }
     // round 0 has one pseudo-move: the initial configuration itself
-    const uint32_t n_moves = pc ? n_cand : 1u;
+    const uint32_t n_moves = has_parent ? n_cand : 1u;
     const uint32_t c0 = (uint32_t)(((uint64_t)n_moves * slice) / S);
     const uint32_t c1 = (uint32_t)(((uint64_t)n_moves * (slice + 1)) / S);
     // The outcome of every move of this slice at once (lane l, slot q: the
@@ -646,44 +763,93 @@ __device__ __forceinline__ bool lv_expand(const LvParams& p, const LvRoundIn& in
     // outcome and hash fold, for those moves in parallel, so a move in the
     // loop below costs only its next head's load. Registers: 5 per slot
     // (NQ <= 6).
+#ifdef S2LC_PROF
+    if (SOLO && threadIdx.x == 0) { const unsigned long long t_ = clock64(); sol->pt[1] += t_ - sol->pt[7]; sol->pt[7] = t_; }
+#endif
     constexpr bool PRE = NQ <= 6;
     constexpr int NP = PRE ? NQ : 1;
     uint64_t mv_tail[NP], mv_hash[NP];
-    uint32_t mv_pk[NP];  // take_opt | take_id << 1 | token << 16
+    uint32_t mv_pk[NP];  // take_opt | take_id << 1 | P1-dead opt child << 2 | token << 16
+    // P1 precheck: a child's P1 bound is the parent's with the moved chain's
+    // head replaced by its next record, so (smallest, second smallest) head
+    // bound over all chains gives every child's bound without its chain; an
+    // opt child past it dies in its closure's first pass, and is counted but
+    // not closed (most children of a hard history end this way)
+    const bool p1 = PRE && (p.hflags & H_NOWRAP);
+    uint64_t b_min = REQ_NONE, b_2nd = REQ_NONE;
+    if (p1) wave_min2_hot<NQ>(H, b_min, b_2nd);
 #pragma unroll
     for (int q = 0; q < NP; ++q) {
       mv_tail[q] = ps.tail;
       mv_hash[q] = ps.hash;
       mv_pk[q] = ps.tok << 16;
       if (PRE && ((cand >> q) & 1u) && my_idx[q] >= c0 && my_idx[q] < c1) {
-        const OpRec r = load_rec(p.recs + s_cs[64 * q + lane] + cnt[q]);  // the head: just loaded, cached
+        const OpRec* hp = p.recs + s_cs[64 * q + lane] + cnt[q];
+        // the chain's next record's P1 bound (solo rounds: in LDS)
+        const uint64_t nx_suf = SOLO ? NX->suf[q][lane] : (p1 ? ld_suf(hp + 1) : REQ_NONE);
+        // the head: solo rounds keep the heads' whole records in LDS; grid
+        // rounds just loaded its hot part (cached)
+        const OpRec r = SOLO ? FR[64 * q + lane] : load_rec(hp);
         const bool g = append_guards_ok(r, ps);
         State opt = ps;
         opt.tail = ps.tail + r.num_records;
         opt.tok = r.set_tok ? r.set_tok : ps.tok;
-        const bool to = (r.flags & OPF_CLS_D) ? (g && opt.tail == r.out_tail) : g;
-        if (to || ((r.flags & OPF_CLS_I) && g)) opt.hash = fold_hashes_blk(ps.hash, p.pool + r.hash_off, r.hash_cnt);
+        bool to = (r.flags & OPF_CLS_D) ? (g && opt.tail == r.out_tail) : g;
+        const bool p1dead = p1 && to && opt.tail > lv_min64(H[q].suf == b_min ? b_2nd : b_min, nx_suf);
+        // the fold: for a live opt child, or for an indefinite append's
+        // identity test (opt == s needs equal tails)
+        const bool fold = (to && !p1dead) || ((r.flags & OPF_CLS_I) && g && opt.tail == ps.tail);
+        if (fold) {
+          if (SOLO) {  // the first LV_SOLO_HP record hashes are in LDS
+            uint64_t h = ps.hash;
+            const uint32_t j = (uint32_t)lane + 64u * q;
+#pragma unroll
+            for (int k = 0; k < LV_SOLO_HP; ++k)
+              if ((uint32_t)k < r.hash_cnt) h = chain_hash(h, sol->hp[k][j]);
+            if (r.hash_cnt > (uint32_t)LV_SOLO_HP)
+              h = fold_hashes_blk(h, p.pool + r.hash_off + LV_SOLO_HP, r.hash_cnt - LV_SOLO_HP);
+            opt.hash = h;
+          } else {
+            opt.hash = fold_hashes_blk(ps.hash, p.pool + r.hash_off, r.hash_cnt);
+          }
+        }
         const bool ti = (r.flags & OPF_CLS_I) && (!idefer || r.ret_ev == pmin) && !(g && state_eq(opt, ps));
         mv_tail[q] = opt.tail;
         mv_hash[q] = opt.hash;
-        mv_pk[q] = (to ? 1u : 0u) | (ti ? 2u : 0u) | (opt.tok << 16);
+        mv_pk[q] = (to && !p1dead ? 1u : 0u) | (ti ? 2u : 0u) | (p1dead ? 4u : 0u) | (opt.tok << 16);
       }
     }
+    // the loop below visits only this slice's moves with a child to close;
+    // the P1-dead opt children are counted here
+    uint32_t live = cand;
+    if (PRE) {
+      live = 0;
+#pragma unroll
+      for (int q = 0; q < NP; ++q) {
+        if (mv_pk[q] & 3u) live |= 1u << q;
+        const uint32_t nd = (uint32_t)__popcll(__ballot((mv_pk[q] >> 2) & 1u));
+        kids += nd;
+        LV_ADD(9, nd);
+      }
+    }
+#ifdef S2LC_PROF
+    if (SOLO && threadIdx.x == 0) { asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); const unsigned long long t_ = clock64(); sol->pt[2] += t_ - sol->pt[7]; sol->pt[7] = t_; }
+#endif
     uint32_t ord = 0, q_cur = 0;
-    uint64_t m = pc ? __ballot(cand & 1u) : 1ull;
+    uint64_t m = has_parent ? __ballot(live & 1u) : 1ull;
     for (;;) {
       // next move (wave-uniform): slot q_cur, owner lane src
-      while (m == 0 && q_cur + 1 < (uint32_t)NQ && pc) {
+      while (m == 0 && q_cur + 1 < (uint32_t)NQ && has_parent) {
         ++q_cur;
-        m = __ballot((cand >> q_cur) & 1u);
+        m = __ballot((live >> q_cur) & 1u);
       }
-      if (m == 0 || ord >= c1) break;
+      if (m == 0 || (!PRE && ord >= c1)) break;
       const int src = __ffsll((unsigned long long)m) - 1;
       m &= m - 1;
       const uint32_t o = ord++;
-      if (o < c0) continue;
+      if (!PRE && o < c0) continue;  // (PRE: live holds this slice's moves only)
       // children of the move: on the owner lane (round 0: the unchanged initial state)
-      bool take_opt = !pc, take_id = false;
+      bool take_opt = !has_parent, take_id = false;
       State opt = ps;
       uint4 nx_obs = make_uint4(0, 0, 0, 0), nx_mid = make_uint4(0, 0, 0, 0);
       uint32_t nx_fl = 0;
@@ -691,7 +857,14 @@ __device__ __forceinline__ bool lv_expand(const LvParams& p, const LvRoundIn& in
       uint32_t fl2;
       State so;
       if (PRE) {
-        if (pc && lane == src) {
+        if (SOLO) {
+          if (lane == src) {  // loaded into LDS with the slice's moves
+            const uint64_t ot = NX->otail[q_cur][lane], oh = NX->ohash[q_cur][lane], sf = NX->suf[q_cur][lane];
+            nx_obs = make_uint4((uint32_t)ot, (uint32_t)(ot >> 32), (uint32_t)oh, (uint32_t)(oh >> 32));
+            nx_mid = make_uint4((uint32_t)sf, (uint32_t)(sf >> 32), NX->call[q_cur][lane], NX->ret[q_cur][lane]);
+            nx_fl = NX->fl[q_cur][lane];
+          }
+        } else if (has_parent && lane == src) {
           // the chain's next head (the child's first new head)
           const OpRec* nx = p.recs + s_cs[64 * q_cur + lane] + sel_cnt<NQ>(cnt, q_cur) + 1;
           nx_obs = ld16(nx, 16);
@@ -699,10 +872,10 @@ __device__ __forceinline__ bool lv_expand(const LvParams& p, const LvRoundIn& in
           nx_fl = nx->flags;
         }
         const uint32_t pk = rl(sel_u32<NP>(mv_pk, q_cur), src);
-        fl2 = pc ? (pk & 3u) : 1u;
-        so = pc ? State{rl64(sel_u64<NP>(mv_tail, q_cur), src), rl64(sel_u64<NP>(mv_hash, q_cur), src), pk >> 16} : ps;
+        fl2 = has_parent ? (pk & 3u) : 1u;
+        so = has_parent ? State{rl64(sel_u64<NP>(mv_tail, q_cur), src), rl64(sel_u64<NP>(mv_hash, q_cur), src), pk >> 16} : ps;
       } else {
-        if (pc && lane == src) {
+        if (has_parent && lane == src) {
           // the move's record, and the chain's next head (the child's first new head) with it
           const OpRec* mrec = p.recs + s_cs[64 * q_cur + lane] + sel_cnt<NQ>(cnt, q_cur);
           const OpRec* nx = mrec + 1;
@@ -718,7 +891,7 @@ __device__ __forceinline__ bool lv_expand(const LvParams& p, const LvRoundIn& in
           if (take_opt || ((r.flags & OPF_CLS_I) && g)) opt.hash = fold_hashes_blk(ps.hash, p.pool + r.hash_off, r.hash_cnt);
           if (r.flags & OPF_CLS_I) take_id = (!idefer || r.ret_ev == pmin) && !(g && state_eq(opt, ps));
         }
-        fl2 = pc ? rl((take_opt ? 1u : 0u) | (take_id ? 2u : 0u), src) : 1u;
+        fl2 = has_parent ? rl((take_opt ? 1u : 0u) | (take_id ? 2u : 0u), src) : 1u;
         so = State{rl64(opt.tail, src), rl64(opt.hash, src), rl(opt.tok, src)};
       }
       const uint32_t j = (uint32_t)src + 64u * q_cur;
@@ -727,8 +900,9 @@ __device__ __forceinline__ bool lv_expand(const LvParams& p, const LvRoundIn& in
       for (int w = 0; w < 2; ++w) {
         if (!((fl2 >> w) & 1u)) continue;
         const State cs_ = w == 0 ? so : ps;
-        const uint32_t mv = !pc ? LV_NONE : (w == 0 ? j : (j | MOVE_IDENT));
-        if (pc) {
+        const uint32_t mv = !has_parent ? LV_NONE : (w == 0 ? j : (j | MOVE_IDENT));
+        if (SOLO) LV_ADD(8, 1);
+        if (has_parent) {
           kids++;
 #pragma unroll
           for (int q = 0; q < NQ; ++q)
@@ -745,10 +919,28 @@ __device__ __forceinline__ bool lv_expand(const LvParams& p, const LvRoundIn& in
         uint32_t mr = 0;
         LV_LAP(4);
         LV_ADD(6, 1);
-        const int cr = lv_closure<NQ>(H, d, cnt, s_cs, PL, lane, cs_, p.hflags, pmin, p.recs, mr);
+#ifdef S2LC_PROF
+        const unsigned long long tc0_ = clock64();
+#endif
+        const int cr = lv_closure<NQ>(H, d, cnt, s_cs, PL, lane, cs_, p.hflags, pmin, p.recs, mr, SOLO ? NX : nullptr);
+#ifdef S2LC_PROF
+        if (SOLO && lane == 0) {  // closure cycles: [8] ALIVE, [9] others; [10] ALIVE count; [11] stage cycles
+          asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+          const unsigned long long dt_ = clock64() - tc0_;
+          atomicAdd(&sol->pc[cr == CL_ALIVE ? 0 : 1], dt_);
+          if (cr == CL_ALIVE) atomicAdd(&sol->pc[2], 1ull);
+        }
+        const unsigned long long ts0_ = clock64();
+#endif
         LV_LAP(3);
         if (cr == CL_COMPLETE || cr == CL_P4) {
-          if (lane == 0 && atomicCAS(&p.ctl->found, 0u, 1u) == 0u) {
+          if (SOLO) {
+            if (lane == 0 && atomicCAS(&sol->found, 0u, 1u) == 0u) {
+              sol->fpar = ptrace;
+              sol->fmov = mv;
+              sol->fp4 = cr == CL_P4 ? 1u : 0u;
+            }
+          } else if (lane == 0 && atomicCAS(&p.ctl->found, 0u, 1u) == 0u) {
             atomicExch(&p.ctl->found_parent, ptrace);
             atomicExch(&p.ctl->found_move, mv);
             atomicExch(&p.ctl->found_p4, cr == CL_P4 ? 1u : 0u);
@@ -760,11 +952,35 @@ __device__ __forceinline__ bool lv_expand(const LvParams& p, const LvRoundIn& in
             const uint32_t jj = (uint32_t)lane + 64u * q;
             if (d[q]) dx ^= lv_chain_term(jj, cnt[q]) ^ lv_chain_term(jj, cnt[q] + d[q]);
           }
-          const uint64_t fp = mix64(parent_chx ^ wave_xor_u64(dx) ^ lv_state_term(cs_.tail, cs_.hash, cs_.tok));
-          if (FUSED)
+          const uint64_t cdx = parent_chx ^ wave_xor_u64(dx);
+          const uint64_t fp = mix64(cdx ^ lv_state_term(cs_.tail, cs_.hash, cs_.tok));
+          if (SOLO) {
+            // distinct children: staging slot = arrival order; the first one is
+            // kept in LDS in case it turns out to be the round's only survivor
+            uint32_t k = 0;
+            if (lane == 0) k = atomicAdd(&sol->alive, 1u);
+            k = rl(k, 0);
+            if (k < p.scs) {
+              lv_solo_put<NQ>(p, k, cs_, fp, mr, ptrace, mv, in.tbase, in.wit, cnt, d);
+            } else if (lane == 0) {
+              sol->ovf = 1u;
+            }
+#ifdef S2LC_PROF
+            if (lane == 0) atomicAdd(&sol->pc[3], clock64() - ts0_);
+#endif
+            if (k == 0) {
+#pragma unroll
+              for (int q = 0; q < NQ; ++q) sol->keep[lane + 64 * q] = (uint16_t)d[q];
+              if (lane == 0) {
+                sol->ktail = cs_.tail; sol->khash = cs_.hash; sol->ktok = cs_.tok;
+                sol->kchx = cdx; sol->kmr = mr;
+              }
+            }
+          } else if (FUSED) {
             lv_stage_insert<NQ>(p, in, stripe, rk, rleft, cs_, fp, mr, ptrace, mv, cnt, d);
-          else
+          } else {
             lv_stage<NQ>(p, stripe, rk, rleft, cs_, fp, mr, ptrace, mv, cnt, d);
+          }
         }
         // back to the parent's heads on the chains this child advanced
 #pragma unroll
@@ -777,11 +993,17 @@ __device__ __forceinline__ bool lv_expand(const LvParams& p, const LvRoundIn& in
     }
   }
 #ifdef S2LC_PROF
-  if (lane == 0 && p.prof && lv_acc[5])  // only waves that had work (idle waves would swamp the counters)
-    for (int i_ = 0; i_ < 9; ++i_) atomicAdd(&p.prof[i_ < 7 ? i_ : i_ + 5], lv_acc[i_]);
+  if (lane == 0 && p.prof && lv_acc[5]) {  // only waves that had work (idle waves would swamp the counters)
+    if (SOLO) {  // [14] closures run, [15] opt children dropped by the P1 precheck
+      atomicAdd(&p.prof[14], lv_acc[8]);
+      atomicAdd(&p.prof[15], lv_acc[9]);
+    } else {
+      for (int i_ = 0; i_ < 9; ++i_) atomicAdd(&p.prof[i_ < 7 ? i_ : i_ + 5], lv_acc[i_]);
+    }
+  }
 #endif
-  if (!FUSED && rleft) lv_release<NQ>(p, stripe, rk, rleft);
-  if (lane == 0 && kids) atomicAdd(&p.ctl->children, kids);
+  if (MODE == 0 && rleft) lv_release<NQ>(p, stripe, rk, rleft);
+  if (lane == 0 && kids) atomicAdd(SOLO ? &sol->kids : &p.ctl->children, kids);
   return wave_id < items;
 }
 
@@ -804,7 +1026,7 @@ __global__ __launch_bounds__(LV_BLOCK) void lv_round(LvParams p) {
   in.S = p.init ? 1u : lv_slices(p.K, in.nf, nwaves, p.run ? p.run->last_nf : 0u, p.run ? p.run->last_children : 0ull);
   in.tbase = 0;
   in.wit = 0;
-  lv_expand<NQ, false>(p, in, s_heads[threadIdx.x >> 6], s_cs);
+  lv_expand<NQ, 0>(p, in, s_heads[threadIdx.x >> 6], s_cs);
 }
 
 template <int NQ>
@@ -1012,6 +1234,7 @@ struct LvPersist {
   unsigned long long* ht[2];  // round r inserts into ht[r & 1]
   uint32_t max_rounds;        // rounds per launch
   uint32_t nf_max;            // leave when the frontier is wider
+  uint32_t solo;              // one-configuration frontiers run as solo rounds (workgroup 0)
   unsigned long long spin_ticks;  // barrier wait limit (wall-clock ticks)
 };
 
@@ -1049,11 +1272,175 @@ __device__ __forceinline__ bool lv_grid_sync(LvBar* B, uint32_t e, unsigned long
   return s_ok != 0;
 }
 
+// A solo configuration's head on chain j at record h (chain end: `end`, its
+// sentinel's index + 1): its whole record into FR[j] (the move's record, read
+// by the expansion), its closure fields into PL, the record after it into NX
+// (a child's first new head on this chain) with its record-hash range, and
+// the head's first LV_SOLO_HP record hashes into S.hp. `known`: the head's
+// hash range is already known (it was the previous head's next record), so
+// the hash loads go out with the record loads instead of after them.
+template <int NQ>
+__device__ __forceinline__ void lv_solo_head(const LvParams& p, const OpRec* h, const OpRec* end, uint32_t j,
+                                             bool known, LvHeadsLds<NQ>& PL, LvHeadsLds<NQ>& NX, OpRec* FR,
+                                             LvSolo<NQ>& S) {
+  const uint4* a = reinterpret_cast<const uint4*>(h);
+  const uint4* b = reinterpret_cast<const uint4*>(h + 1 < end ? h + 1 : h);  // (the sentinel has no next record)
+  const uint4 x0 = a[0], x1 = a[1], x2 = a[2], x3 = a[3];
+  const uint4 y1 = b[1], y2 = b[2], y3 = b[3];
+  uint64_t hv[LV_SOLO_HP];
+  if (known) {
+    const uint32_t ho = S.nx_hoff[j], hc = S.nx_hcnt[j];
+#pragma unroll
+    for (int k = 0; k < LV_SOLO_HP; ++k) hv[k] = (uint32_t)k < hc ? p.pool[ho + k] : 0ull;
+  } else {
+#pragma unroll
+    for (int k = 0; k < LV_SOLO_HP; ++k) hv[k] = (uint32_t)k < x3.y ? p.pool[x3.x + k] : 0ull;
+  }
+  uint4* f = reinterpret_cast<uint4*>(FR + j);
+  f[0] = x0; f[1] = x1; f[2] = x2; f[3] = x3;
+  const int q = (int)(j >> 6), l = (int)(j & 63);
+  PL.otail[q][l] = (uint64_t)x1.x | ((uint64_t)x1.y << 32);
+  PL.ohash[q][l] = (uint64_t)x1.z | ((uint64_t)x1.w << 32);
+  PL.suf[q][l] = (uint64_t)x2.x | ((uint64_t)x2.y << 32);
+  PL.call[q][l] = x2.z;
+  PL.ret[q][l] = x2.w;
+  PL.fl[q][l] = x3.w;
+  NX.otail[q][l] = (uint64_t)y1.x | ((uint64_t)y1.y << 32);
+  NX.ohash[q][l] = (uint64_t)y1.z | ((uint64_t)y1.w << 32);
+  NX.suf[q][l] = (uint64_t)y2.x | ((uint64_t)y2.y << 32);
+  NX.call[q][l] = y2.z;
+  NX.ret[q][l] = y2.w;
+  NX.fl[q][l] = y3.w;
+  S.nx_hoff[j] = y3.x;
+  S.nx_hcnt[j] = y3.y;
+#pragma unroll
+  for (int k = 0; k < LV_SOLO_HP; ++k) S.hp[k][j] = hv[k];
+}
+
+// Solo rounds (LvSolo), run by workgroup 0 of lv_persist while the others
+// wait at the grid barrier: enter from the frontier's one configuration, go on
+// while every round keeps exactly one, and stop when a round keeps none or
+// several, completes, overflows, or after max_rounds. R is the workgroup's run
+// state; every round is closed on it exactly as a grid round is.
+template <int NQ>
+__device__ void lv_solo_rounds(const LvParams& p, const LvPersist& q, LvRun& R, LvHeadsLds<NQ>& PL,
+                               LvHeadsLds<NQ>* NX, OpRec* FR, const uint32_t* s_cs, LvSolo<NQ>& S,
+                               uint32_t max_rounds) {
+  const uint32_t K = p.K;
+  // end of chain j's records (its sentinel's index + 1)
+  auto chain_end = [&](uint32_t j) { return p.recs + (j + 1 < K ? s_cs[j + 1] : S.cs_end); };
+  if (threadIdx.x == 0) S.cs_end = p.cs[K];
+  lv_sync_lds();
+  {  // the configuration: counts, heads (all four waves share them), state, chain terms
+    const uint32_t r = R.round + 1;
+    const LCfg<NQ>* pc = lv_cfg<NQ>(q.stg[(r + 1) & 1], q.idx[(r + 1) & 1][0]);
+    uint64_t chx = 0;
+    for (uint32_t j = threadIdx.x; j < 64u * NQ; j += LV_BLOCK) {
+      const int qq = (int)(j >> 6), l = (int)(j & 63);
+      const uint32_t c = j < K ? (uint32_t)pc->cnt[j] : 0u;
+      S.cnt[j] = (uint16_t)c;
+      S.keep[j] = 0;
+      if (j < K) {
+        lv_solo_head<NQ>(p, p.recs + s_cs[j] + c, chain_end(j), j, false, PL, *NX, FR, S);
+        chx ^= lv_chain_term(j, c);
+      } else {
+        PL.fl[qq][l] = OPF_SENTINEL; PL.call[qq][l] = EV_INF; PL.ret[qq][l] = EV_INF; PL.suf[qq][l] = REQ_NONE;
+        NX->fl[qq][l] = OPF_SENTINEL; NX->call[qq][l] = EV_INF; NX->ret[qq][l] = EV_INF; NX->suf[qq][l] = REQ_NONE;
+      }
+    }
+    chx = wave_xor_u64(chx);
+    if ((threadIdx.x & 63) == 0) S.wx[threadIdx.x >> 6] = chx;
+    if (threadIdx.x == 0) {
+      S.tail = pc->tail; S.hash = pc->hash; S.tok = pc->tok;
+      S.pmin = pc->minret; S.ptrace = pc->trace;
+      if (pc->slot <= p.ht_mask) st_wt64(&q.ht[(r + 1) & 1][pc->slot], HT_EMPTY);
+    }
+    lv_sync_lds();
+    if (threadIdx.x == 0) {
+      uint64_t x = 0;
+      for (int w = 0; w < LV_BLOCK / 64; ++w) x ^= S.wx[w];
+      S.chx = x;
+    }
+  }
+#ifdef S2LC_PROF
+  const unsigned long long t_solo = wall_clock64();
+  uint32_t n_solo = 0;
+#endif
+#ifdef S2LC_PROF
+  if (threadIdx.x == 0) { for (int i_ = 0; i_ < 8; ++i_) S.pt[i_] = 0; for (int i_ = 0; i_ < 4; ++i_) S.pc[i_] = 0; S.pt[7] = clock64(); }
+#define LV_SOLO_T(i) do { if (threadIdx.x == 0) { const unsigned long long t_ = clock64(); S.pt[i] += t_ - S.pt[7]; S.pt[7] = t_; } } while (0)
+#else
+#define LV_SOLO_T(i) do { } while (0)
+#endif
+  for (uint32_t n = 0; n < max_rounds; ++n) {
+    const uint32_t r = R.round + 1;
+#ifdef S2LC_PROF
+    ++n_solo;
+#endif
+    if (threadIdx.x == 0) {
+      S.alive = 0; S.found = 0; S.ovf = 0; S.kids = 0;
+      S.tbase = (uint32_t)R.tnext; S.wit = R.witness;
+    }
+    lv_sync_lds();
+    LvParams rp = p;
+    rp.round = r;
+    rp.stg = q.stg[r & 1];
+    rp.nxt_idx = q.idx[r & 1];
+    LvRoundIn in;
+    in.f0 = 0; in.nf = 1; in.S = LV_BLOCK / 64; in.tbase = S.tbase; in.wit = S.wit;
+    LV_SOLO_T(0);
+    (void)lv_expand<NQ, 2>(rp, in, PL, s_cs, &S, NX, FR);
+    LV_SOLO_T(3);
+    lv_sync_lds();
+    if (threadIdx.x == 0) {
+      LvCounts k;
+      k.nn = S.alive; k.ovf = S.ovf; k.fnd = S.found;
+      k.fpar = S.fpar; k.fmov = S.fmov; k.fp4 = S.fp4; k.ch = S.kids;
+      lv_close_state(R, k, r, p.rcounts, p.scap, p.trace_cap);
+      R.solo_rounds++;
+    }
+    lv_sync_lds();
+    LV_SOLO_T(4);
+    if (R.done != LVR_RUNNING || R.nf != 1) break;
+    // the only survivor (staging slot 0) is the next round's configuration:
+    // reload the heads of the chains it advanced
+    for (uint32_t j = threadIdx.x; j < 64u * NQ; j += LV_BLOCK) {
+      const uint32_t dj = S.keep[j];
+      if (dj) {
+        const uint32_t c = S.cnt[j] + dj;
+        S.cnt[j] = (uint16_t)c;
+        lv_solo_head<NQ>(p, p.recs + s_cs[j] + c, chain_end(j), j, dj == 1, PL, *NX, FR, S);
+      }
+    }
+    if (threadIdx.x == 0) {
+      S.tail = S.ktail; S.hash = S.khash; S.tok = S.ktok; S.chx = S.kchx; S.pmin = S.kmr;
+      S.ptrace = S.wit ? p.tgid + S.tbase : TRACE_NONE;
+    }
+#ifdef S2LC_PROF
+    lv_sync_lds();
+#endif
+    LV_SOLO_T(5);
+  }
+#ifdef S2LC_PROF
+  if (threadIdx.x == 0 && p.prof) {  // [7] solo rounds, [8] their wall-clock ticks, [16..21] phase cycles
+    atomicAdd(&p.prof[7], (unsigned long long)n_solo);
+    atomicAdd(&p.prof[8], wall_clock64() - t_solo);
+    for (int i_ = 0; i_ < 6; ++i_) atomicAdd(&p.prof[16 + i_], S.pt[i_]);
+    for (int i_ = 0; i_ < 4; ++i_) atomicAdd(&p.prof[22 + i_], S.pc[i_]);
+  }
+#endif
+#undef LV_SOLO_T
+}
+
 template <int NQ>
 __global__ __launch_bounds__(LV_BLOCK) void lv_persist(LvParams p, LvPersist q) {
-  __shared__ LvHeadsLds<NQ> s_heads[LV_BLOCK / 64];
+  // solo rounds use s_heads[0] (the configuration's heads), s_heads[1] (the
+  // moves' next heads) and s_heads[2..3] as the heads' whole records
+  __shared__ __attribute__((aligned(16))) LvHeadsLds<NQ> s_heads[LV_BLOCK / 64];
+  static_assert(2 * sizeof(LvHeadsLds<NQ>) >= 64 * NQ * sizeof(OpRec), "solo head records fit in s_heads[2..3]");
   __shared__ uint32_t s_cs[64 * NQ];
   __shared__ LvRun s_run;
+  __shared__ LvSolo<(NQ <= 5 ? NQ : 1)> s_solo;  // (solo rounds only for NQ <= 5)
   for (uint32_t x = threadIdx.x; x < 64u * NQ; x += LV_BLOCK) s_cs[x] = x < p.K ? p.cs[x] : 0u;
   if (threadIdx.x == 0) s_run = *p.run;  // written by an earlier launch
   __syncthreads();
@@ -1063,7 +1450,31 @@ __global__ __launch_bounds__(LV_BLOCK) void lv_persist(LvParams p, LvPersist q) 
 #ifdef S2LC_PROF
   unsigned long long t_round = wall_clock64();
 #endif
-  for (uint32_t it = 0; ok; ++it) {
+  uint32_t it = 0, ep = 0;  // rounds run by this launch, barrier epochs
+  while (ok) {
+    const uint32_t r_before = s_run.round;
+    // solo rounds for NQ <= 5 (K <= 320): wider layouts would lose the second
+    // resident workgroup per CU the grid barrier relies on (VGPRs)
+    if (NQ <= 5 && q.solo && s_run.nf == 1) {
+      if (blockIdx.x == 0) {
+        if constexpr (NQ <= 5) lv_solo_rounds<NQ>(p, q, s_run, s_heads[0], &s_heads[1],
+                                                   reinterpret_cast<OpRec*>(&s_heads[2]), s_cs, s_solo, max(1u, q.max_rounds - it));
+        // the next grid round's counters start at zero; the other workgroups
+        // take the run state from here after the barrier
+        uint32_t* z = reinterpret_cast<uint32_t*>(q.ctl3 + ((s_run.round + 1) % 3));
+        for (uint32_t i = threadIdx.x; i < sizeof(LvCtl) / 4; i += LV_BLOCK) st_wt32(z + i, 0u);
+        if (threadIdx.x < sizeof(LvRun) / 4)
+          st_wt32(reinterpret_cast<uint32_t*>(p.run) + threadIdx.x, reinterpret_cast<const uint32_t*>(&s_run)[threadIdx.x]);
+      }
+      ok = lv_grid_sync(q.bar, ++ep, q.spin_ticks);
+      if (ok && blockIdx.x != 0 && threadIdx.x < sizeof(LvRun) / 4)
+        reinterpret_cast<uint32_t*>(&s_run)[threadIdx.x] = ld_agent(reinterpret_cast<const uint32_t*>(p.run) + threadIdx.x);
+      if (!ok && threadIdx.x == 0) s_run.done = LVR_ABORT;
+      __syncthreads();
+      it += max(1u, s_run.round - r_before);
+      if (s_run.done != LVR_RUNNING || it >= q.max_rounds || s_run.nf > q.nf_max) break;
+      continue;
+    }
     const uint32_t r = s_run.round + 1;  // the round this iteration expands
     LvParams rp = p;
     rp.round = r;
@@ -1083,13 +1494,13 @@ __global__ __launch_bounds__(LV_BLOCK) void lv_persist(LvParams p, LvPersist q) 
     in.S = lv_slices(p.K, in.nf, nwaves, s_run.last_nf, s_run.last_children);
     in.tbase = (uint32_t)s_run.tnext;
     in.wit = s_run.witness;
-    const bool worked = lv_expand<NQ, true>(rp, in, s_heads[threadIdx.x >> 6], s_cs);
+    const bool worked = lv_expand<NQ, 1>(rp, in, s_heads[threadIdx.x >> 6], s_cs);
 #ifdef S2LC_PROF
     if (worked && (threadIdx.x & 63) == 0 && p.prof) atomicMax(&rp.ctl->prof_end, wall_clock64());
 #else
     (void)worked;
 #endif
-    ok = lv_grid_sync(q.bar, it + 1, q.spin_ticks);
+    ok = lv_grid_sync(q.bar, ++ep, q.spin_ticks);
 #ifdef S2LC_PROF
     if (blockIdx.x == 0 && threadIdx.x == 0 && p.prof) {
       // [9] round time, [10] expansion critical path, [11] rounds (wall-clock ticks)
@@ -1109,7 +1520,8 @@ __global__ __launch_bounds__(LV_BLOCK) void lv_persist(LvParams p, LvPersist q) 
       }
     }
     __syncthreads();
-    if (s_run.done != LVR_RUNNING || it + 1 >= q.max_rounds || s_run.nf > q.nf_max) break;
+    ++it;
+    if (s_run.done != LVR_RUNNING || it >= q.max_rounds || s_run.nf > q.nf_max) break;
   }
   if (blockIdx.x == 0 && threadIdx.x == 0) {
     if (ld_agent(&q.bar->abort[0])) s_run.done = LVR_ABORT;  // some block left early: nothing here is valid
@@ -1126,7 +1538,7 @@ __global__ __attribute__((unused)) void lv_run_init(LvRun* R, unsigned long long
   R->configs = 0; R->children = 0; R->tnext = tnext; R->max_configs = max_configs;
   R->found_parent = TRACE_NONE; R->found_move = LV_NONE; R->found_p4 = 0;
   R->witness = witness; R->deep_trace = TRACE_NONE; R->deep_len = 0; R->last_tbase = TRACE_NONE;
-  R->last_nf = 0; R->last_children = 0;
+  R->last_nf = 0; R->last_children = 0; R->solo_rounds = 0;
 }
 
 // ---- distributed: owner of a configuration ---------------------------------

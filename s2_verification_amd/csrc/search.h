@@ -83,6 +83,7 @@ struct LevelStats {
   uint32_t max_frontier = 0, histories = 0, chunk_retries = 0;
   uint32_t syncs = 0;  // host synchronizations (one per batch of device-driven rounds)
   uint64_t persist_rounds = 0, persist_launches = 0;  // rounds run inside lv_persist
+  uint64_t solo_rounds = 0;  // of those, one-configuration rounds run by one workgroup
 };
 
 // A batch of histories resident on one device. Every buffer is grown on

@@ -178,10 +178,12 @@ def test_round_counts_match_reduced_search(engine, abl):
                                                              if x != y][:5])
 
 
-# level-search round modes: narrow rounds inside the persistent kernel
-# (default), host-enqueued lv_round / lv_insert only, or every round inside
-# the persistent kernel (fused stage-and-insert also on wide frontiers)
-LEVEL_MODES = {"default": {}, "no_persist": {"S2LC_NO_PERSIST": "1"}, "all_persist": {"S2LC_PERSIST_NF": "4294967295"}}
+# level-search round modes: narrow rounds inside the persistent kernel, with
+# one-configuration rounds as solo rounds of workgroup 0 (default) or on the
+# grid (no_solo), host-enqueued lv_round / lv_insert only, or every round
+# inside the persistent kernel (fused stage-and-insert also on wide frontiers)
+LEVEL_MODES = {"default": {}, "no_solo": {"S2LC_NO_SOLO": "1"}, "no_persist": {"S2LC_NO_PERSIST": "1"},
+               "all_persist": {"S2LC_PERSIST_NF": "4294967295"}}
 
 
 def _set_mode(monkeypatch, mode):
@@ -217,9 +219,13 @@ def test_hard_round_counts(name, off, mode, monkeypatch):
         assert st["level_persist_rounds"] > 0, st
     if mode == "all_persist":
         assert st["level_persist_rounds"] == r.rounds, st
+    if mode in ("no_solo", "no_persist"):
+        assert st["level_solo_rounds"] == 0, st
+    else:  # most rounds of these histories keep one configuration
+        assert st["level_solo_rounds"] > r.rounds // 2, st
 
 
-@pytest.mark.parametrize("mode", ["default", "all_persist"])
+@pytest.mark.parametrize("mode", ["default", "no_solo", "all_persist"])
 @pytest.mark.parametrize("abl", ["all_on", "no_p2", "no_idefer"])
 def test_level_persist_round_counts_match_reduced_search(mode, abl, monkeypatch):
     """The persistent rounds against oracle/reduced.c, round by round, on the
