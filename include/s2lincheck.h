@@ -370,12 +370,19 @@ int s2lc_dist_info(const s2lc_dist* d, s2lc_dist_info_t* out);
  * when the frontier is wide and back when it is narrow again.
  *   s2lc_dist_local_round   one replicated round (round 0 included);
  *                           n_next = frontier size, found = a child completed
+ *   s2lc_dist_local_run     replicated rounds inside one resident kernel (the
+ *                           single-GPU engine's persistent and solo rounds)
+ *                           until the frontier reaches `wide` or the search
+ *                           ends; rounds = rounds run; S2LC_EUNSUPPORTED when
+ *                           not available (before round 0, or a layout without
+ *                           the persistent kernel): use s2lc_dist_local_round
  *   s2lc_dist_keep_owned    replicated -> partitioned: keep the owned configurations
  *   s2lc_dist_frontier_pack partitioned -> replicated: this rank's frontier,
  *                           frontier * config_bytes bytes, into a device buffer
  *   s2lc_dist_frontier_load the all-gathered frontier (device buffer kept alive
  *                           by the caller) becomes every rank's frontier */
 int s2lc_dist_local_round(s2lc_dist* d, uint64_t* n_next, int32_t* found);
+int s2lc_dist_local_run(s2lc_dist* d, uint32_t wide, uint64_t* n_next, int32_t* found, uint32_t* rounds);
 int s2lc_dist_keep_owned(s2lc_dist* d, uint64_t* n_kept);
 int s2lc_dist_frontier_pack(s2lc_dist* d, void* buf);
 int s2lc_dist_frontier_load(s2lc_dist* d, void* buf, uint64_t n);

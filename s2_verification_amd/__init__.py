@@ -196,6 +196,8 @@ SIGNATURES = [
     ("s2lc_dist_info", ctypes.c_int, [_P, ctypes.POINTER(c_dist_info)]),
     ("s2lc_dist_trace", ctypes.c_int, [_P, _P, ctypes.c_uint64, ctypes.POINTER(ctypes.c_uint64)]),
     ("s2lc_dist_local_round", ctypes.c_int, [_P, ctypes.POINTER(ctypes.c_uint64), ctypes.POINTER(ctypes.c_int32)]),
+    ("s2lc_dist_local_run", ctypes.c_int, [_P, ctypes.c_uint32, ctypes.POINTER(ctypes.c_uint64),
+                                           ctypes.POINTER(ctypes.c_int32), ctypes.POINTER(ctypes.c_uint32)]),
     ("s2lc_dist_keep_owned", ctypes.c_int, [_P, ctypes.POINTER(ctypes.c_uint64)]),
     ("s2lc_dist_frontier_pack", ctypes.c_int, [_P, _P]),
     ("s2lc_dist_frontier_load", ctypes.c_int, [_P, _P, ctypes.c_uint64]),

@@ -848,6 +848,14 @@ int s2lc_dist_local_round(s2lc_dist* x, uint64_t* n_next, int32_t* found) {
   return rc;
 }
 
+int s2lc_dist_local_run(s2lc_dist* x, uint32_t wide, uint64_t* n_next, int32_t* found, uint32_t* rounds) {
+  if (!x || !n_next || !found || !rounds) return S2LC_EINVAL;
+  int f = 0;
+  const int rc = dist_local_run(x->d, wide, n_next, &f, rounds, x->ctx->err);
+  *found = f;
+  return rc;
+}
+
 int s2lc_dist_keep_owned(s2lc_dist* x, uint64_t* n_kept) {
   if (!x || !n_kept) return S2LC_EINVAL;
   return dist_keep_owned(x->d, n_kept, x->ctx->err);

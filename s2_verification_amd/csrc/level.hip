@@ -671,6 +671,96 @@ int dist_local_round(DistLevel& d, uint64_t* n_next, int* found, std::string& er
   return 0;
 }
 
+// Replicated rounds inside lv_persist (solo rounds included), on the
+// single-GPU engine's conventions: the frontier is copied into the staging
+// array of round R0 + 1's parity, the run state starts at round R0 with this
+// rank's trace pool, and the launches run until the frontier reaches `wide`
+// configurations or the search ends. Every rank runs the same rounds on the
+// same configurations, so every rank reaches the same state. Returns
+// S2LC_EUNSUPPORTED when the persistent kernel is not available for this
+// layout (the caller runs host-driven replicated rounds instead).
+int dist_local_run(DistLevel& d, uint32_t wide, uint64_t* n_next, int* found, uint32_t* rounds, std::string& err) {
+  LevelBufs& L = d.b.lv;
+  *rounds = 0;
+  *found = 0;
+  if (!L.grid_persist || d.round == 0 || wide < 2) { err = "persistent replicated rounds unavailable"; return S2LC_EUNSUPPORTED; }
+  hipStream_t st = d.stream;
+  const size_t ht_bytes = ((size_t)L.ht_mask + 1) * 8;
+  // the frontier, contiguous, into the staging array it does not live in
+  const int x = d.cur == L.stg[0] ? 1 : 0;
+  const uint32_t R0 = 3u - (uint32_t)x;  // (R0 + 1) & 1 == x
+  LvParams p = dist_params(d);
+  p.f1 = d.nf;
+  p.send = L.stg[x];
+  if (d.nf) {
+    const uint64_t pieces = (uint64_t)d.nf * (d.cb / 16);
+    LVCHK(lv_dispatch(d.nq, LK_GATHER, (uint32_t)std::min<uint64_t>(2048, (pieces + LV_BLOCK - 1) / LV_BLOCK), p, st));
+    hipLaunchKernelGGL(lv_iota, dim3((uint32_t)std::min<uint64_t>(1024, (d.nf + 255) / 256)), dim3(256), 0, st, L.idx[x], d.nf);
+    LVCHK(hipGetLastError());
+  }
+  for (int i = 0; i < 2; ++i) LVCHK(hipMemsetAsync(L.ht[i], 0xFF, ht_bytes, st));
+  LvRun* hr = reinterpret_cast<LvRun*>(L.h_run);
+  LvRun* d_pub = nullptr;
+  LVCHK(hipHostGetDevicePointer((void**)&d_pub, hr, 0));
+  LvRun r0;
+  memset(&r0, 0, sizeof r0);
+  r0.done = LVR_RUNNING; r0.round = R0; r0.nf = d.nf; r0.max_frontier = (uint32_t)d.max_frontier;
+  r0.tnext = d.tnext; r0.witness = d.tnext + L.scap <= d.trace_cap ? 1u : 0u;
+  r0.found_parent = TRACE_NONE; r0.found_move = LV_NONE; r0.deep_trace = TRACE_NONE; r0.last_tbase = TRACE_NONE;
+  LVCHK(hipMemcpyAsync(L.run, &r0, sizeof r0, hipMemcpyHostToDevice, st));
+  p.run = reinterpret_cast<LvRun*>(L.run); p.publish = d_pub; p.close_round = 1; p.publish_always = 1;
+  p.rcounts = nullptr; p.init = 0;
+  LvPersist pq;
+  memset(&pq, 0, sizeof pq);
+  pq.ctl3 = reinterpret_cast<LvCtl*>(L.ctl); pq.bar = reinterpret_cast<LvBar*>(L.bar);
+  for (int i = 0; i < 2; ++i) { pq.stg[i] = L.stg[i]; pq.idx[i] = L.idx[i]; pq.ht[i] = L.ht[i]; }
+  pq.max_rounds = 4096;
+  pq.nf_max = wide - 1;
+  pq.solo = getenv("S2LC_NO_SOLO") ? 0u : 1u;
+  {
+    int dev = 0, khz = 100000;
+    LVCHK(hipGetDevice(&dev));
+    (void)hipDeviceGetAttribute(&khz, hipDeviceAttributeWallClockRate, dev);
+    pq.spin_ticks = (unsigned long long)khz * 2000ull;
+  }
+  LVCHK(hipEventRecord(L.ev[0], st));
+  memset(hr, 0, sizeof(LvRun));
+  for (;;) {
+    LVCHK(hipMemsetAsync(L.bar, 0, sizeof(LvBar), st));
+    LVCHK(hipMemsetAsync(L.ctl, 0, 3 * sizeof(LvCtl), st));
+    LVCHK(lv_persist_launch(d.nq, L.grid_persist, p, pq, st));
+    LVCHK(hipStreamSynchronize(st));
+    if (hr->done != LVR_RUNNING || hr->nf >= wide) break;
+  }
+  LVCHK(hipEventRecord(L.ev[1], st));
+  LVCHK(hipMemsetAsync(L.ht[0], 0xFF, ht_bytes, st));  // the dist rounds insert into ht[0]: no stale entries
+  LVCHK(hipStreamSynchronize(st));
+  float ms = 0;
+  LVCHK(hipEventElapsedTime(&ms, L.ev[0], L.ev[1]));
+  d.ms += ms;
+  const LvRun fin = *hr;
+  if (fin.done == LVR_ABORT) { err = "replicated rounds: a persistent-round barrier timed out"; return S2LC_EHIP; }
+  if (fin.done == LVR_OVERFLOW) { err = "replicated round exceeds the device buffers"; return S2LC_ENOMEM; }
+  d.children += fin.children;
+  d.configs += fin.configs;
+  d.max_frontier = std::max<uint64_t>(d.max_frontier, fin.max_frontier);
+  *rounds = fin.round - R0;
+  d.round += *rounds;
+  d.tnext = fin.tnext;  // (trace entries written by these rounds: the witness walk reads them)
+  if (fin.done == LVR_FOUND) {
+    d.found_parent = fin.found_parent; d.found_move = fin.found_move; d.found_p4 = fin.found_p4;
+    *found = 1;
+    *n_next = 0;
+    return 0;
+  }
+  if (fin.done == LVR_EMPTY) { d.nf = 0; *n_next = 0; return 0; }
+  d.cur_sel = (int)((fin.round + 1) & 1);
+  d.cur = L.stg[d.cur_sel];
+  d.nf = fin.nf;
+  *n_next = fin.nf;
+  return 0;
+}
+
 // replicated -> partitioned: keep only the frontier configurations this rank owns
 int dist_keep_owned(DistLevel& d, uint64_t* n_kept, std::string& err) {
   LevelBufs& L = d.b.lv;

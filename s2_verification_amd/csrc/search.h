@@ -206,6 +206,7 @@ int dist_pack(DistLevel& d, uint8_t* send, const uint64_t* counts, std::string& 
 int dist_insert(DistLevel& d, uint8_t* recv, uint64_t n_recv, uint64_t* n_next, std::string& err);
 int dist_trace(DistLevel& d, uint32_t* out, uint64_t cap, uint64_t* n, std::string& err);
 int dist_local_round(DistLevel& d, uint64_t* n_next, int* found, std::string& err);
+int dist_local_run(DistLevel& d, uint32_t wide, uint64_t* n_next, int* found, uint32_t* rounds, std::string& err);
 int dist_keep_owned(DistLevel& d, uint64_t* n_kept, std::string& err);
 int dist_frontier_pack(DistLevel& d, uint8_t* buf, std::string& err);
 int dist_frontier_load(DistLevel& d, uint8_t* buf, uint64_t n, std::string& err);

@@ -100,6 +100,22 @@ class DistSearch:
         self._chk(lib().s2lc_dist_local_round(self._d, ctypes.byref(nn), ctypes.byref(found)), "dist_local_round")
         return nn.value, bool(found.value)
 
+    def local_run(self, wide: int):
+        """Replicated rounds inside the persistent kernel until the frontier
+        reaches `wide` or the search ends: (frontier, found, rounds run,
+        configurations inserted), or None where the kernel is unavailable
+        (then: local_round)."""
+        c0 = self.info().configs
+        nn = ctypes.c_uint64(0)
+        found = ctypes.c_int32(0)
+        nr = ctypes.c_uint32(0)
+        rc = lib().s2lc_dist_local_run(self._d, min(wide, 0xFFFFFFFF), ctypes.byref(nn), ctypes.byref(found),
+                                       ctypes.byref(nr))
+        if rc == -6:  # S2LC_EUNSUPPORTED
+            return None
+        self._chk(rc, "dist_local_run")
+        return nn.value, bool(found.value), nr.value, self.info().configs - c0
+
     def keep_owned(self) -> int:
         n = ctypes.c_uint64(0)
         self._chk(lib().s2lc_dist_keep_owned(self._d, ctypes.byref(n)), "dist_keep_owned")
@@ -212,17 +228,28 @@ def _walk(traces: List[np.ndarray], parent: int, move: int) -> Optional[List[int
 
 
 def check_distributed(checker, history: History, group=None, witness: bool = True,
-                      wide: int = 4096) -> DistResult:
+                      wide: int = 4096, persistent: Optional[bool] = None) -> DistResult:
     """Check one history with every rank of `group` (default: the world).
 
     Rounds whose frontier is narrower than `wide` configurations run
-    replicated (every rank the whole round, no exchange); wider rounds run
-    partitioned by owner with one all-to-all per round. wide=0 partitions
-    every round."""
+    replicated (every rank the whole round, no exchange): after round 0 they
+    run inside the persistent kernel of the single-GPU level search
+    (s2lc_dist_local_run: solo and persistent rounds, one host sync per
+    launch) unless persistent=False (one host-driven round per call). Wider
+    rounds run partitioned by owner with one all-to-all per round. wide=0
+    partitions every round.
+
+    persistent=None: on with nccl (one process per GPU) and for one rank; off
+    for several gloo ranks, which are the tests' ranks sharing one GPU: the
+    persistent grid of one process needs a workgroup resident on every CU at
+    once, and kernels of other processes on the same GPU do not leave room
+    for it (its barrier times out after 2 s and the call fails)."""
     rank = dist.get_rank(group)
     world = dist.get_world_size(group)
     device = torch.device("cuda", torch.cuda.current_device())
     ex = _Exchange(group, device)
+    if persistent is None:
+        persistent = ex.on_gpu or world == 1
     ds = DistSearch(checker, history, rank, world)
     cb = ds.info().config_bytes
     keep = []  # device buffers holding this rank's frontier (kept alive)
@@ -241,14 +268,20 @@ def check_distributed(checker, history: History, group=None, witness: bool = Tru
                 rounds += 1
             first = False
             if replicated:
-                nn, found = ds.local_round()
+                run = ds.local_run(wide if world > 1 else 1 << 32) if (persistent and rounds > 0) else None
+                if run is not None:
+                    nn, found, nr, dconf = run
+                    rounds += nr - 1  # (this iteration counted one)
+                else:
+                    nn, found = ds.local_round()
+                    dconf = 0 if found else nn
+                configs += dconf
                 if found:
                     verdict = Ok
                     break
                 if nn == 0:
                     verdict = Illegal
                     break
-                configs += nn
                 if world > 1 and nn >= wide:
                     ds.keep_owned()
                     replicated = False

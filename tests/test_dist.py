@@ -52,22 +52,28 @@ def test_walk_crosses_ranks():
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("world,wide,backend", [(1, 4096, "gloo"), (2, 0, "gloo"), (2, 256, "gloo"),
-                                                (3, 1024, "gloo"), (1, 0, "nccl")])
-def test_distributed_search_one_gpu(world, wide, backend):
+@pytest.mark.parametrize("world,wide,backend,persistent", [(1, 4096, "gloo", True), (1, 4096, "gloo", False),
+                                                           (2, 0, "gloo", None), (2, 256, "gloo", None),
+                                                           (3, 1024, "gloo", None),
+                                                           (1, 0, "nccl", None), (1, 4096, "nccl", True)])
+def test_distributed_search_one_gpu(world, wide, backend, persistent):
     """wide=0: every round partitioned; otherwise replicated while the
     frontier is narrower than `wide`, partitioned above it (both switches
-    happen on H212 / C5bad at 256 and 1024). The nccl case is RCCL with one
-    rank partitioning every round (a self-exchange through the same
-    all-to-all calls the multi-GPU run makes)."""
+    happen on H212 / C5bad at 256 and 1024); replicated rounds inside the
+    persistent kernel (s2lc_dist_local_run) or host-driven one by one. The
+    nccl cases are RCCL with one rank: partitioning every round (a
+    self-exchange through the same all-to-all calls the multi-GPU run makes),
+    and the persistent replicated rounds."""
     import dist_worker
     ref = golden("hard_reduced.json")
     names = [n for n in ("H174", "C5bad", "H212") if n in ref]
     port = random.randint(20000, 40000)
-    out = _spawn(dist_worker.search_worker, [(r, world, port, backend, names, wide) for r in range(world)])
+    out = _spawn(dist_worker.search_worker, [(r, world, port, backend, names, wide, persistent) for r in range(world)])
+    rc = golden("hard_round_counts.json")
     for rank, res in out:
         for name, verdict, rounds, configs, wvalid, wlen, n_ops in res:
             assert verdict == ref[name]["verdict"], (rank, name, verdict)
+            assert rounds == rc[name]["0"]["rounds"], (rank, name, rounds)
             if verdict == "Ok":
                 assert wvalid and wlen == n_ops, (rank, name, wvalid, wlen)
     # every rank agrees
