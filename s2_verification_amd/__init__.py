@@ -559,6 +559,7 @@ class Checker:
         if not ctx:
             raise S2LCError(st.value, "no usable HIP device for the S2 checker")
         self._ctx = ctx
+        self.stream = stream or 0  # the caller's hipStream_t the context launches on (0: its own)
 
     def __del__(self):
         c, self._ctx = getattr(self, "_ctx", None), None

@@ -805,7 +805,8 @@ int s2lc_dist_create(s2lc_ctx* c, const s2lc_history* h, int rank, int world, s2
     if (hipSetDevice(c->device) != hipSuccess) { c->err = "hipSetDevice"; return S2LC_EHIP; }
     auto* x = new s2lc_dist();
     x->ctx = c;
-    const int rc = dist_create(x->d, &h->h, (uint32_t)rank, (uint32_t)world, c->red_off, c->err);
+    const int rc = dist_create(x->d, &h->h, (uint32_t)rank, (uint32_t)world, c->red_off,
+                               c->own_stream ? nullptr : c->stream, c->err);
     if (rc) { dist_release(x->d); delete x; return rc; }
     *out = x;
     return 0;

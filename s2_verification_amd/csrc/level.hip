@@ -473,7 +473,7 @@ int level_search(DevBatch& b, uint32_t h, hipStream_t st, const RunOpts& ro, int
 // ============================================================================
 
 int dist_create(DistLevel& d, const History* h, uint32_t rank, uint32_t world, uint32_t reductions_off,
-                std::string& err) {
+                hipStream_t stream, std::string& err) {
   if (world < 1 || world > 8 || rank >= world) { err = "world must be 1..8"; return S2LC_EINVAL; }
   std::vector<const History*> hs{h};
   int rc = batch_upload(d.b, hs, reductions_off, err);
@@ -492,7 +492,15 @@ int dist_create(DistLevel& d, const History* h, uint32_t rank, uint32_t world, u
   LVCHK(hipMemGetInfo(&free_b, &total_b));
   d.trace_cap = std::min<uint64_t>(1ull << 29, (uint64_t)(free_b / 16) / sizeof(TraceEnt));
   LVCHK(hipMalloc(&d.trace, d.trace_cap * sizeof(TraceEnt)));
-  LVCHK(hipStreamCreateWithFlags(&d.stream, hipStreamNonBlocking));
+  // the caller's stream (its collectives and the search are then ordered on
+  // the device), else a stream of its own
+  if (stream) {
+    d.stream = stream;
+    d.own_stream = false;
+  } else {
+    LVCHK(hipStreamCreateWithFlags(&d.stream, hipStreamNonBlocking));
+    d.own_stream = true;
+  }
   d.round = 0;
   return 0;
 }
@@ -501,7 +509,7 @@ void dist_release(DistLevel& d) {
   if (d.own_cnt) (void)hipFree(d.own_cnt);
   if (d.own_pos) (void)hipFree(d.own_pos);
   if (d.trace) (void)hipFree(d.trace);
-  if (d.stream) (void)hipStreamDestroy(d.stream);
+  if (d.stream && d.own_stream) (void)hipStreamDestroy(d.stream);
   d.own_cnt = nullptr; d.own_pos = nullptr; d.trace = nullptr; d.stream = nullptr;
   batch_release(d.b);
 }

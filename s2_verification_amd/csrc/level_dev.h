@@ -73,7 +73,7 @@ struct LvCtl {
   uint32_t found;     // a child completed (Ok)
   uint32_t overflow;  // a staging stripe over capacity
   uint32_t done_blocks;  // lv_insert blocks finished (the last one closes the round)
-  uint32_t found_parent, found_move, found_p4, _p0;
+  uint32_t found_parent, found_move, found_p4, closed;  // closed: children closed (the rest failed the P1 precheck)
   unsigned long long children;  // children generated this round
   unsigned long long prof_end;  // S2LC_PROF: latest expansion end of the round (wall clock)
   uint32_t _pad[4];
@@ -106,7 +106,7 @@ struct LvRun {
   uint32_t deep_trace, deep_len;  // Illegal: a configuration of the deepest non-empty round
   uint32_t last_tbase;     // trace index of the first winner of the last non-empty round
   uint32_t last_nf;        // frontier expanded by the last round
-  unsigned long long last_children;  // children it generated (slices per configuration)
+  unsigned long long last_closed;  // children it closed (slices per configuration)
   uint32_t solo_rounds;    // rounds run as solo rounds (LvSolo)
   uint32_t _pad;
 };
@@ -487,9 +487,9 @@ struct LvRoundIn {
 // whole configurations. The expected moves per configuration come from the
 // previous round.
 __device__ __forceinline__ uint32_t lv_slices(uint32_t K, uint32_t nf, uint32_t nwaves, uint32_t last_nf,
-                                              unsigned long long last_children) {
+                                              unsigned long long last_closed) {
   uint32_t c_est = K;
-  if (last_nf) c_est = (uint32_t)min<unsigned long long>(K, last_children / last_nf + 1);
+  if (last_nf) c_est = (uint32_t)min<unsigned long long>(K, last_closed / last_nf + 1);
   return max(1u, min(c_est + (c_est >> 2) + 1, (2u * nwaves + nf - 1) / max(nf, 1u)));
 }
 
@@ -694,6 +694,7 @@ __device__ __forceinline__ bool lv_expand(const LvParams& p, const LvRoundIn& in
     rleft = LV_RESERVE;
   }
   unsigned long long kids = 0;
+  uint32_t closed = 0;  // children closed by this wave (wave-uniform)
 #ifdef S2LC_PROF
   unsigned long long lv_acc[10] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0}, lv_t = 0;
 #endif
@@ -922,6 +923,7 @@ __device__ __forceinline__ bool lv_expand(const LvParams& p, const LvRoundIn& in
 #ifdef S2LC_PROF
         const unsigned long long tc0_ = clock64();
 #endif
+        ++closed;
         const int cr = lv_closure<NQ>(H, d, cnt, s_cs, PL, lane, cs_, p.hflags, pmin, p.recs, mr, SOLO ? NX : nullptr);
 #ifdef S2LC_PROF
         if (SOLO && lane == 0) {  // closure cycles: [8] ALIVE, [9] others; [10] ALIVE count; [11] stage cycles
@@ -1004,6 +1006,7 @@ __device__ __forceinline__ bool lv_expand(const LvParams& p, const LvRoundIn& in
 #endif
   if (MODE == 0 && rleft) lv_release<NQ>(p, stripe, rk, rleft);
   if (lane == 0 && kids) atomicAdd(SOLO ? &sol->kids : &p.ctl->children, kids);
+  if (!SOLO && lane == 0 && closed) atomicAdd(&p.ctl->closed, closed);
   return wave_id < items;
 }
 
@@ -1023,7 +1026,7 @@ __global__ __launch_bounds__(LV_BLOCK) void lv_round(LvParams p) {
   if (p.f1 == LV_NONE) in.f0 = 0;
   if (p.init) in.nf = 1;
   const uint32_t nwaves = gridDim.x * (LV_BLOCK / 64);
-  in.S = p.init ? 1u : lv_slices(p.K, in.nf, nwaves, p.run ? p.run->last_nf : 0u, p.run ? p.run->last_children : 0ull);
+  in.S = p.init ? 1u : lv_slices(p.K, in.nf, nwaves, p.run ? p.run->last_nf : 0u, p.run ? p.run->last_closed : 0ull);
   in.tbase = 0;
   in.wit = 0;
   lv_expand<NQ, 0>(p, in, s_heads[threadIdx.x >> 6], s_cs);
@@ -1047,6 +1050,7 @@ __device__ __forceinline__ bool lv_eq(const LCfg<NQ>* a, const LCfg<NQ>* b, uint
 struct LvCounts {
   uint32_t nn, ovf, fnd, fpar, fmov, fp4;
   unsigned long long ch;
+  uint32_t closed;
 };
 __device__ __forceinline__ LvCounts lv_read_counts(LvCtl* c) {
   LvCounts k;
@@ -1057,6 +1061,7 @@ __device__ __forceinline__ LvCounts lv_read_counts(LvCtl* c) {
   k.fmov = ld_agent(&c->found_move);
   k.fp4 = ld_agent(&c->found_p4);
   k.ch = ld_agent64(&c->children);
+  k.closed = ld_agent(&c->closed);
   return k;
 }
 
@@ -1066,7 +1071,7 @@ __device__ __forceinline__ void lv_close_state(LvRun& R, const LvCounts& k, uint
                                                uint32_t scap, uint64_t trace_cap) {
   R.children += k.ch;
   R.last_nf = rnd == 0 ? 0u : R.nf;
-  R.last_children = k.ch;
+  R.last_closed = k.closed;
   if (k.ovf) {
     R.done = LVR_OVERFLOW;  // the host re-runs this round in frontier chunks
   } else if (k.fnd) {
@@ -1395,7 +1400,7 @@ __device__ void lv_solo_rounds(const LvParams& p, const LvPersist& q, LvRun& R, 
     if (threadIdx.x == 0) {
       LvCounts k;
       k.nn = S.alive; k.ovf = S.ovf; k.fnd = S.found;
-      k.fpar = S.fpar; k.fmov = S.fmov; k.fp4 = S.fp4; k.ch = S.kids;
+      k.fpar = S.fpar; k.fmov = S.fmov; k.fp4 = S.fp4; k.ch = S.kids; k.closed = 0;
       lv_close_state(R, k, r, p.rcounts, p.scap, p.trace_cap);
       R.solo_rounds++;
     }
@@ -1471,6 +1476,9 @@ __global__ __launch_bounds__(LV_BLOCK) void lv_persist(LvParams p, LvPersist q) 
         reinterpret_cast<uint32_t*>(&s_run)[threadIdx.x] = ld_agent(reinterpret_cast<const uint32_t*>(p.run) + threadIdx.x);
       if (!ok && threadIdx.x == 0) s_run.done = LVR_ABORT;
       __syncthreads();
+#ifdef S2LC_PROF
+      t_round = wall_clock64();  // (the grid rounds' timing excludes the solo phases)
+#endif
       it += max(1u, s_run.round - r_before);
       if (s_run.done != LVR_RUNNING || it >= q.max_rounds || s_run.nf > q.nf_max) break;
       continue;
@@ -1491,7 +1499,7 @@ __global__ __launch_bounds__(LV_BLOCK) void lv_persist(LvParams p, LvPersist q) 
     LvRoundIn in;
     in.f0 = 0;
     in.nf = s_run.nf;
-    in.S = lv_slices(p.K, in.nf, nwaves, s_run.last_nf, s_run.last_children);
+    in.S = lv_slices(p.K, in.nf, nwaves, s_run.last_nf, s_run.last_closed);
     in.tbase = (uint32_t)s_run.tnext;
     in.wit = s_run.witness;
     const bool worked = lv_expand<NQ, 1>(rp, in, s_heads[threadIdx.x >> 6], s_cs);
@@ -1538,7 +1546,7 @@ __global__ __attribute__((unused)) void lv_run_init(LvRun* R, unsigned long long
   R->configs = 0; R->children = 0; R->tnext = tnext; R->max_configs = max_configs;
   R->found_parent = TRACE_NONE; R->found_move = LV_NONE; R->found_p4 = 0;
   R->witness = witness; R->deep_trace = TRACE_NONE; R->deep_len = 0; R->last_tbase = TRACE_NONE;
-  R->last_nf = 0; R->last_children = 0; R->solo_rounds = 0;
+  R->last_nf = 0; R->last_closed = 0; R->solo_rounds = 0;
 }
 
 // ---- distributed: owner of a configuration ---------------------------------

@@ -191,6 +191,7 @@ struct DistLevel {
   TraceEnt* trace = nullptr;     // this rank's trace pool
   uint64_t trace_cap = 0, tnext = 0;
   hipStream_t stream = nullptr;
+  bool own_stream = true;        // false: the context's (caller's) stream
   const uint8_t* cur = nullptr;  // current frontier: received buffer (caller-owned)
   int cur_sel = 0;               // index list of the current frontier: b.lv.idx[cur_sel]
   uint32_t nf = 0, slot_hi = 0, round = 0;  // slot_hi: staging walk bound (64 x longest stripe)
@@ -199,7 +200,7 @@ struct DistLevel {
   double ms = 0;
 };
 int dist_create(DistLevel& d, const History* h, uint32_t rank, uint32_t world, uint32_t reductions_off,
-                std::string& err);
+                hipStream_t stream, std::string& err);
 void dist_release(DistLevel& d);
 int dist_expand(DistLevel& d, uint64_t* counts, int* found, std::string& err);
 int dist_pack(DistLevel& d, uint8_t* send, const uint64_t* counts, std::string& err);

@@ -140,12 +140,20 @@ class _Exchange:
     """The two collectives of a round, on CUDA tensors (nccl/RCCL) or staged
     through host memory (gloo)."""
 
-    def __init__(self, group, device: torch.device):
+    def __init__(self, group, device: torch.device, lib_stream: int = 0):
         self.group = group
         self.device = device
         self.on_gpu = dist.get_backend(group) == "nccl"
         self.tdev = device if self.on_gpu else torch.device("cpu")
         self.world = dist.get_world_size(group)
+        # the library launches on torch's current stream (Checker(stream=...)):
+        # its kernels are ordered after the collectives on the device, with no
+        # host synchronization in between
+        self.same_stream = lib_stream != 0 and lib_stream == torch.cuda.current_stream(device).cuda_stream
+
+    def _lib_sync(self):
+        if not self.same_stream:
+            torch.cuda.current_stream(self.device).synchronize()  # the library reads on its own stream
 
     def counts(self, counts, found: bool, staged: int):
         """All-to-all of (count for the receiver, found, staged total) triples."""
@@ -161,12 +169,12 @@ class _Exchange:
         if self.on_gpu:
             recv = torch.empty(max(total, 1), dtype=torch.uint8, device=self.device)
             dist.all_to_all_single(recv[:total] if total else recv[:0], send, out_bytes, in_bytes, group=self.group)
-            torch.cuda.current_stream(self.device).synchronize()  # the library reads recv on its own stream
+            self._lib_sync()
             return recv
         recv_h = torch.empty(total, dtype=torch.uint8)
         dist.all_to_all_single(recv_h, send.cpu(), out_bytes, in_bytes, group=self.group)
         recv = recv_h.to(self.device) if total else torch.empty(1, dtype=torch.uint8, device=self.device)
-        torch.cuda.current_stream(self.device).synchronize()
+        self._lib_sync()
         return recv
 
     def sum(self, v: int) -> int:
@@ -184,7 +192,7 @@ class _Exchange:
         dist.all_gather(out, src, group=self.group)
         full = torch.cat([out[w][:n_bytes[w]] for w in range(self.world)]) if sum(n_bytes) else out[0][:1]
         full = full.to(self.device).contiguous()
-        torch.cuda.current_stream(self.device).synchronize()
+        self._lib_sync()
         return full
 
     def gather_small(self, vals: List[int]) -> List[List[int]]:
@@ -247,7 +255,7 @@ def check_distributed(checker, history: History, group=None, witness: bool = Tru
     rank = dist.get_rank(group)
     world = dist.get_world_size(group)
     device = torch.device("cuda", torch.cuda.current_device())
-    ex = _Exchange(group, device)
+    ex = _Exchange(group, device, getattr(checker, "stream", 0))
     if persistent is None:
         persistent = ex.on_gpu or world == 1
     ds = DistSearch(checker, history, rank, world)

@@ -26,6 +26,12 @@ CONFIGS = {
                **{**BASE, "p_indefinite": 0.03}),
     "C5bad": dict(workflow=WF_REGULAR, num_clients=32, ops_per_client=1000, seed=5, max_client_ids=1 << 20,
                   violation=VIOL_READ_HASH, **{**BASE, "p_indefinite": 0.03}),
+    # a single hard history whose WIDE rounds dominate (the shape the
+    # distributed search partitions): 24 clients x 300 ops with 10% indefinite
+    # appends, K = 243 chains; 30 of its 2,231 rounds hold 1.03 M of its 1.11 M
+    # unique configurations (frontier up to 273 k); CPU reduced search ~2 min
+    "C5wide": dict(workflow=WF_REGULAR, num_clients=24, ops_per_client=300, seed=12, max_client_ids=1 << 20,
+                   **{**BASE, "p_indefinite": 0.10}),
     # mid-size hard histories (level-search parity against the CPU reduced search)
     "H174": dict(workflow=WF_REGULAR, num_clients=32, ops_per_client=1000, seed=5, max_client_ids=1 << 20,
                  **{**BASE, "p_indefinite": 0.015}),

@@ -43,7 +43,9 @@ def search_worker(rank, world, port, backend, names, wide, persistent, q):
         from s2_verification_amd.distributed import check_distributed
         torch.cuda.set_device(0 if backend == "gloo" else rank)
         dist = _init(rank, world, port, backend)
-        checker = s2.Checker(device=torch.cuda.current_device())
+        # nccl: the library on torch's stream (no host syncs around the collectives)
+        checker = s2.Checker(device=torch.cuda.current_device(),
+                             stream=torch.cuda.current_stream().cuda_stream if backend == "nccl" else 0)
         out = []
         for name in names:
             h = W.config_history(name)

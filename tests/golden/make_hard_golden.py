@@ -1,5 +1,5 @@
 """Verdicts of the hard single histories (workloads.CONFIGS C5, C5bad, H174,
-H212) from the CPU reduced search (oracle/reduced.c), committed as
+H212, C5wide) from the CPU reduced search (oracle/reduced.c), committed as
 tests/golden/hard_reduced.json so the GPU tests need not re-run minutes of CPU
 search. Also records a fingerprint of each history's event list, so a changed
 simulator is caught instead of silently comparing against stale verdicts.
@@ -36,4 +36,4 @@ def main(names):
 
 
 if __name__ == "__main__":
-    main(sys.argv[1:] or ["H174", "H212", "C5bad", "C5"])
+    main(sys.argv[1:] or ["H174", "H212", "C5bad", "C5", "C5wide"])

@@ -25,14 +25,16 @@ import oracle as orc  # noqa: E402
 from s2_verification_amd import workloads as W  # noqa: E402
 from helpers import config_digest  # noqa: E402
 
-CASES = {"H174": [0, 2], "H212": [0, 2], "C5bad": [0, 2, 4]}
+CASES = {"H174": [0, 2], "H212": [0, 2], "C5bad": [0, 2, 4], "C5wide": [0]}
 
 
-def main():
-    out = {}
-    for name, offs in CASES.items():
+def main(names):
+    path = os.path.join(HERE, "hard_round_counts.json")
+    out = json.load(open(path)) if os.path.exists(path) else {}
+    for name in names:
+        offs = CASES[name]
         h = W.config_history(name)
-        ea = orc.from_s2lc_numpy(h.events_numpy())
+        ea = orc.from_s2lc_numpy(h.events_numpy(), owner=h)
         out[name] = {"digest": config_digest(name)}
         for off in offs:
             t = time.time()
@@ -40,9 +42,9 @@ def main():
             out[name][str(off)] = {"verdict": v, "rounds": st["rounds"], "configs": st["configs"],
                                    "counts": st["round_counts"], "cpu_seconds": round(time.time() - t, 1)}
             print(name, off, v, st["rounds"], st["configs"], flush=True)
-    with open(os.path.join(HERE, "hard_round_counts.json"), "w") as f:
+    with open(path, "w") as f:
         json.dump(out, f, sort_keys=True, separators=(",", ":"))
 
 
 if __name__ == "__main__":
-    main()
+    main(sys.argv[1:] or list(CASES))

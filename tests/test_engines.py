@@ -193,7 +193,7 @@ def _set_mode(monkeypatch, mode):
 
 @pytest.mark.parametrize("mode", list(LEVEL_MODES))
 @pytest.mark.parametrize("name,off", [("H174", 0), ("H174", 2), ("H212", 0), ("H212", 2), ("C5bad", 0),
-                                      ("C5bad", 2), ("C5bad", 4)])
+                                      ("C5bad", 2), ("C5bad", 4), ("C5wide", 0)])
 def test_hard_round_counts(name, off, mode, monkeypatch):
     """Hard single histories (> 128 chains, the level search): per-round counts
     against the committed CPU reduced-search counts, in every round mode."""
@@ -221,7 +221,7 @@ def test_hard_round_counts(name, off, mode, monkeypatch):
         assert st["level_persist_rounds"] == r.rounds, st
     if mode in ("no_solo", "no_persist"):
         assert st["level_solo_rounds"] == 0, st
-    else:  # most rounds of these histories keep one configuration
+    elif name != "C5wide":  # most rounds of these histories keep one configuration
         assert st["level_solo_rounds"] > r.rounds // 2, st
 
 

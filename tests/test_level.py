@@ -79,7 +79,7 @@ def test_level_configs_c1_c3(checker, level_only):
             assert g.witness is not None and len(g.witness) == h.info()["n_ops"]
 
 
-@pytest.mark.parametrize("name", ["H174", "H212", "C5bad", "C5"])
+@pytest.mark.parametrize("name", ["H174", "H212", "C5bad", "C5", "C5wide"])
 def test_hard_single_history(checker, name):
     """> 128 chains: always the level search. Verdict = CPU reduced search
     (committed), Ok witness replay-verified; the bad C5 differs from C5 in

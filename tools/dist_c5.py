@@ -31,7 +31,7 @@ if a.backend == "nccl":
     dist.init_process_group("nccl", device_id=torch.device("cuda", dev))
 else:
     dist.init_process_group("gloo")
-ck = s2.Checker(device=dev)
+ck = s2.Checker(device=dev, stream=torch.cuda.current_stream().cuda_stream if a.backend == "nccl" else 0)
 for name in a.names:
     h = W.config_history(name)
     r = check_distributed(ck, h, wide=a.wide)
