@@ -266,13 +266,23 @@ int batch_upload(DevBatch& b, const std::vector<const History*>& hs, uint32_t re
   // times larger (twice the histories per wave).
   const char* e8 = getenv("S2LC_PACK8");
   const uint32_t k8 = (e8 && e8[0] == '1') ? 8u : 0u;
+  // S2LC_PACK32_TOP=n (diagnostics): the n longest K <= 16 histories run in
+  // 32-lane groups (two histories per wave instead of four)
+  const char* e32 = getenv("S2LC_PACK32_TOP");
+  const uint32_t top32 = e32 ? (uint32_t)strtoul(e32, nullptr, 10) : 0u;
+  std::vector<uint8_t> to32(n, 0);
+  {
+    uint32_t c = 0;
+    for (uint32_t i : b.lpt)
+      if (c < top32 && b.h_hist[i].K > k8 && b.h_hist[i].K <= 16) { to32[i] = 1; ++c; }
+  }
   b.pack8_kmax = k8;
   uint32_t no = 0;
   for (uint32_t i : b.lpt) if (b.h_hist[i].K <= k8) s_order[no++] = i;
   b.n_pack8 = no;
-  for (uint32_t i : b.lpt) if (b.h_hist[i].K > k8 && b.h_hist[i].K <= 16) s_order[no++] = i;
+  for (uint32_t i : b.lpt) if (b.h_hist[i].K > k8 && b.h_hist[i].K <= 16 && !to32[i]) s_order[no++] = i;
   b.n_pack16 = no - b.n_pack8;
-  for (uint32_t i : b.lpt) if (b.h_hist[i].K > 16 && b.h_hist[i].K <= 32) s_order[no++] = i;
+  for (uint32_t i : b.lpt) if ((b.h_hist[i].K > 16 && b.h_hist[i].K <= 32) || to32[i]) s_order[no++] = i;
   b.n_pack32 = no - b.n_pack8 - b.n_pack16;
   HIPCHK(hipMemcpy(b.arena, b.stage, stage_bytes, hipMemcpyHostToDevice));
   return 0;
