@@ -597,7 +597,7 @@ struct LvSolo {
   uint16_t keep[64 * NQ];  // advance per chain of the child with staging index 0
   uint64_t tail, hash, chx;        // the configuration: state, XOR of its chain terms
   uint64_t ktail, khash, kchx;     // the kept child
-  uint32_t tok, pmin, ptrace, ktok, kmr, cs_end;
+  uint32_t tok, pmin, ptrace, ktok, kmr, kmv, cs_end;
   uint32_t alive, found, fpar, fmov, fp4, ovf, tbase, wit;
   unsigned long long kids;
   uint64_t wx[LV_BLOCK / 64];
@@ -962,7 +962,16 @@ __device__ __forceinline__ bool lv_expand(const LvParams& p, const LvRoundIn& in
             uint32_t k = 0;
             if (lane == 0) k = atomicAdd(&sol->alive, 1u);
             k = rl(k, 0);
-            if (k < p.scs) {
+            // the first survivor stays in LDS only: it is written to the
+            // staging array after the round if it is not the only one
+            if (k == 0) {
+#pragma unroll
+              for (int q = 0; q < NQ; ++q) sol->keep[lane + 64 * q] = (uint16_t)d[q];
+              if (lane == 0) {
+                sol->ktail = cs_.tail; sol->khash = cs_.hash; sol->ktok = cs_.tok;
+                sol->kchx = cdx; sol->kmr = mr; sol->kmv = mv;
+              }
+            } else if (k < p.scs) {
               lv_solo_put<NQ>(p, k, cs_, fp, mr, ptrace, mv, in.tbase, in.wit, cnt, d);
             } else if (lane == 0) {
               sol->ovf = 1u;
@@ -970,14 +979,6 @@ __device__ __forceinline__ bool lv_expand(const LvParams& p, const LvRoundIn& in
 #ifdef S2LC_PROF
             if (lane == 0) atomicAdd(&sol->pc[3], clock64() - ts0_);
 #endif
-            if (k == 0) {
-#pragma unroll
-              for (int q = 0; q < NQ; ++q) sol->keep[lane + 64 * q] = (uint16_t)d[q];
-              if (lane == 0) {
-                sol->ktail = cs_.tail; sol->khash = cs_.hash; sol->ktok = cs_.tok;
-                sol->kchx = cdx; sol->kmr = mr;
-              }
-            }
           } else if (FUSED) {
             lv_stage_insert<NQ>(p, in, stripe, rk, rleft, cs_, fp, mr, ptrace, mv, cnt, d);
           } else {
@@ -1322,6 +1323,34 @@ __device__ __forceinline__ void lv_solo_head(const LvParams& p, const OpRec* h, 
   for (int k = 0; k < LV_SOLO_HP; ++k) S.hp[k][j] = hv[k];
 }
 
+// The whole workgroup writes a solo configuration held in LDS (counts
+// S.cnt[j] + (child ? S.keep[j] : 0), the configuration's or the kept child's
+// header) into staging slot 0 of `stg` / index list `idx`: the form a grid
+// round leaves its frontier in.
+template <int NQ>
+__device__ void lv_solo_write(const LvSolo<NQ>& S, bool child, uint8_t* stg, uint32_t* idx, uint32_t tgid,
+                              uint32_t trace_id, uint32_t K) {
+  LCfg<NQ>* o = lv_cfg<NQ>(stg, 0);
+  for (uint32_t j = threadIdx.x; j < 64u * NQ; j += LV_BLOCK)
+    st_wt16(&o->cnt[j], (uint16_t)(j < K ? S.cnt[j] + (child ? S.keep[j] : 0u) : 0u));
+  if (threadIdx.x < 16) {
+    const uint32_t l = threadIdx.x;
+    const uint64_t tail = child ? S.ktail : S.tail, hash = child ? S.khash : S.hash;
+    const uint32_t tok = child ? S.ktok : S.tok, mr = child ? S.kmr : S.pmin;
+    const uint64_t fp = mix64((child ? S.kchx : S.chx) ^ lv_state_term(tail, hash, tok));
+    const unsigned long long w = l == 0 ? tail
+                               : l == 1 ? hash
+                               : l == 2 ? fp
+                               : l == 3 ? ((unsigned long long)mr << 32 | tok)
+                               : l == 4 ? ((unsigned long long)(child ? S.kmv : LV_NONE) << 32 | (child ? S.ptrace : TRACE_NONE))
+                               : l == 5 ? ((unsigned long long)LV_NONE << 32 | trace_id)
+                                        : 0ull;
+    st_wt64(reinterpret_cast<unsigned long long*>(o) + l, w);
+  }
+  if (threadIdx.x == 0) st_wt32(&idx[0], 0u);
+  (void)tgid;
+}
+
 // Solo rounds (LvSolo), run by workgroup 0 of lv_persist while the others
 // wait at the grid barrier: enter from the frontier's one configuration, go on
 // while every round keeps exactly one, and stop when a round keeps none or
@@ -1403,8 +1432,17 @@ __device__ void lv_solo_rounds(const LvParams& p, const LvPersist& q, LvRun& R, 
       k.fpar = S.fpar; k.fmov = S.fmov; k.fp4 = S.fp4; k.ch = S.kids; k.closed = 0;
       lv_close_state(R, k, r, p.rcounts, p.scap, p.trace_cap);
       R.solo_rounds++;
+      // the first survivor's trace entry (it was not staged)
+      if (!S.found && !S.ovf && S.alive && S.wit) p.trace[S.tbase] = TraceEnt{S.ptrace, S.kmv};
     }
     lv_sync_lds();
+    if (S.ovf && !S.found) {
+      // the host re-runs round r from its frontier: this configuration, in
+      // the staging array the round read its frontier from
+      lv_solo_write<NQ>(S, false, q.stg[(r + 1) & 1], q.idx[(r + 1) & 1], p.tgid, S.ptrace, K);
+    } else if (!S.found && S.alive >= 2) {
+      lv_solo_write<NQ>(S, true, q.stg[r & 1], q.idx[r & 1], p.tgid, S.wit ? p.tgid + S.tbase : TRACE_NONE, K);
+    }
     LV_SOLO_T(4);
     if (R.done != LVR_RUNNING || R.nf != 1) break;
     // the only survivor (staging slot 0) is the next round's configuration:
@@ -1421,10 +1459,10 @@ __device__ void lv_solo_rounds(const LvParams& p, const LvPersist& q, LvRun& R, 
       S.tail = S.ktail; S.hash = S.khash; S.tok = S.ktok; S.chx = S.kchx; S.pmin = S.kmr;
       S.ptrace = S.wit ? p.tgid + S.tbase : TRACE_NONE;
     }
-#ifdef S2LC_PROF
     lv_sync_lds();
-#endif
     LV_SOLO_T(5);
+    if (n + 1 == max_rounds)  // leaving with one configuration: the next round's frontier
+      lv_solo_write<NQ>(S, false, q.stg[r & 1], q.idx[r & 1], p.tgid, S.ptrace, K);
   }
 #ifdef S2LC_PROF
   if (threadIdx.x == 0 && p.prof) {  // [7] solo rounds, [8] their wall-clock ticks, [16..21] phase cycles
