@@ -129,6 +129,9 @@ struct ChainLane {
   uint32_t cc;                     // count of r
   uint4 wa[4], wb[4], wc[4], wd[4];  // window: records at counts w0 .. w0+3
   OpRec r;                         // record at count cc (null record when !on)
+#ifdef S2LC_PROF
+  bool refilled;                   // the last at() reloaded the window
+#endif
   __device__ __forceinline__ void reset(const OpRec* b, bool on_, uint32_t len_) {
     base = b;
     on = on_;
@@ -141,9 +144,15 @@ struct ChainLane {
     r.flags = OPF_SENTINEL;
   }
   __device__ __forceinline__ void at(uint32_t c) {
+#ifdef S2LC_PROF
+    refilled = false;
+#endif
     if (!on || c == cc) return;
     uint32_t o = c - w0;
     if (o >= (uint32_t)PACK_W) {
+#ifdef S2LC_PROF
+      refilled = true;
+#endif
       // clamp to the chain: a record past its sentinel is never selected
       const OpRec* q = base + c;
       const uint32_t last = len - 1 - c;  // c < len always (sentinel included)
@@ -176,12 +185,19 @@ struct ChainLane {
 template <int L>
 __device__ __forceinline__ int pack_closure(ChainLane& ch, const uint64_t* __restrict__ pool, uint32_t& cnt,
                                             const State& s, uint32_t hflags,
-                                            uint64_t gmask, uint32_t& minret_out) {
+                                            uint64_t gmask, uint32_t& minret_out,
+                                            unsigned long long* prof_pass = nullptr) {
   const bool nowrap = hflags & H_NOWRAP;
   const bool p2 = hflags & H_P2OK;
   const bool p4 = hflags & H_P4;
   for (;;) {
     ch.at(cnt);
+#ifdef S2LC_PROF
+    if (prof_pass) {  // [0] passes, [1] passes that reloaded a window (the group waited on memory)
+      prof_pass[0]++;
+      if (__ballot(ch.refilled) & gmask) prof_pass[1]++;
+    }
+#endif
     const OpRec& r = ch.r;
     const uint32_t minret = gmin_u32<L>(r.ret_ev);
     const uint64_t bound = gmin_u64<L>(r.sufmin);
@@ -226,6 +242,7 @@ template <int L>
 __global__ __launch_bounds__(PACK_BLOCK, S2LC_PACK_MINW) void pack_kernel(Params p) {
 #ifdef S2LC_PROF
   unsigned long long pk_acc[6] = {0, 0, 0, 0, 0, 0};
+  unsigned long long pk_pass[2] = {0, 0};
   unsigned long long pk_t = 0;
 #endif
   using C = PCfg<L>;
@@ -358,7 +375,11 @@ __global__ __launch_bounds__(PACK_BLOCK, S2LC_PACK_MINW) void pack_kernel(Params
           uint32_t cnt = pcnt + (gl == j ? 1u : 0u);
           uint32_t mr = 0;
           PK_LAP(2);
+#ifdef S2LC_PROF
+          const int cr = pack_closure<L>(ch, p.pool, cnt, ks, hd.flags, gmask, mr, pk_pass);
+#else
           const int cr = pack_closure<L>(ch, p.pool, cnt, ks, hd.flags, gmask, mr);
+#endif
           if (cr == CL_ALIVE && nn == 0) {
             // this child becomes the next round's first configuration: start
             // loading its candidate heads' record hashes now
@@ -443,6 +464,9 @@ __global__ __launch_bounds__(PACK_BLOCK, S2LC_PACK_MINW) void pack_kernel(Params
     if (gl == 0) {
       for (int i_ = 0; i_ < 3; ++i_) { atomicAdd(&g_prof[10 + i_], pk_acc[i_]); pk_acc[i_] = 0; }
       atomicAdd(&g_prof[13], (unsigned long long)rounds);
+      atomicAdd(&g_prof[8], pk_pass[0]);
+      atomicAdd(&g_prof[9], pk_pass[1]);
+      pk_pass[0] = pk_pass[1] = 0;
       atomicAdd(&g_prof[15], (unsigned long long)children);
     }
 #endif

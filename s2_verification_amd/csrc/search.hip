@@ -439,8 +439,9 @@ int batch_run(DevBatch& b, hipStream_t stream, const RunOpts& ro, RunStats& st, 
       unsigned long long gp[16];
       HIPCHK(hipMemcpyFromSymbol(gp, HIP_SYMBOL(g_prof), sizeof gp));
       const double rd = gp[13] ? (double)gp[13] : 1.0;
-      fprintf(stderr, "[s2lc prof] pack: rounds %llu children %llu | cycles/round expand %.0f closure %.0f dedupe+rest %.0f\n",
-              gp[13], gp[15], gp[10] / rd, gp[11] / rd, gp[12] / rd);
+      fprintf(stderr, "[s2lc prof] pack: rounds %llu children %llu | cycles/round expand %.0f closure %.0f dedupe+rest %.0f"
+              " | closure passes/round %.2f, of which with a window reload %.2f\n",
+              gp[13], gp[15], gp[10] / rd, gp[11] / rd, gp[12] / rd, gp[8] / rd, gp[9] / rd);
     }
 #endif
     // histories that outgrew the packed frontier go on to the workgroup passes
