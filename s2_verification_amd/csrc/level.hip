@@ -238,6 +238,11 @@ int level_search(DevBatch& b, uint32_t h, hipStream_t st, const RunOpts& ro, int
   pq.max_rounds = 4096;
   pq.nf_max = persist_nf;
   pq.solo = getenv("S2LC_NO_SOLO") ? 0u : 1u;  // S2LC_NO_SOLO=1: one-configuration rounds on the grid too
+  // wide rounds: stage every child, then lv_insert dedupes (plain stores,
+  // combined in L2); S2LC_WIDE_FUSED=1: lv_round inserts as it expands (CAS
+  // first, so a duplicate is never written; measured slower on C5 / C5wide:
+  // its write-through stores cost more HBM writes than the duplicates do)
+  const uint32_t fused_wide = getenv("S2LC_WIDE_FUSED") ? 1u : 0u;
   {
     int dev = 0, khz = 100000;
     LVCHK(hipGetDevice(&dev));
@@ -307,6 +312,7 @@ int level_search(DevBatch& b, uint32_t h, hipStream_t st, const RunOpts& ro, int
       // with the grid (~11 ns each), so narrow rounds use a small grid
       const uint32_t g_ins = narrow ? std::min<uint32_t>(L.grid_insert, 128) : L.grid_insert;
       p.f0 = 0; p.f1 = LV_NONE; p.clear_slots = 1;
+      p.fused = fused_wide;
       for (uint32_t k = 0; k < batch; ++k) {
         set_round(next_round + k);
         p.publish_always = k + 1 == batch;  // the host reads the state after the batch
@@ -331,6 +337,7 @@ int level_search(DevBatch& b, uint32_t h, hipStream_t st, const RunOpts& ro, int
       LVCHK(hipMemsetAsync(p.ht, 0xFF, ht_bytes, st));
       p.clear_slots = 0;  // a chunk must not break the probe chains of earlier chunks' entries
       p.close_round = 0;
+      p.fused = 0;        // (a chunk that overflows is re-run: its children must not be in the table yet)
       uint32_t f0 = 0, chunk = nf;
       LvCtl* hc = reinterpret_cast<LvCtl*>(L.h_ctl);
       LvCtl snap;  // the counters before the current chunk (restored when it overflows)

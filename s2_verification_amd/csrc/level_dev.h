@@ -140,6 +140,7 @@ struct LvParams {
   LvRun* run;            // device run state
   LvRun* publish;        // host-mapped mirror of *run (the last lv_insert block copies it)
   uint32_t close_round;  // lv_insert's last block closes the round (0: a chunk of a host-driven round)
+  uint32_t fused;        // lv_round inserts its children itself (lv_stage_insert); lv_insert only closes
   uint32_t publish_always;  // publish the run state after this round (else only when the search ends)
   uint32_t* rcounts;     // per-round unique configurations (nullable)
   TraceEnt* trace;
@@ -493,6 +494,21 @@ __device__ __forceinline__ uint32_t lv_slices(uint32_t K, uint32_t nf, uint32_t 
   return max(1u, min(c_est + (c_est >> 2) + 1, (2u * nwaves + nf - 1) / max(nf, 1u)));
 }
 
+// A configuration's counters (lane l holds chains l + 64 q) with 8-byte
+// write-through stores: lanes l = 0 mod 4 store chains l .. l+3 of each slot
+// (a 2-byte write-through store per lane costs a memory write per request).
+template <int NQ>
+__device__ __forceinline__ void lv_store_cnt_wt(uint16_t* dst, const uint32_t (&cnt)[NQ], const uint32_t (&d)[NQ]) {
+  const int lane = (int)(threadIdx.x & 63);
+#pragma unroll
+  for (int q = 0; q < NQ; ++q) {
+    const uint32_t v = (cnt[q] + d[q]) & 0xFFFFu;
+    const uint32_t p2 = v | ((uint32_t)__shfl_xor((int)v, 1, 64) << 16);  // chains l, l+1 (l even)
+    const uint32_t o2 = (uint32_t)__shfl_xor((int)p2, 2, 64);              // chains l+2, l+3
+    if ((lane & 3) == 0) st_wt64(dst + 64 * q + lane, ((unsigned long long)o2 << 32) | p2);
+  }
+}
+
 // Persistent kernel: stage one closed child with write-through stores and
 // insert it at once (the producing wave deduplicates its own child: a 64-bit
 // CAS, and on a tag hit a wave-parallel compare against the resident entry).
@@ -516,21 +532,11 @@ __device__ __forceinline__ void lv_stage_insert(const LvParams& p, const LvRound
   }
   const uint32_t k = st * p.scs + i;
   LCfg<NQ>* o = lv_cfg<NQ>(p.stg, k);
-  // the header line: lanes 0..15 store one 8-byte word each (one whole-line store)
-  const unsigned long long w = lane == 0 ? s.tail
-                             : lane == 1 ? s.hash
-                             : lane == 2 ? fp
-                             : lane == 3 ? ((unsigned long long)minret << 32 | s.tok)
-                             : lane == 4 ? ((unsigned long long)move << 32 | ptrace)
-                             : lane == 5 ? ((unsigned long long)LV_NONE << 32 | TRACE_NONE)
-                                         : 0ull;
-  if (lane < 16) st_wt64(reinterpret_cast<unsigned long long*>(o) + lane, w);
-#pragma unroll
-  for (int q = 0; q < NQ; ++q) st_wt16(&o->cnt[lane + 64 * q], (uint16_t)(cnt[q] + d[q]));
-  // The CAS goes out with the stores: the entry is published PENDING (bit 31
-  // of the index) and made final once this wave's stores have landed. A wave
-  // that meets a pending entry with its tag waits for the final form before
-  // it reads the configuration. A duplicate never waits for its own stores.
+  // The CAS goes first: the entry is published PENDING (bit 31 of the index)
+  // and made final once the winner's stores have landed, so a duplicate writes
+  // nothing at all (wide rounds stage several copies of most configurations).
+  // A wave that meets a pending entry with its tag waits for the final form
+  // before it reads the configuration.
   const uint32_t tag = (uint32_t)(fp >> 32);
   const unsigned long long mine = ((unsigned long long)tag << 32) | k;
   uint32_t slot = (uint32_t)fp & p.ht_mask;
@@ -555,21 +561,28 @@ __device__ __forceinline__ void lv_stage_insert(const LvParams& p, const LvRound
     }
     slot = (slot + 1) & p.ht_mask;
   }
-  // the winner: its stores land, then the entry loses its PENDING bit
-  lv_drain();
-  if (lane == 0) atomicExch(&p.ht[slot], mine);
-  // next-frontier position, table slot, trace entry
+  // the winner: next-frontier position, then the configuration (header line:
+  // lanes 0..15 store one 8-byte word each, one whole-line store), its index
+  // and trace entry; its stores land, then the entry loses its PENDING bit
   uint32_t n = 0;
   if (lane == 0) n = atomicAdd(&p.ctl->nnext, 1u);
   n = rl(n, 0);
+  const uint32_t tr = in.wit ? p.tgid + in.tbase + n : TRACE_NONE;
+  const unsigned long long w = lane == 0 ? s.tail
+                             : lane == 1 ? s.hash
+                             : lane == 2 ? fp
+                             : lane == 3 ? ((unsigned long long)minret << 32 | s.tok)
+                             : lane == 4 ? ((unsigned long long)move << 32 | ptrace)
+                             : lane == 5 ? ((unsigned long long)slot << 32 | tr)
+                                         : 0ull;
+  if (lane < 16) st_wt64(reinterpret_cast<unsigned long long*>(o) + lane, w);
+  lv_store_cnt_wt<NQ>(o->cnt, cnt, d);
   if (lane == 0) {
     st_wt32(&p.nxt_idx[n], k);
-    st_wt32(&o->slot, slot);
-    if (in.wit) {
-      st_wt32(&o->trace, p.tgid + in.tbase + n);
-      p.trace[in.tbase + n] = TraceEnt{ptrace, move};
-    }
+    if (in.wit) p.trace[in.tbase + n] = TraceEnt{ptrace, move};
   }
+  lv_drain();
+  if (lane == 0) atomicExch(&p.ht[slot], mine);
 }
 
 // ---- solo rounds: a frontier of ONE configuration ---------------------------
@@ -655,8 +668,7 @@ __device__ __forceinline__ void lv_solo_put(const LvParams& p, uint32_t k, const
                              : lane == 5 ? ((unsigned long long)LV_NONE << 32 | tr)
                                          : 0ull;
   if (lane < 16) st_wt64(reinterpret_cast<unsigned long long*>(o) + lane, w);
-#pragma unroll
-  for (int q = 0; q < NQ; ++q) st_wt16(&o->cnt[lane + 64 * q], (uint16_t)(cnt[q] + d[q]));
+  lv_store_cnt_wt<NQ>(o->cnt, cnt, d);
   if (lane == 0) {
     st_wt32(&p.nxt_idx[k], k);
     if (wit) p.trace[tbase + k] = TraceEnt{ptrace, move};
@@ -1028,9 +1040,15 @@ __global__ __launch_bounds__(LV_BLOCK) void lv_round(LvParams p) {
   if (p.init) in.nf = 1;
   const uint32_t nwaves = gridDim.x * (LV_BLOCK / 64);
   in.S = p.init ? 1u : lv_slices(p.K, in.nf, nwaves, p.run ? p.run->last_nf : 0u, p.run ? p.run->last_closed : 0ull);
-  in.tbase = 0;
-  in.wit = 0;
-  lv_expand<NQ, 0>(p, in, s_heads[threadIdx.x >> 6], s_cs);
+  if (p.fused) {
+    in.tbase = (uint32_t)p.run->tnext;
+    in.wit = p.run->witness;
+    lv_expand<NQ, 1>(p, in, s_heads[threadIdx.x >> 6], s_cs);
+  } else {
+    in.tbase = 0;
+    in.wit = 0;
+    lv_expand<NQ, 0>(p, in, s_heads[threadIdx.x >> 6], s_cs);
+  }
 }
 
 template <int NQ>
@@ -1130,7 +1148,9 @@ __global__ __launch_bounds__(LV_BLOCK) void lv_insert(LvParams p) {
   const bool wit = p.run ? p.run->witness != 0 : p.witness_host != 0;
   const uint32_t tbase = p.run ? (uint32_t)p.run->tnext : p.tbase_host;
   uint32_t lo = 0, hi = 0;  // this lane's stripe range (striped mode)
-  if (p.dense) {
+  if (p.fused) {
+    // lv_round inserted the children itself: only the round's close is left
+  } else if (p.dense) {
     hi = p.dense;
   } else if (!ld_agent(&p.ctl->overflow)) {
     lo = p.ctl->lo[lane];

@@ -180,9 +180,11 @@ def test_round_counts_match_reduced_search(engine, abl):
 
 # level-search round modes: narrow rounds inside the persistent kernel, with
 # one-configuration rounds as solo rounds of workgroup 0 (default) or on the
-# grid (no_solo), host-enqueued lv_round / lv_insert only, or every round
-# inside the persistent kernel (fused stage-and-insert also on wide frontiers)
+# grid (no_solo), host-enqueued rounds only (lv_round staging everything for
+# lv_insert, or inserting as it expands: wide_fused), or every round inside
+# the persistent kernel
 LEVEL_MODES = {"default": {}, "no_solo": {"S2LC_NO_SOLO": "1"}, "no_persist": {"S2LC_NO_PERSIST": "1"},
+               "wide_fused": {"S2LC_WIDE_FUSED": "1", "S2LC_NO_PERSIST": "1"},
                "all_persist": {"S2LC_PERSIST_NF": "4294967295"}}
 
 
@@ -213,13 +215,13 @@ def test_hard_round_counts(name, off, mode, monkeypatch):
     assert got == want["counts"], (name, off, mode, bad[:5])
     if r.verdict == s2.Ok:
         assert r.witness is not None
-    if mode == "no_persist":
+    if mode in ("no_persist", "wide_fused"):
         assert st["level_persist_rounds"] == 0, st
     else:
         assert st["level_persist_rounds"] > 0, st
     if mode == "all_persist":
         assert st["level_persist_rounds"] == r.rounds, st
-    if mode in ("no_solo", "no_persist"):
+    if mode in ("no_solo", "no_persist", "wide_fused"):
         assert st["level_solo_rounds"] == 0, st
     elif name != "C5wide":  # most rounds of these histories keep one configuration
         assert st["level_solo_rounds"] > r.rounds // 2, st
