@@ -1,5 +1,7 @@
 // cli.cpp — s2-porcupine: drop-in for golang/s2-porcupine/main.go:568-640.
-//   -file=<path> | -file - (stdin) | -version ; exit 0 = linearizable, 1 otherwise
+//   -file=<path> | -file - (stdin) | -version ; exit 0 = linearizable, 1 = not
+//   linearizable (or an input error), 3 = witness certification failed,
+//   4 = unknown (device capacity)
 //   stderr: slog-style JSON lines ("passed: is linearizable" /
 //   "failed: is NOT linearizable" with res), "failed to decode history: ..."
 // The check runs on the GPU through libs2lincheck (s2lc_check).
@@ -145,19 +147,26 @@ int main(int argc, char** argv) {
     }
   }
   const bool ok = r.verdict == S2LC_OK;
+  int code = 0;
   if (ok) {
     slog("INFO", "passed: is linearizable");
+  } else if (r.verdict == S2LC_ILLEGAL) {
+    // main.go:636: res is porcupine's CheckResult
+    slog("ERROR", "failed: is NOT linearizable", ",\"res\":\"Illegal\"");
+    code = 1;
   } else {
-    // main.go:636: res is porcupine's CheckResult; Unknown (a device capacity
-    // limit; the reference at timeout 0 never returns it) also names its reason
-    std::string extra = std::string(",\"res\":\"") + (r.verdict == S2LC_ILLEGAL ? "Illegal" : "Unknown") + "\"";
-    if (r.verdict == S2LC_UNKNOWN)
-      extra += std::string(",\"reason\":\"") + (r.reason == S2LC_R_FRONTIER ? "frontier exceeds device capacity" :
-                                                r.reason == S2LC_R_TIMEOUT ? "timeout" : r.reason == S2LC_R_BUDGET ? "budget" : "other") + "\"";
-    slog("ERROR", "failed: is NOT linearizable", extra);
+    // Unknown: a device capacity limit (the reference at timeout 0 never
+    // returns it). Not a verdict on the history, so neither message above and
+    // its own exit code (4): a DST script must not read it as a violation.
+    const char* why = r.reason == S2LC_R_FRONTIER ? "frontier exceeds device capacity"
+                    : r.reason == S2LC_R_TIMEOUT  ? "timeout"
+                    : r.reason == S2LC_R_BUDGET   ? "budget" : "other";
+    slog("ERROR", "failed: linearizability unknown",
+         std::string(",\"res\":\"Unknown\",\"reason\":\"") + why + "\"");
+    code = 4;
   }
   s2lc_result_free(&r);
   s2lc_destroy(ctx);
   s2lc_history_free(h);
-  return ok ? 0 : 1;
+  return code;
 }

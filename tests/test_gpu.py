@@ -147,6 +147,16 @@ def test_cli_verdicts_and_exit_codes(tmp_path):
             assert p.returncode == 0 and line["msg"] == "passed: is linearizable", (c["name"], p.stderr)
         else:
             assert p.returncode == 1 and line["msg"] == "failed: is NOT linearizable" and line["res"] == "Illegal"
+    # Unknown (a staging array too small for H174's widest rounds): its own
+    # message and exit code, never read as a violation
+    from s2_verification_amd import workloads as W
+    path = tmp_path / "h174.jsonl"
+    path.write_bytes(W.config_jsonl("H174"))
+    p = subprocess.run([s2.CLI_PATH, "-file=" + str(path)], capture_output=True, text=True, timeout=120,
+                       cwd=tmp_path, env={**os.environ, "S2LC_LEVEL_SCAP": "4096"})
+    line = json.loads(p.stderr.strip().splitlines()[-1])
+    assert p.returncode == 4 and line["msg"] == "failed: linearizability unknown", p.stderr[-400:]
+    assert line["res"] == "Unknown" and line["reason"] == "frontier exceeds device capacity"
     # stdin
     with open(os.path.join(GOLDEN, "ref_BasicNoConcurrency.jsonl"), "rb") as f:
         p = subprocess.run([s2.CLI_PATH, "-file", "-"], stdin=f, capture_output=True, timeout=120, cwd=tmp_path)
