@@ -370,9 +370,21 @@ int batch_run(DevBatch& b, hipStream_t stream, const RunOpts& ro, RunStats& st, 
   std::vector<uint32_t> todo;   // workgroup passes
   std::vector<uint32_t> level;  // device-wide level search
   const bool use_pack = engine == S2LC_ENGINE_AUTO;
+  // A few histories with 32 < K <= 128 go to the level search too: one
+  // workgroup per history (search_kernel) pays every round's latency in one
+  // workgroup, while the level search runs each round on the whole device
+  // (H96: 182 ms against 14 ms); a batch of many of them keeps the workgroup
+  // engine, which checks them side by side. S2LC_MIDK_LEVEL_MAX overrides
+  // the count (default 8).
+  uint32_t midk_level_max = 8;
+  if (const char* e = getenv("S2LC_MIDK_LEVEL_MAX")) midk_level_max = (uint32_t)strtoul(e, nullptr, 10);
+  uint32_t n_midk = 0;
+  for (uint32_t i : b.lpt)
+    if (b.h_hist[i].K > 32 && b.h_hist[i].K <= 128) ++n_midk;
+  const bool midk_level = engine == S2LC_ENGINE_AUTO && n_midk <= midk_level_max;
   for (uint32_t i : b.lpt) {
     const uint32_t K = b.h_hist[i].K;
-    if (engine == S2LC_ENGINE_LEVEL || K > 128) level.push_back(i);
+    if (engine == S2LC_ENGINE_LEVEL || K > 128 || (midk_level && K > 32)) level.push_back(i);
     else if (!use_pack || K > 32) todo.push_back(i);
   }
   // histories settled by pack_kernel<8> / <16> (roofline accounting of those kernels)

@@ -107,20 +107,27 @@ def test_engine_c4_sample_vs_wgl(engine):
     assert all(r.witness is not None for r in res if r.verdict == s2.Ok)
 
 
+@pytest.mark.parametrize("route", ["workgroup", "auto_many", "auto_few"])
 @pytest.mark.parametrize("name", ["H48", "H48bad", "H96", "H100", "H120m"])
-def test_mid_k_histories_take_search_kernel(name):
-    """32 < K <= 128 with the collector's client-id cap: the default route is
-    the workgroup engine (search_kernel), not the packed or level kernels.
-    Porcupine's DFS does not finish; verdict = the CPU reduced search."""
+def test_mid_k_histories(name, route, monkeypatch):
+    """32 < K <= 128 with the collector's client-id cap. The workgroup engine
+    (search_kernel) forced, the default route of a batch with many of them
+    (search_kernel: S2LC_MIDK_LEVEL_MAX=0 here), and of a batch with a few
+    (the level search). Porcupine's DFS does not finish; verdict = the CPU
+    reduced search."""
     from s2_verification_amd import workloads as W
     h = W.config_history(name)
     K = h.info()["n_chains"]
     assert 32 < K <= 128
-    v, _ = orc.check_reduced(orc.from_s2lc_numpy(h.events_numpy()))
-    b, res = run(checker_for(), [h])
+    v, _ = orc.check_reduced(orc.from_s2lc_numpy(h.events_numpy(), owner=h))
+    if route == "auto_many":
+        monkeypatch.setenv("S2LC_MIDK_LEVEL_MAX", "0")
+    ck = checker_for(s2.ENGINE_WORKGROUP) if route == "workgroup" else s2.Checker()
+    b, res = run(ck, [h])
     r = res[0]
     st = b.stats()
-    assert st["pack8_histories"] == 0 and st["pack16_histories"] == 0 and st["level_histories"] == 0, st
+    assert st["pack8_histories"] == 0 and st["pack16_histories"] == 0, st
+    assert st["level_histories"] == (1 if route == "auto_few" else 0), st
     assert r.verdict == v, (name, r)
     if r.verdict == s2.Ok:
         assert r.witness is not None and len(r.witness) == h.info()["n_ops"]
