@@ -563,7 +563,7 @@ int batch_run(DevBatch& b, hipStream_t stream, const RunOpts& ro, RunStats& st, 
   // for what the other passes settled (walk_kernel skips walked histories)
   const bool other_work = n_passes_run > 0 || !todo.empty() || !use_pack;
   if (witness && b.n_hist && other_work) {
-    hipLaunchKernelGGL(walk_kernel, dim3((b.n_hist + 255) / 256), dim3(256), 0, stream, b.n_hist, b.res,
+    hipLaunchKernelGGL(walk_kernel, dim3((b.n_hist + 3) / 4), dim3(256), 0, stream, b.n_hist, b.res,
                        (const TraceEnt*)b.trace, b.moves);
     HIPCHK(hipGetLastError());
   }

@@ -723,16 +723,23 @@ __global__ __launch_bounds__(BT) void search_kernel(Params p) {
 // and writes the move list in order. Ok: the completing move after the path
 // to its parent. Illegal: the path to a configuration of the deepest
 // non-empty round (the partial linearization the visualization shows).
+// One WAVE per history (launch: 4 waves per 256-thread block): lane i reads
+// the entry i steps below the current one, and a ballot finds how far the
+// chain runs through consecutive entries (a parent is usually the entry just
+// before its child: the level search's one-configuration rounds append one
+// entry per round), so those moves are written in one step instead of one
+// dependent load each.
 __global__ __attribute__((unused)) void walk_kernel(uint32_t n, HistResult* res, const TraceEnt* trace, uint32_t* moves) {
-  const uint32_t h = blockIdx.x * blockDim.x + threadIdx.x;
+  const uint32_t h = blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
+  const uint32_t lane = threadIdx.x & 63;
   if (h >= n) return;
-  HistResult r = res[h];
+  const HistResult r = res[h];
   if (r.has_witness != 2u) return;
   uint32_t* out = moves + r.witness_off;
   uint32_t len, pos, idx;
   if (r.verdict == V_OK) {
     len = (r.final_move == TRACE_NONE) ? 0u : r.rounds;
-    if (len) out[len - 1] = r.final_move;
+    if (len && lane == 0) out[len - 1] = r.final_move;
     pos = len ? len - 1 : 0;
     idx = r.final_parent;
   } else {
@@ -741,13 +748,27 @@ __global__ __attribute__((unused)) void walk_kernel(uint32_t n, HistResult* res,
     idx = r.deep_trace;
   }
   while (pos > 0 && idx != TRACE_NONE) {
-    const TraceEnt e = trace[idx];
-    out[--pos] = e.move;
-    idx = e.parent;
+    const uint32_t my = idx - lane;
+    const bool valid = lane <= idx && lane < pos;
+    TraceEnt e{TRACE_NONE, TRACE_NONE};
+    if (valid) e = trace[my];
+    // lane i's entry ends the consecutive run when its parent is elsewhere
+    const bool brk = !valid || e.parent == TRACE_NONE || e.parent != my - 1;
+    const unsigned long long bm = __ballot(brk);
+    // the run ends at the first breaking lane (all 64 lanes consecutive: lane 63)
+    const uint32_t last = bm ? (uint32_t)__ffsll(bm) - 1 : 63u;
+    const bool last_valid = __shfl((int)valid, (int)last, 64) != 0;
+    const uint32_t cnt = last_valid ? last + 1 : last;
+    if (lane < cnt) out[pos - 1 - lane] = e.move;
+    const uint32_t nidx = (uint32_t)__shfl((int)e.parent, (int)last, 64);
+    pos -= cnt;
+    idx = last_valid ? nidx : TRACE_NONE;
   }
-  const bool ok = pos == 0;
-  res[h].witness_len = ok ? len : 0u;
-  res[h].has_witness = ok ? 1u : 0u;
+  if (lane == 0) {
+    const bool ok = pos == 0;
+    res[h].witness_len = ok ? len : 0u;
+    res[h].has_witness = ok ? 1u : 0u;
+  }
 }
 
 }  // namespace
