@@ -125,3 +125,22 @@ def test_reduced_p2_only_prunes():
         if on["verdict"] == "Ok":
             assert on["rounds"] == off["rounds"]
         assert all(a <= b for a, b in zip(on["counts"], off["counts"]))
+
+
+def test_from_s2lc_numpy_owns_its_hashes():
+    """Without the owning history, the oracle's event array copies the record
+    hashes: checking it after the history is gone gives the same verdict and
+    search as with the history alive (a use-after-free before the copy)."""
+    import gc
+
+    from s2_verification_amd import workloads as W
+    h = W.c4_histories(1, first_seed=4007)[0]
+    with_owner = orc.from_s2lc_numpy(h.events_numpy(), owner=h)
+    v1, st1 = orc.check_reduced(with_owner, round_counts=True)
+    ea = orc.from_s2lc_numpy(h.events_numpy())
+    del h, with_owner
+    gc.collect()
+    junk = [bytearray(1 << 16) for _ in range(64)]  # reuse the freed memory
+    v2, st2 = orc.check_reduced(ea, round_counts=True)
+    assert (v1, st1["round_counts"]) == (v2, st2["round_counts"])
+    del junk
