@@ -290,6 +290,11 @@ typedef struct s2lc_batch_stats {
   uint64_t pack8_algo_bytes;
   uint32_t pack8_histories;
   uint32_t _pad3;
+  /* level searches restarted with host-driven rounds because a persistent
+   * launch was refused or its grid barrier timed out (a workgroup never became
+   * resident: another process holding CUs). Not an error: same verdict. */
+  uint32_t level_persist_fallbacks;
+  uint32_t _pad4;
 } s2lc_batch_stats;
 int s2lc_batch_stats_get(const s2lc_batch* b, s2lc_batch_stats* out);
 /* With S2LC_F_ROUND_COUNTS: the unique-configuration count of each completed

@@ -108,7 +108,8 @@ class c_batch_stats(ctypes.Structure):
                 ("level_persist_rounds", ctypes.c_uint64), ("level_persist_launches", ctypes.c_uint32),
                 ("level_chunk_retries", ctypes.c_uint32), ("level_syncs", ctypes.c_uint32), ("level_solo_rounds", ctypes.c_uint32),
                 ("n_ops_total", ctypes.c_uint64), ("pack8_ms", ctypes.c_double),
-                ("pack8_algo_bytes", ctypes.c_uint64), ("pack8_histories", ctypes.c_uint32), ("_pad3", ctypes.c_uint32)]
+                ("pack8_algo_bytes", ctypes.c_uint64), ("pack8_histories", ctypes.c_uint32), ("_pad3", ctypes.c_uint32),
+                ("level_persist_fallbacks", ctypes.c_uint32), ("_pad4", ctypes.c_uint32)]
 
 
 class c_sim_params(ctypes.Structure):

@@ -634,6 +634,7 @@ int s2lc_batch_stats_get(const s2lc_batch* b, s2lc_batch_stats* out) {
   out->pack8_ms = b->stats.pack8_ms;
   out->pack8_algo_bytes = b->stats.pack8_algo_bytes;
   out->pack8_histories = b->stats.pack8_histories;
+  out->level_persist_fallbacks = b->stats.level.persist_fallbacks;
   return 0;
 }
 

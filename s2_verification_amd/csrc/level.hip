@@ -59,22 +59,35 @@ hipError_t lv_launch(int which, uint32_t grid, const LvParams& p, hipStream_t st
   return hipGetLastError();
 }
 
+// lv_persist's grid barrier needs every workgroup resident at once. A
+// cooperative launch guarantees that or is refused before any work runs
+// (hipErrorCooperativeLaunchTooLarge); a plain launch (devices without
+// cooperative launches) relies on the occupancy query, and a workgroup that
+// never becomes resident ends in the barrier's time-out (LVR_ABORT). Either
+// way the caller goes on with host-driven rounds: neither is an error.
 template <int NQ>
-hipError_t lv_persist_t(uint32_t grid, const LvParams& p, const LvPersist& q, hipStream_t st) {
+hipError_t lv_persist_t(uint32_t grid, const LvParams& p, const LvPersist& q, bool coop, hipStream_t st) {
+  if (coop) {
+    LvParams pp = p;
+    LvPersist qq = q;
+    void* args[] = {&pp, &qq};
+    return hipLaunchCooperativeKernel(reinterpret_cast<const void*>(lv_persist<NQ>), dim3(grid), dim3(LV_BLOCK), args, 0, st);
+  }
   hipLaunchKernelGGL(lv_persist<NQ>, dim3(grid), dim3(LV_BLOCK), 0, st, p, q);
   return hipGetLastError();
 }
 
-hipError_t lv_persist_launch(uint32_t nq, uint32_t grid, const LvParams& p, const LvPersist& q, hipStream_t st) {
+hipError_t lv_persist_launch(uint32_t nq, uint32_t grid, const LvParams& p, const LvPersist& q, bool coop,
+                             hipStream_t st) {
   switch (nq) {
-    case 1: return lv_persist_t<1>(grid, p, q, st);
-    case 2: return lv_persist_t<2>(grid, p, q, st);
-    case 3: return lv_persist_t<3>(grid, p, q, st);
-    case 4: return lv_persist_t<4>(grid, p, q, st);
-    case 5: return lv_persist_t<5>(grid, p, q, st);
-    case 6: return lv_persist_t<6>(grid, p, q, st);
-    case 7: return lv_persist_t<7>(grid, p, q, st);
-    default: return lv_persist_t<8>(grid, p, q, st);
+    case 1: return lv_persist_t<1>(grid, p, q, coop, st);
+    case 2: return lv_persist_t<2>(grid, p, q, coop, st);
+    case 3: return lv_persist_t<3>(grid, p, q, coop, st);
+    case 4: return lv_persist_t<4>(grid, p, q, coop, st);
+    case 5: return lv_persist_t<5>(grid, p, q, coop, st);
+    case 6: return lv_persist_t<6>(grid, p, q, coop, st);
+    case 7: return lv_persist_t<7>(grid, p, q, coop, st);
+    default: return lv_persist_t<8>(grid, p, q, coop, st);
   }
 }
 
@@ -124,6 +137,10 @@ int lv_grids_t(LevelBufs& L, std::string& err) {
   // the API can over-report by one block per CU)
   L.grid_persist = bp >= 2 ? (uint32_t)n_cu : 0u;
   L.grid_nq = (uint32_t)NQ;
+  int dev = 0, coop = 0;
+  LVCHK(hipGetDevice(&dev));
+  (void)hipDeviceGetAttribute(&coop, hipDeviceAttributeCooperativeLaunch, dev);
+  L.coop = coop != 0 && !getenv("S2LC_PERSIST_PLAIN");  // S2LC_PERSIST_PLAIN=1: plain launches (tests)
   return 0;
 }
 
@@ -228,14 +245,16 @@ int level_search(DevBatch& b, uint32_t h, hipStream_t st, const RunOpts& ro, int
 
   // persistent narrow rounds (lv_persist): S2LC_NO_PERSIST=1 turns them off,
   // S2LC_PERSIST_NF sets the widest frontier they take (default: one wave each)
-  const bool persist_on = L.grid_persist > 0 && !getenv("S2LC_NO_PERSIST");
+  bool persist_on = L.grid_persist > 0 && !L.persist_refused && !getenv("S2LC_NO_PERSIST");
   uint32_t persist_nf = L.grid_persist * (LV_BLOCK / 64);
   if (const char* e = getenv("S2LC_PERSIST_NF")) persist_nf = (uint32_t)strtoul(e, nullptr, 10);
   LvPersist pq;
   memset(&pq, 0, sizeof pq);
   pq.ctl3 = ctl; pq.bar = reinterpret_cast<LvBar*>(L.bar);
   for (int i = 0; i < 2; ++i) { pq.stg[i] = L.stg[i]; pq.idx[i] = L.idx[i]; pq.ht[i] = L.ht[i]; }
-  pq.max_rounds = 4096;
+  // rounds per launch: the host checks the deadline between launches, so a
+  // search with a deadline takes shorter launches (~1 ms of narrow rounds)
+  pq.max_rounds = deadline_ns ? 128 : 4096;
   pq.nf_max = persist_nf;
   pq.solo = getenv("S2LC_NO_SOLO") ? 0u : 1u;  // S2LC_NO_SOLO=1: one-configuration rounds on the grid too
   // wide rounds: stage every child, then lv_insert dedupes (plain stores,
@@ -247,7 +266,11 @@ int level_search(DevBatch& b, uint32_t h, hipStream_t st, const RunOpts& ro, int
     int dev = 0, khz = 100000;
     LVCHK(hipGetDevice(&dev));
     (void)hipDeviceGetAttribute(&khz, hipDeviceAttributeWallClockRate, dev);
-    pq.spin_ticks = (unsigned long long)khz * 2000ull;  // a barrier wait above 2 s means a block is not resident
+    // a barrier wait above 2 s means a workgroup is not resident (plain launches;
+    // S2LC_PERSIST_SPIN_US: a shorter limit, for the fallback's tests)
+    unsigned long long us_ = 2000000;
+    if (const char* e = getenv("S2LC_PERSIST_SPIN_US")) us_ = std::max<unsigned long long>(1, strtoull(e, nullptr, 10));
+    pq.spin_ticks = std::max<unsigned long long>(1, (unsigned long long)khz * us_ / 1000);
   }
 
 #ifdef S2LC_PROF
@@ -257,12 +280,6 @@ int level_search(DevBatch& b, uint32_t h, hipStream_t st, const RunOpts& ro, int
   p.prof = d_prof;
 #endif
   LVCHK(hipEventRecord(L.ev[0], st));
-  memset(hr, 0, sizeof(LvRun));
-  LVCHK(hipMemsetAsync(L.ctl, 0, 3 * sizeof(LvCtl), st));
-  hipLaunchKernelGGL(lv_run_init, dim3(1), dim3(1), 0, st, run, tb0, wit0 ? 1u : 0u,
-                     (unsigned long long)ro.max_configs);
-  LVCHK(hipGetLastError());
-  // round 0: the closed initial configuration, staged into stg[0]
   auto set_round = [&](uint32_t r) {
     const int w = (int)(r & 1), pr = (int)((r + 1) & 1);  // round r stages into w; its frontier is in pr
     p.round = r;
@@ -271,111 +288,137 @@ int level_search(DevBatch& b, uint32_t h, hipStream_t st, const RunOpts& ro, int
     p.ht = L.ht[w]; p.ht_clear = L.ht[pr];
     p.ctl = ctl + w; p.ctl_next = ctl + pr;
   };
-  set_round(0);
-  p.init = 1; p.f0 = 0; p.f1 = 1; p.clear_slots = 0;
-  LVCHK(lv_dispatch(nq, LK_ROUND, 1, p, st));
-  LVCHK(lv_dispatch(nq, LK_INSERT, 1, p, st));
-  LVCHK(hipStreamSynchronize(st));
-  p.init = 0;
+  bool timed_out = false;
+  uint32_t syncs = 0;
+  // A search runs once; when a persistent launch is refused or its barrier
+  // times out (a workgroup never became resident: another process holding
+  // CUs) it is run again from round 0 with host-driven rounds only.
+  for (;;) {
+    bool aborted = false;
+    memset(hr, 0, sizeof(LvRun));
+    LVCHK(hipMemsetAsync(L.ctl, 0, 3 * sizeof(LvCtl), st));
+    hipLaunchKernelGGL(lv_run_init, dim3(1), dim3(1), 0, st, run, tb0, wit0 ? 1u : 0u,
+                       (unsigned long long)ro.max_configs);
+    LVCHK(hipGetLastError());
+    // round 0: the closed initial configuration, staged into stg[0]
+    set_round(0);
+    p.init = 1; p.f0 = 0; p.f1 = 1; p.clear_slots = 0; p.close_round = 1; p.fused = 0;
+    LVCHK(lv_dispatch(nq, LK_ROUND, 1, p, st));
+    LVCHK(lv_dispatch(nq, LK_INSERT, 1, p, st));
+    LVCHK(hipStreamSynchronize(st));
+    p.init = 0;
+    ++syncs;
 
-  uint32_t next_round = 1;         // first round not yet enqueued
-  uint32_t nf_last = hr->nf;        // frontier size at the last sync
-  bool timed_out = false, aborted = false;
-  bool ctl_dirty = false;           // lv_persist left the double-buffer convention of ctl behind
-  uint32_t syncs = 1;
-  while (hr->done == LVR_RUNNING) {
-    if (deadline_ns && steady_ns() > deadline_ns) { timed_out = true; break; }
-    if (persist_on && nf_last <= persist_nf) {
-      // narrow: rounds inside one resident launch until the frontier widens
-      LVCHK(hipMemsetAsync(L.bar, 0, sizeof(LvBar), st));
-      LVCHK(hipMemsetAsync(L.ctl, 0, 3 * sizeof(LvCtl), st));
-      const uint32_t r0 = next_round;
-      LVCHK(lv_persist_launch(nq, L.grid_persist, p, pq, st));
-      LVCHK(hipStreamSynchronize(st));
-      ++syncs;
-      ++ls.persist_launches;
-      if (hr->done == LVR_ABORT) { aborted = true; break; }
-      next_round = hr->round + 1;
-      ls.persist_rounds += next_round - r0 + (hr->done == LVR_OVERFLOW ? 1 : 0);
-      ctl_dirty = true;
-    } else {
-      if (ctl_dirty) {  // back from lv_persist: round r's counters must start at zero in ctl[r & 1]
+    uint32_t next_round = 1;         // first round not yet enqueued
+    uint32_t nf_last = hr->nf;        // frontier size at the last sync
+    bool ctl_dirty = false;           // lv_persist left the double-buffer convention of ctl behind
+    while (hr->done == LVR_RUNNING) {
+      if (deadline_ns && steady_ns() > deadline_ns) { timed_out = true; break; }
+      if (persist_on && nf_last <= persist_nf) {
+        // narrow: rounds inside one resident launch until the frontier widens
+        LVCHK(hipMemsetAsync(L.bar, 0, sizeof(LvBar), st));
         LVCHK(hipMemsetAsync(L.ctl, 0, 3 * sizeof(LvCtl), st));
-        ctl_dirty = false;
-      }
-      // batch length from the last known frontier; the kernels are persistent
-      // (grid = what the chip holds at once) and size their work on the device
-      const bool narrow = nf_last < 4096;
-      const uint32_t batch = narrow ? 16 : 1;
-      const uint32_t g_round = L.grid_round;
-      // lv_insert's last block closes the round: its done-counter atomics grow
-      // with the grid (~11 ns each), so narrow rounds use a small grid
-      const uint32_t g_ins = narrow ? std::min<uint32_t>(L.grid_insert, 128) : L.grid_insert;
-      p.f0 = 0; p.f1 = LV_NONE; p.clear_slots = 1;
-      p.fused = fused_wide;
-      for (uint32_t k = 0; k < batch; ++k) {
-        set_round(next_round + k);
-        p.publish_always = k + 1 == batch;  // the host reads the state after the batch
-        LVCHK(lv_dispatch(nq, LK_ROUND, g_round, p, st));
-        LVCHK(lv_dispatch(nq, LK_INSERT, g_ins, p, st));
-      }
-      p.publish_always = 1;
-      next_round += batch;
-      LVCHK(hipStreamSynchronize(st));
-      ++syncs;
-    }
-    if (hr->done == LVR_OVERFLOW) {
-      // round r overflowed the staging array: its frontier (stg[(r+1)&1]) is
-      // intact; re-run it host-driven over halves of the frontier, into a
-      // clean table (an aborted persistent round left entries behind)
-      const uint32_t r = hr->round + 1;
-      const uint32_t nf = hr->nf;
-      LvRun cont = *hr;
-      cont.done = LVR_RUNNING;
-      LVCHK(hipMemcpyAsync(run, &cont, sizeof cont, hipMemcpyHostToDevice, st));
-      set_round(r);
-      LVCHK(hipMemsetAsync(p.ht, 0xFF, ht_bytes, st));
-      p.clear_slots = 0;  // a chunk must not break the probe chains of earlier chunks' entries
-      p.close_round = 0;
-      p.fused = 0;        // (a chunk that overflows is re-run: its children must not be in the table yet)
-      uint32_t f0 = 0, chunk = nf;
-      LvCtl* hc = reinterpret_cast<LvCtl*>(L.h_ctl);
-      LvCtl snap;  // the counters before the current chunk (restored when it overflows)
-      memset(&snap, 0, sizeof snap);
-      bool stop = false;
-      while (f0 < nf) {
-        const uint32_t f1 = (uint32_t)std::min<uint64_t>(nf, (uint64_t)f0 + chunk);
-        LVCHK(hipMemcpyAsync(p.ctl, &snap, sizeof(LvCtl), hipMemcpyHostToDevice, st));
-        p.f0 = f0; p.f1 = f1;
-        LVCHK(lv_dispatch(nq, LK_ROUND, L.grid_round, p, st));
-        LVCHK(lv_dispatch(nq, LK_INSERT, L.grid_insert, p, st));
-        LVCHK(hipMemcpyAsync(hc, p.ctl, sizeof(LvCtl), hipMemcpyDeviceToHost, st));
+        const uint32_t r0 = next_round;
+        const hipError_t le = lv_persist_launch(nq, L.grid_persist, p, pq, L.coop, st);
+        if (le != hipSuccess) {  // refused before it ran (residency not available)
+          (void)hipGetLastError();
+          aborted = true;
+          break;
+        }
         LVCHK(hipStreamSynchronize(st));
         ++syncs;
-        if (hc->found) break;
-        if (hc->overflow) {
-          if (f1 - f0 == 1) { stop = true; break; }
-          chunk = std::max<uint32_t>(1, (f1 - f0) / 2);
-          ++ls.chunk_retries;
-          continue;
+        ++ls.persist_launches;
+        if (hr->done == LVR_ABORT) { aborted = true; break; }
+        next_round = hr->round + 1;
+        ls.persist_rounds += next_round - r0 + (hr->done == LVR_OVERFLOW ? 1 : 0);
+        ctl_dirty = true;
+      } else {
+        if (ctl_dirty) {  // back from lv_persist: round r's counters must start at zero in ctl[r & 1]
+          LVCHK(hipMemsetAsync(L.ctl, 0, 3 * sizeof(LvCtl), st));
+          ctl_dirty = false;
         }
-        // this chunk's staging is inserted: the next chunk inserts from here on
-        snap = *hc;
-        for (int s_ = 0; s_ < LV_STRIPES; ++s_) snap.lo[s_] = std::min(snap.cnt[16 * s_], p.scs);
-        snap.done_blocks = 0;
-        f0 = f1;
+        // batch length from the last known frontier; the kernels are persistent
+        // (grid = what the chip holds at once) and size their work on the device
+        const bool narrow = nf_last < 4096;
+        const uint32_t batch = narrow ? 16 : 1;
+        const uint32_t g_round = L.grid_round;
+        // lv_insert's last block closes the round: its done-counter atomics grow
+        // with the grid (~11 ns each), so narrow rounds use a small grid
+        const uint32_t g_ins = narrow ? std::min<uint32_t>(L.grid_insert, 128) : L.grid_insert;
+        p.f0 = 0; p.f1 = LV_NONE; p.clear_slots = 1;
+        p.fused = fused_wide;
+        for (uint32_t k = 0; k < batch; ++k) {
+          set_round(next_round + k);
+          p.publish_always = k + 1 == batch;  // the host reads the state after the batch
+          LVCHK(lv_dispatch(nq, LK_ROUND, g_round, p, st));
+          LVCHK(lv_dispatch(nq, LK_INSERT, g_ins, p, st));
+        }
+        p.publish_always = 1;
+        next_round += batch;
+        LVCHK(hipStreamSynchronize(st));
+        ++syncs;
       }
-      if (stop) break;  // hr->done stays LVR_OVERFLOW: Unknown (frontier)
-      LVCHK(lv_dispatch(nq, LK_CLOSE, 1, p, st));  // the round's bookkeeping (publishes hr)
-      // chunked rounds did not clear their frontier's table slots: reset the tables
-      for (int i = 0; i < 2; ++i) LVCHK(hipMemsetAsync(L.ht[i], 0xFF, ht_bytes, st));
-      LVCHK(hipMemsetAsync(L.ctl, 0, 3 * sizeof(LvCtl), st));
-      ctl_dirty = false;
-      LVCHK(hipStreamSynchronize(st));
-      p.close_round = 1;
-      next_round = r + 1;
+      if (hr->done == LVR_OVERFLOW) {
+        // round r overflowed the staging array: its frontier (stg[(r+1)&1]) is
+        // intact; re-run it host-driven over halves of the frontier, into a
+        // clean table (an aborted persistent round left entries behind)
+        const uint32_t r = hr->round + 1;
+        const uint32_t nf = hr->nf;
+        LvRun cont = *hr;
+        cont.done = LVR_RUNNING;
+        LVCHK(hipMemcpyAsync(run, &cont, sizeof cont, hipMemcpyHostToDevice, st));
+        set_round(r);
+        LVCHK(hipMemsetAsync(p.ht, 0xFF, ht_bytes, st));
+        p.clear_slots = 0;  // a chunk must not break the probe chains of earlier chunks' entries
+        p.close_round = 0;
+        p.fused = 0;        // (a chunk that overflows is re-run: its children must not be in the table yet)
+        uint32_t f0 = 0, chunk = nf;
+        LvCtl* hc = reinterpret_cast<LvCtl*>(L.h_ctl);
+        LvCtl snap;  // the counters before the current chunk (restored when it overflows)
+        memset(&snap, 0, sizeof snap);
+        bool stop = false;
+        while (f0 < nf) {
+          const uint32_t f1 = (uint32_t)std::min<uint64_t>(nf, (uint64_t)f0 + chunk);
+          LVCHK(hipMemcpyAsync(p.ctl, &snap, sizeof(LvCtl), hipMemcpyHostToDevice, st));
+          p.f0 = f0; p.f1 = f1;
+          LVCHK(lv_dispatch(nq, LK_ROUND, L.grid_round, p, st));
+          LVCHK(lv_dispatch(nq, LK_INSERT, L.grid_insert, p, st));
+          LVCHK(hipMemcpyAsync(hc, p.ctl, sizeof(LvCtl), hipMemcpyDeviceToHost, st));
+          LVCHK(hipStreamSynchronize(st));
+          ++syncs;
+          if (hc->found) break;
+          if (hc->overflow) {
+            if (f1 - f0 == 1) { stop = true; break; }
+            chunk = std::max<uint32_t>(1, (f1 - f0) / 2);
+            ++ls.chunk_retries;
+            continue;
+          }
+          // this chunk's staging is inserted: the next chunk inserts from here on
+          snap = *hc;
+          for (int s_ = 0; s_ < LV_STRIPES; ++s_) snap.lo[s_] = std::min(snap.cnt[16 * s_], p.scs);
+          snap.done_blocks = 0;
+          f0 = f1;
+        }
+        if (stop) break;  // hr->done stays LVR_OVERFLOW: Unknown (frontier)
+        LVCHK(lv_dispatch(nq, LK_CLOSE, 1, p, st));  // the round's bookkeeping (publishes hr)
+        // chunked rounds did not clear their frontier's table slots: reset the tables
+        for (int i = 0; i < 2; ++i) LVCHK(hipMemsetAsync(L.ht[i], 0xFF, ht_bytes, st));
+        LVCHK(hipMemsetAsync(L.ctl, 0, 3 * sizeof(LvCtl), st));
+        ctl_dirty = false;
+        LVCHK(hipStreamSynchronize(st));
+        p.close_round = 1;
+        next_round = r + 1;
+      }
+      nf_last = hr->nf;
     }
-    nf_last = hr->nf;
+    if (!aborted) break;
+    // start over, host-driven: clean tables; the round counts and trace
+    // entries of the aborted attempt are overwritten round by round
+    persist_on = false;
+    L.persist_refused = true;  // (this context's later searches too)
+    ++ls.persist_fallbacks;
+    for (int i = 0; i < 2; ++i) LVCHK(hipMemsetAsync(L.ht[i], 0xFF, ht_bytes, st));
+    LVCHK(hipStreamSynchronize(st));
   }
   LVCHK(hipEventRecord(L.ev[1], st));
   LVCHK(hipEventSynchronize(L.ev[1]));
@@ -408,12 +451,6 @@ int level_search(DevBatch& b, uint32_t h, hipStream_t st, const RunOpts& ro, int
             g[24], g[22] / (g[24] ? (double)g[24] : 1.0), g[23] / ns, g[25] / (g[24] ? (double)g[24] : 1.0));
   }
 #endif
-  if (aborted) {
-    err = "level search: a persistent-round barrier timed out (a workgroup was not resident)";
-    for (int i = 0; i < 2; ++i) (void)hipMemsetAsync(L.ht[i], 0xFF, ht_bytes, st);
-    (void)hipStreamSynchronize(st);
-    return S2LC_EHIP;
-  }
   // clear the tables for the next search
   for (int i = 0; i < 2; ++i) LVCHK(hipMemsetAsync(L.ht[i], 0xFF, ht_bytes, st));
 
@@ -513,6 +550,9 @@ int dist_create(DistLevel& d, const History* h, uint32_t rank, uint32_t world, u
 }
 
 void dist_release(DistLevel& d) {
+  if (d.snap) (void)hipFree(d.snap);
+  d.snap = nullptr;
+  d.snap_cap = 0;
   if (d.own_cnt) (void)hipFree(d.own_cnt);
   if (d.own_pos) (void)hipFree(d.own_pos);
   if (d.trace) (void)hipFree(d.trace);
@@ -687,29 +727,46 @@ int dist_local_round(DistLevel& d, uint64_t* n_next, int* found, std::string& er
 }
 
 // Replicated rounds inside lv_persist (solo rounds included), on the
-// single-GPU engine's conventions: the frontier is copied into the staging
-// array of round R0 + 1's parity, the run state starts at round R0 with this
-// rank's trace pool, and the launches run until the frontier reaches `wide`
-// configurations or the search ends. Every rank runs the same rounds on the
-// same configurations, so every rank reaches the same state. Returns
-// S2LC_EUNSUPPORTED when the persistent kernel is not available for this
-// layout (the caller runs host-driven replicated rounds instead).
+// single-GPU engine's conventions: round r reads its frontier from stg /
+// idx[(r + 1) & 1] and stages into stg / idx[r & 1]. The frontier is copied
+// contiguously into the staging array it does not live in (x), and the run
+// state starts at round R0 with R0 & 1 == x, so round R0 + 1 reads it there;
+// the launches run until the frontier reaches `wide` configurations or the
+// search ends, and the last closed round R leaves the frontier in stg /
+// idx[R & 1]. Every rank runs the same rounds on the same configurations, so
+// every rank reaches the same state. Returns S2LC_EUNSUPPORTED when the
+// persistent kernel is not available for this layout, or when a launch was
+// refused or its barrier timed out: then the frontier is restored and the
+// caller runs host-driven replicated rounds (dist_local_round) instead.
 int dist_local_run(DistLevel& d, uint32_t wide, uint64_t* n_next, int* found, uint32_t* rounds, std::string& err) {
   LevelBufs& L = d.b.lv;
   *rounds = 0;
   *found = 0;
-  if (!L.grid_persist || d.round == 0 || wide < 2) { err = "persistent replicated rounds unavailable"; return S2LC_EUNSUPPORTED; }
+  if (!L.grid_persist || L.persist_refused || d.round == 0 || wide < 2) {
+    err = "persistent replicated rounds unavailable";
+    return S2LC_EUNSUPPORTED;
+  }
   hipStream_t st = d.stream;
   const size_t ht_bytes = ((size_t)L.ht_mask + 1) * 8;
-  // the frontier, contiguous, into the staging array it does not live in
+  // the frontier, contiguous, into the staging array it does not live in, and
+  // into the snapshot (the persistent rounds overwrite both staging arrays)
   const int x = d.cur == L.stg[0] ? 1 : 0;
-  const uint32_t R0 = 3u - (uint32_t)x;  // (R0 + 1) & 1 == x
+  const uint32_t R0 = 2u + (uint32_t)x;  // R0 & 1 == x: round R0 + 1 reads stg / idx[x]
   LvParams p = dist_params(d);
   p.f1 = d.nf;
   p.send = L.stg[x];
+  const size_t fb = (size_t)d.nf * d.cb;
+  if (fb > d.snap_cap) {
+    if (d.snap) (void)hipFree(d.snap);
+    d.snap = nullptr;
+    d.snap_cap = 0;
+    LVCHK(hipMalloc(&d.snap, fb));
+    d.snap_cap = fb;
+  }
   if (d.nf) {
     const uint64_t pieces = (uint64_t)d.nf * (d.cb / 16);
     LVCHK(lv_dispatch(d.nq, LK_GATHER, (uint32_t)std::min<uint64_t>(2048, (pieces + LV_BLOCK - 1) / LV_BLOCK), p, st));
+    LVCHK(hipMemcpyAsync(d.snap, L.stg[x], fb, hipMemcpyDeviceToDevice, st));
     hipLaunchKernelGGL(lv_iota, dim3((uint32_t)std::min<uint64_t>(1024, (d.nf + 255) / 256)), dim3(256), 0, st, L.idx[x], d.nf);
     LVCHK(hipGetLastError());
   }
@@ -736,25 +793,47 @@ int dist_local_run(DistLevel& d, uint32_t wide, uint64_t* n_next, int* found, ui
     int dev = 0, khz = 100000;
     LVCHK(hipGetDevice(&dev));
     (void)hipDeviceGetAttribute(&khz, hipDeviceAttributeWallClockRate, dev);
-    pq.spin_ticks = (unsigned long long)khz * 2000ull;
+    unsigned long long us_ = 2000000;
+    if (const char* e = getenv("S2LC_PERSIST_SPIN_US")) us_ = std::max<unsigned long long>(1, strtoull(e, nullptr, 10));
+    pq.spin_ticks = std::max<unsigned long long>(1, (unsigned long long)khz * us_ / 1000);
   }
   LVCHK(hipEventRecord(L.ev[0], st));
   memset(hr, 0, sizeof(LvRun));
+  bool aborted = false;
   for (;;) {
     LVCHK(hipMemsetAsync(L.bar, 0, sizeof(LvBar), st));
     LVCHK(hipMemsetAsync(L.ctl, 0, 3 * sizeof(LvCtl), st));
-    LVCHK(lv_persist_launch(d.nq, L.grid_persist, p, pq, st));
+    if (lv_persist_launch(d.nq, L.grid_persist, p, pq, L.coop, st) != hipSuccess) {
+      (void)hipGetLastError();
+      aborted = true;
+      break;
+    }
     LVCHK(hipStreamSynchronize(st));
+    if (hr->done == LVR_ABORT) { aborted = true; break; }
     if (hr->done != LVR_RUNNING || hr->nf >= wide) break;
   }
   LVCHK(hipEventRecord(L.ev[1], st));
-  LVCHK(hipMemsetAsync(L.ht[0], 0xFF, ht_bytes, st));  // the dist rounds insert into ht[0]: no stale entries
+  for (int i = 0; i < 2; ++i) LVCHK(hipMemsetAsync(L.ht[i], 0xFF, ht_bytes, st));  // the dist rounds insert into ht[0]
   LVCHK(hipStreamSynchronize(st));
   float ms = 0;
   LVCHK(hipEventElapsedTime(&ms, L.ev[0], L.ev[1]));
   d.ms += ms;
+  if (aborted) {
+    // the frontier from the snapshot, as a caller-side buffer (no staging
+    // array: the host-driven rounds stage into stg[0] and index into idx[1]);
+    // trace entries from d.tnext on are overwritten by those rounds
+    L.persist_refused = true;
+    if (d.nf) {
+      hipLaunchKernelGGL(lv_iota, dim3((uint32_t)std::min<uint64_t>(1024, (d.nf + 255) / 256)), dim3(256), 0, st, L.idx[0], d.nf);
+      LVCHK(hipGetLastError());
+    }
+    LVCHK(hipStreamSynchronize(st));
+    d.cur = d.snap;
+    d.cur_sel = 0;
+    err = "persistent replicated rounds refused or timed out: host-driven rounds";
+    return S2LC_EUNSUPPORTED;
+  }
   const LvRun fin = *hr;
-  if (fin.done == LVR_ABORT) { err = "replicated rounds: a persistent-round barrier timed out"; return S2LC_EHIP; }
   if (fin.done == LVR_OVERFLOW) { err = "replicated round exceeds the device buffers"; return S2LC_ENOMEM; }
   d.children += fin.children;
   d.configs += fin.configs;
@@ -769,7 +848,7 @@ int dist_local_run(DistLevel& d, uint32_t wide, uint64_t* n_next, int* found, ui
     return 0;
   }
   if (fin.done == LVR_EMPTY) { d.nf = 0; *n_next = 0; return 0; }
-  d.cur_sel = (int)((fin.round + 1) & 1);
+  d.cur_sel = (int)(fin.round & 1);  // the last closed round's staging and index list
   d.cur = L.stg[d.cur_sel];
   d.nf = fin.nf;
   *n_next = fin.nf;

@@ -1253,7 +1253,7 @@ struct LvBar {
 };
 
 struct LvPersist {
-  LvCtl* ctl3;                // round r counts in ctl3[r % 3]
+  LvCtl* ctl3;                // round r counts in ctl3[(r + co) % 3] (co: lv_persist)
   LvBar* bar;
   uint8_t* stg[2];            // round r stages into stg[r & 1]; its frontier is stg[(r + 1) & 1]
   uint32_t* idx[2];
@@ -1514,6 +1514,9 @@ __global__ __launch_bounds__(LV_BLOCK) void lv_persist(LvParams p, LvPersist q) 
   unsigned long long t_round = wall_clock64();
 #endif
   uint32_t it = 0, ep = 0;  // rounds run by this launch, barrier epochs
+  // grid round r counts in ctl3[(r + co) % 3]; co changes only across a solo
+  // phase (the same on every workgroup: it follows from the run state)
+  uint32_t co = 0;
   while (ok) {
     const uint32_t r_before = s_run.round;
     // solo rounds for NQ <= 5 (K <= 320): wider layouts would lose the second
@@ -1522,9 +1525,11 @@ __global__ __launch_bounds__(LV_BLOCK) void lv_persist(LvParams p, LvPersist q) 
       if (blockIdx.x == 0) {
         if constexpr (NQ <= 5) lv_solo_rounds<NQ>(p, q, s_run, s_heads[0], &s_heads[1],
                                                    reinterpret_cast<OpRec*>(&s_heads[2]), s_cs, s_solo, max(1u, q.max_rounds - it));
-        // the next grid round's counters start at zero; the other workgroups
-        // take the run state from here after the barrier
-        uint32_t* z = reinterpret_cast<uint32_t*>(q.ctl3 + ((s_run.round + 1) % 3));
+        // the next grid round's counters start at zero: the slot after
+        // r_before's, never r_before's own (a workgroup that left round
+        // r_before's barrier late may still be reading it: ADVICE r2); the
+        // other workgroups take the run state from here after the barrier
+        uint32_t* z = reinterpret_cast<uint32_t*>(q.ctl3 + (r_before + co + 1) % 3);
         for (uint32_t i = threadIdx.x; i < sizeof(LvCtl) / 4; i += LV_BLOCK) st_wt32(z + i, 0u);
         if (threadIdx.x < sizeof(LvRun) / 4)
           st_wt32(reinterpret_cast<uint32_t*>(p.run) + threadIdx.x, reinterpret_cast<const uint32_t*>(&s_run)[threadIdx.x]);
@@ -1534,6 +1539,8 @@ __global__ __launch_bounds__(LV_BLOCK) void lv_persist(LvParams p, LvPersist q) 
         reinterpret_cast<uint32_t*>(&s_run)[threadIdx.x] = ld_agent(reinterpret_cast<const uint32_t*>(p.run) + threadIdx.x);
       if (!ok && threadIdx.x == 0) s_run.done = LVR_ABORT;
       __syncthreads();
+      // round s_run.round + 1 counts in slot (r_before + co + 1) % 3 (zeroed above)
+      co = (r_before + co + 1 + 3 * 3 - (s_run.round + 1) % 3) % 3;
 #ifdef S2LC_PROF
       t_round = wall_clock64();  // (the grid rounds' timing excludes the solo phases)
 #endif
@@ -1547,11 +1554,11 @@ __global__ __launch_bounds__(LV_BLOCK) void lv_persist(LvParams p, LvPersist q) 
     rp.cur = q.stg[(r + 1) & 1]; rp.cur_idx = q.idx[(r + 1) & 1];
     rp.stg = q.stg[r & 1]; rp.nxt_idx = q.idx[r & 1];
     rp.ht = q.ht[r & 1]; rp.ht_clear = q.ht[(r + 1) & 1];
-    rp.ctl = q.ctl3 + (r % 3);
+    rp.ctl = q.ctl3 + (r + co) % 3;
     rp.clear_slots = 1;
     rp.init = 0;
     if (blockIdx.x == 0) {  // the counters of round r + 1 (last read in round r - 2's close)
-      uint32_t* z = reinterpret_cast<uint32_t*>(q.ctl3 + ((r + 1) % 3));
+      uint32_t* z = reinterpret_cast<uint32_t*>(q.ctl3 + (r + 1 + co) % 3);
       for (uint32_t i = threadIdx.x; i < sizeof(LvCtl) / 4; i += LV_BLOCK) st_wt32(z + i, 0u);
     }
     LvRoundIn in;

@@ -75,6 +75,8 @@ struct LevelBufs {
   size_t stg_bytes[2] = {0, 0}, idx_bytes[2] = {0, 0}, ht_bytes[2] = {0, 0};
   uint32_t grid_round = 0, grid_insert = 0, grid_nq = 0;  // resident grids (for grid_nq)
   uint32_t grid_persist = 0;                // lv_persist: one workgroup per CU
+  bool coop = false;                        // lv_persist launched cooperatively (residency guaranteed)
+  bool persist_refused = false;             // a persistent launch was refused or timed out: host-driven rounds
 };
 
 struct LevelStats {
@@ -84,6 +86,7 @@ struct LevelStats {
   uint32_t syncs = 0;  // host synchronizations (one per batch of device-driven rounds)
   uint64_t persist_rounds = 0, persist_launches = 0;  // rounds run inside lv_persist
   uint64_t solo_rounds = 0;  // of those, one-configuration rounds run by one workgroup
+  uint32_t persist_fallbacks = 0;  // searches restarted host-driven (persistent launch refused / timed out)
 };
 
 // A batch of histories resident on one device. Every buffer is grown on
@@ -198,6 +201,8 @@ struct DistLevel {
   uint32_t found_parent = TRACE_NONE, found_move = TRACE_NONE, found_p4 = 0;
   uint64_t configs = 0, children = 0, max_frontier = 0;
   double ms = 0;
+  uint8_t* snap = nullptr;       // the frontier entering persistent replicated rounds (restored if they abort)
+  size_t snap_cap = 0;
 };
 int dist_create(DistLevel& d, const History* h, uint32_t rank, uint32_t world, uint32_t reductions_off,
                 hipStream_t stream, std::string& err);

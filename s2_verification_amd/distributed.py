@@ -236,7 +236,8 @@ def _walk(traces: List[np.ndarray], parent: int, move: int) -> Optional[List[int
 
 
 def check_distributed(checker, history: History, group=None, witness: bool = True,
-                      wide: int = 4096, persistent: Optional[bool] = None) -> DistResult:
+                      wide: int = 4096, persistent: Optional[bool] = None,
+                      self_exchange: bool = False) -> DistResult:
     """Check one history with every rank of `group` (default: the world).
 
     Rounds whose frontier is narrower than `wide` configurations run
@@ -251,7 +252,13 @@ def check_distributed(checker, history: History, group=None, witness: bool = Tru
     for several gloo ranks, which are the tests' ranks sharing one GPU: the
     persistent grid of one process needs a workgroup resident on every CU at
     once, and kernels of other processes on the same GPU do not leave room
-    for it (its barrier times out after 2 s and the call fails)."""
+    for it. persistent=True there still gives the right answer: a refused
+    cooperative launch or a timed-out grid barrier sends the search back to
+    host-driven replicated rounds from the frontier it started from.
+
+    self_exchange: with one rank, still switch to partitioned rounds at
+    `wide` (every child goes through the all-to-all to rank 0 itself): the
+    multi-GPU round sequence, rehearsed on one GPU."""
     rank = dist.get_rank(group)
     world = dist.get_world_size(group)
     device = torch.device("cuda", torch.cuda.current_device())
@@ -276,7 +283,8 @@ def check_distributed(checker, history: History, group=None, witness: bool = Tru
                 rounds += 1
             first = False
             if replicated:
-                run = ds.local_run(wide if world > 1 else 1 << 32) if (persistent and rounds > 0) else None
+                split = world > 1 or self_exchange  # partitioned rounds at `wide`
+                run = ds.local_run(wide if split else 1 << 32) if (persistent and rounds > 0) else None
                 if run is not None:
                     nn, found, nr, dconf = run
                     rounds += nr - 1  # (this iteration counted one)
@@ -290,7 +298,7 @@ def check_distributed(checker, history: History, group=None, witness: bool = Tru
                 if nn == 0:
                     verdict = Illegal
                     break
-                if world > 1 and nn >= wide:
+                if split and nn >= wide:
                     ds.keep_owned()
                     replicated = False
                 continue

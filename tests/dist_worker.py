@@ -34,7 +34,7 @@ def exchange_worker(rank, world, port, q):
         q.put((rank, "error", traceback.format_exc()))
 
 
-def search_worker(rank, world, port, backend, names, wide, persistent, q):
+def search_worker(rank, world, port, backend, names, wide, persistent, self_exchange, q):
     """GPU: every rank checks the named histories with check_distributed."""
     try:
         import torch
@@ -49,7 +49,7 @@ def search_worker(rank, world, port, backend, names, wide, persistent, q):
         out = []
         for name in names:
             h = W.config_history(name)
-            r = check_distributed(checker, h, wide=wide, persistent=persistent)
+            r = check_distributed(checker, h, wide=wide, persistent=persistent, self_exchange=self_exchange)
             out.append((name, r.verdict, r.rounds, r.configs, r.witness_valid,
                         None if r.witness is None else len(r.witness), h.info()["n_ops"]))
         q.put((rank, out))

@@ -52,23 +52,32 @@ def test_walk_crosses_ranks():
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("world,wide,backend,persistent", [(1, 4096, "gloo", True), (1, 4096, "gloo", False),
-                                                           (2, 0, "gloo", None), (2, 256, "gloo", None),
-                                                           (3, 1024, "gloo", None),
-                                                           (1, 0, "nccl", None), (1, 4096, "nccl", True)])
-def test_distributed_search_one_gpu(world, wide, backend, persistent):
+@pytest.mark.parametrize("world,wide,backend,persistent,selfx", [
+    (1, 4096, "gloo", True, False), (1, 4096, "gloo", False, False),
+    (2, 0, "gloo", None, False), (2, 256, "gloo", None, False),
+    (3, 1024, "gloo", None, False),
+    (1, 0, "nccl", None, False), (1, 4096, "nccl", True, False),
+    (1, 256, "nccl", True, True), (1, 1024, "gloo", True, True),
+    (2, 256, "gloo", True, False)])
+def test_distributed_search_one_gpu(world, wide, backend, persistent, selfx):
     """wide=0: every round partitioned; otherwise replicated while the
     frontier is narrower than `wide`, partitioned above it (both switches
     happen on H212 / C5bad at 256 and 1024); replicated rounds inside the
     persistent kernel (s2lc_dist_local_run) or host-driven one by one. The
     nccl cases are RCCL with one rank: partitioning every round (a
     self-exchange through the same all-to-all calls the multi-GPU run makes),
-    and the persistent replicated rounds."""
+    the persistent replicated rounds, and (selfx) the multi-GPU sequence
+    replicated-in-the-persistent-kernel -> partitioned -> gathered ->
+    replicated again on one rank. World 2 with persistent=True: two processes'
+    persistent grids on one GPU (cooperative launches, or a barrier time-out
+    that sends the search back to host-driven rounds; the verdict and round
+    counts must not change)."""
     import dist_worker
     ref = golden("hard_reduced.json")
     names = [n for n in ("H174", "C5bad", "H212") if n in ref]
     port = random.randint(20000, 40000)
-    out = _spawn(dist_worker.search_worker, [(r, world, port, backend, names, wide, persistent) for r in range(world)])
+    out = _spawn(dist_worker.search_worker, [(r, world, port, backend, names, wide, persistent, selfx)
+                                             for r in range(world)])
     rc = golden("hard_round_counts.json")
     for rank, res in out:
         for name, verdict, rounds, configs, wvalid, wlen, n_ops in res:
@@ -92,7 +101,8 @@ def test_distributed_wide_history(world, wide, backend):
     rc = golden("hard_round_counts.json")["C5wide"]["0"]
     assert config_digest("C5wide") == ref["digest"], "simulator output changed: regenerate the fixture"
     port = random.randint(20000, 40000)
-    out = _spawn(dist_worker.search_worker, [(r, world, port, backend, ["C5wide"], wide, None) for r in range(world)])
+    out = _spawn(dist_worker.search_worker, [(r, world, port, backend, ["C5wide"], wide, None, False)
+                                             for r in range(world)])
     for rank, res in out:
         for name, verdict, rounds, configs, wvalid, wlen, n_ops in res:
             assert verdict == ref["verdict"] and rounds == rc["rounds"], (rank, verdict, rounds)

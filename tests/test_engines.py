@@ -406,3 +406,70 @@ def test_results_flat_matches_results():
     assert any(r.verdict == s2.Illegal for r in res) and any(r.verdict == s2.Ok for r in res)
     nw = b.results_flat(with_witness=False)
     assert (nw["witness_offs"] == 0).all() and (nw["verdict"] == flat["verdict"]).all()
+
+
+@pytest.mark.parametrize("plain", [False, True])
+def test_persist_fallback_keeps_round_counts(plain, monkeypatch):
+    """ADVICE / VERDICT r2: lv_persist's grid barrier. A barrier wait past its
+    limit (forced here: 1 us, so the first wait of a launch gives up) must not
+    surface as an error: the search restarts from round 0 with host-driven
+    rounds, with the same verdict and the same unique-configuration count in
+    every round as the committed CPU reduced search. Cooperative launches and
+    plain ones (S2LC_PERSIST_PLAIN=1)."""
+    from s2_verification_amd import workloads as W
+    monkeypatch.setenv("S2LC_PERSIST_SPIN_US", "1")
+    if plain:
+        monkeypatch.setenv("S2LC_PERSIST_PLAIN", "1")
+    ref = golden("hard_round_counts.json")["H174"]
+    want = ref["0"]
+    h = W.config_history("H174")
+    c = s2.Checker(round_counts=True)  # a fresh context: the fallback is sticky per context
+    b = c.batch([h])
+    r = b.check()[0]
+    st = b.stats()
+    assert r.verdict == want["verdict"] and r.rounds == want["rounds"], (r, st)
+    assert b.round_counts(0) == want["counts"]
+    assert st["level_persist_fallbacks"] == 1 and st["level_solo_rounds"] == 0, st
+    if r.verdict == s2.Ok:
+        assert r.witness is not None and len(r.witness) == h.info()["n_ops"]
+    # the context's next search runs host-driven from the start
+    b2 = c.batch([h])
+    r2 = b2.check()[0]
+    assert r2.verdict == r.verdict and b2.stats()["level_persist_launches"] == 0
+
+
+def test_concurrent_contexts_persistent_rounds():
+    """Two contexts on GPU 0 checking hard histories from two threads at once
+    (each with persistent grids of 256 workgroups), and one context sharding
+    H174 + H212 over devices=[0, 0]: verdicts and round counts as committed."""
+    import threading
+    from s2_verification_amd import workloads as W
+    rc = golden("hard_round_counts.json")
+    names = ["H174", "H212"]
+    hs = {n: W.config_history(n) for n in names}
+    out, errs = {}, []
+
+    def work(name):
+        try:
+            c = s2.Checker(round_counts=True)
+            b = c.batch([hs[name]])
+            r = b.check()[0]
+            out[name] = (r.verdict, r.rounds, b.round_counts(0), r.witness is not None, b.stats())
+        except Exception as e:  # noqa: BLE001
+            errs.append(repr(e))
+
+    ts = [threading.Thread(target=work, args=(n,)) for n in names]
+    for t in ts:
+        t.start()
+    for t in ts:
+        t.join(timeout=300)
+    assert not errs, errs
+    for n in names:
+        v, rounds, counts, has_w, st = out[n]
+        want = rc[n]["0"]
+        assert (v, rounds) == (want["verdict"], want["rounds"]), (n, v, rounds, st)
+        assert counts == want["counts"], n
+        assert v != s2.Ok or has_w
+    res = s2.Checker(devices=[0, 0]).check_many([hs["H174"], hs["H212"]])
+    assert [r.verdict for r in res] == [rc[n]["0"]["verdict"] for n in names]
+    assert [r.rounds for r in res] == [rc[n]["0"]["rounds"] for n in names]
