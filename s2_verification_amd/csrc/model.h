@@ -76,12 +76,16 @@ __host__ __device__ inline uint64_t fold_hashes(uint64_t h, const uint64_t* rs, 
 
 // Device fold with the record-hash loads issued 8 at a time: the fold is a
 // dependent chain of multiplies, but its loads are independent, and a loop that
-// loads inside the chain pays one memory latency per record.
+// loads inside the chain pays one memory latency per record. The 8 loads are
+// unconditional (indices clamped to the last record): a guarded load becomes a
+// branch per record, and gfx950 code then waits for each load before the
+// next one issues (8 memory latencies instead of one).
 __device__ inline uint64_t fold_hashes_blk(uint64_t h, const uint64_t* __restrict__ rs, uint32_t n) {
   for (uint32_t b = 0; b < n; b += 8) {
     uint64_t v[8];
+    const uint32_t last = n - 1 - b;
 #pragma unroll
-    for (int q = 0; q < 8; ++q) v[q] = b + q < n ? rs[b + q] : 0;
+    for (int q = 0; q < 8; ++q) v[q] = rs[b + min((uint32_t)q, last)];
 #pragma unroll
     for (int q = 0; q < 8; ++q)
       if (b + q < n) h = chain_hash(h, v[q]);

@@ -8,7 +8,8 @@ against the CPU results committed in tests/golden/c4_verdicts.json
   * every Ok carries a witness certified by the library's CPU replay;
   * rounds and the per-round unique-configuration counts = the CPU reduced
     search (oracle/reduced.c), and for Illegal histories (whole search
-    space) the total unique configurations too.
+    space) the total unique configurations too (the GPU counts round 0's
+    initial configuration, oracle/reduced.c does not).
 
 The simulator output is pinned by a digest of the batch's collector JSONL.
 """
@@ -73,6 +74,6 @@ def test_c4_full_batch_round_counts(c4):
         wv, _, rv, rounds, configs, dig = row
         counts = b.round_counts(i)
         d = hashlib.sha256(np.asarray(counts, dtype="<u4").tobytes()).hexdigest()[:16]
-        if r.verdict != V[rv] or r.rounds != rounds or d != dig or (rv == "I" and r.configs_explored != configs):
+        if r.verdict != V[rv] or r.rounds != rounds or d != dig or (rv == "I" and r.configs_explored != configs + 1):
             mism.append((i, r.verdict, rv, r.rounds, rounds, r.configs_explored, configs))
     assert not mism, (len(mism), mism[:5])

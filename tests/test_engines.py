@@ -423,7 +423,7 @@ def test_persist_fallback_keeps_round_counts(plain, monkeypatch):
     ref = golden("hard_round_counts.json")["H174"]
     want = ref["0"]
     h = W.config_history("H174")
-    c = s2.Checker(round_counts=True)  # a fresh context: the fallback is sticky per context
+    c = s2.Checker(round_counts=True)
     b = c.batch([h])
     r = b.check()[0]
     st = b.stats()
@@ -432,10 +432,12 @@ def test_persist_fallback_keeps_round_counts(plain, monkeypatch):
     assert st["level_persist_fallbacks"] == 1 and st["level_solo_rounds"] == 0, st
     if r.verdict == s2.Ok:
         assert r.witness is not None and len(r.witness) == h.info()["n_ops"]
-    # the context's next search runs host-driven from the start
-    b2 = c.batch([h])
-    r2 = b2.check()[0]
-    assert r2.verdict == r.verdict and b2.stats()["level_persist_launches"] == 0
+    # the same batch's next search runs host-driven from the start (the
+    # fallback is sticky per device batch: no further persistent launch)
+    r1 = b.check()[0]
+    st1 = b.stats()
+    assert (r1.verdict, r1.rounds) == (r.verdict, r.rounds) and b.round_counts(0) == want["counts"]
+    assert st1["level_persist_launches"] == 0 and st1["level_persist_fallbacks"] == 0, st1
 
 
 def test_concurrent_contexts_persistent_rounds():
