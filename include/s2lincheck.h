@@ -211,6 +211,20 @@ int s2lc_history_get_event(const s2lc_history* h, size_t i, s2lc_event* out);
 /* Bulk export of events [0, n); equal token strings share one pointer. */
 int s2lc_history_get_events(const s2lc_history* h, s2lc_event* out, size_t n);
 
+/* ----- binary SoA history cache --------------------
+ * eventsFromReader (main.go:529-563) decodes every history from JSONL on every
+ * run. The cache is the decoded, finalized form (events, record-hash pool,
+ * tokens, the chain-major record table and its index arrays) as one byte
+ * image; loading it skips JSON decode and the chain decomposition.
+ * save_many: *out (free with s2lc_free) holds n histories.
+ * load_many: out[0 .. *n) get new histories (free each with
+ * s2lc_history_free); out == NULL only sets *n. Parallel over histories
+ * (n_threads == 1: serial). Every array is bounds-checked against the image;
+ * a malformed image gives S2LC_EDECODE and no histories. */
+int s2lc_history_save_many(const s2lc_history* const* hs, size_t n, uint8_t** out, size_t* out_len);
+int s2lc_history_load_many(const uint8_t* buf, size_t len, int n_threads, s2lc_history** out, size_t cap,
+                           size_t* n);
+
 typedef struct s2lc_history_info {
   uint32_t n_events;
   uint32_t n_ops;

@@ -187,6 +187,11 @@ SIGNATURES = [
                                             ctypes.c_size_t, ctypes.c_int, ctypes.POINTER(_P),
                                             ctypes.POINTER(ctypes.c_size_t), ctypes.c_char_p, ctypes.c_size_t]),
     ("s2lc_visualize", ctypes.c_int, [_P, ctypes.POINTER(c_result), ctypes.c_char_p]),
+    ("s2lc_history_save_many", ctypes.c_int, [ctypes.POINTER(_P), ctypes.c_size_t,
+                                              ctypes.POINTER(ctypes.POINTER(ctypes.c_uint8)),
+                                              ctypes.POINTER(ctypes.c_size_t)]),
+    ("s2lc_history_load_many", ctypes.c_int, [ctypes.c_char_p, ctypes.c_size_t, ctypes.c_int, ctypes.POINTER(_P),
+                                              ctypes.c_size_t, ctypes.POINTER(ctypes.c_size_t)]),
     ("s2lc_witness_from_moves", ctypes.c_int, [_P, ctypes.POINTER(ctypes.c_uint32), ctypes.c_size_t, ctypes.c_int,
                                                ctypes.POINTER(ctypes.c_int64), ctypes.c_size_t]),
     ("s2lc_dist_create", ctypes.c_int, [_P, _P, ctypes.c_int, ctypes.c_int, ctypes.POINTER(_P)]),
@@ -406,6 +411,36 @@ def load_many(blobs: Sequence[bytes], threads: int = 0) -> List[History]:
     if rc:
         raise S2LCError(rc, err.value.decode(errors="replace"))
     return [History(out[i]) for i in range(n)]
+
+
+def save_cache(hs: Sequence[History]) -> bytes:
+    """s2lc_history_save_many: the binary SoA cache image of `hs` (decoded and
+    finalized; load_cache skips JSONL decode)."""
+    arr = (ctypes.c_void_p * max(1, len(hs)))(*[h._h for h in hs])
+    buf = ctypes.POINTER(ctypes.c_uint8)()
+    n = ctypes.c_size_t()
+    rc = lib().s2lc_history_save_many(arr, len(hs), ctypes.byref(buf), ctypes.byref(n))
+    if rc:
+        raise S2LCError(rc, "save_cache")
+    data = ctypes.string_at(buf, n.value)
+    lib().s2lc_free(buf)
+    return data
+
+
+def load_cache(data: bytes, threads: int = 0) -> List[History]:
+    """s2lc_history_load_many: histories from a save_cache image (bytes, or a
+    read-only buffer such as an mmap of a cache file)."""
+    if not isinstance(data, bytes):
+        data = bytes(data)
+    n = ctypes.c_size_t()
+    rc = lib().s2lc_history_load_many(data, len(data), threads, None, 0, ctypes.byref(n))
+    if rc:
+        raise S2LCError(rc, "load_cache: not a history cache image")
+    out = (ctypes.c_void_p * max(1, n.value))()
+    rc = lib().s2lc_history_load_many(data, len(data), threads, out, n.value, ctypes.byref(n))
+    if rc:
+        raise S2LCError(rc, "load_cache: malformed history cache image")
+    return [History(out[i]) for i in range(n.value)]
 
 
 def events_from_reader(data) -> History:

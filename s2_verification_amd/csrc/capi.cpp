@@ -303,10 +303,11 @@ int s2lc_history_from_events(const s2lc_event* ev, size_t n, s2lc_history** out,
 
 void s2lc_history_free(s2lc_history* h) { delete h; }
 
-size_t s2lc_history_event_count(const s2lc_history* h) { return h ? h->h.events.size() : 0; }
+size_t s2lc_history_event_count(const s2lc_history* h) { return h ? h->h.n_events() : 0; }
 
 int s2lc_history_get_event(const s2lc_history* h, size_t i, s2lc_event* out) {
-  if (!h || !out || i >= h->h.events.size()) return S2LC_EINVAL;
+  if (!h || !out || i >= h->h.n_events()) return S2LC_EINVAL;
+  h->h.ensure_events();
   const History& H = h->h;
   const Event& e = H.events[i];
   memset(out, 0, sizeof *out);
@@ -335,7 +336,8 @@ int s2lc_history_get_event(const s2lc_history* h, size_t i, s2lc_event* out) {
 }
 
 int s2lc_history_get_events(const s2lc_history* h, s2lc_event* out, size_t n) {
-  if (!h || (!out && n) || n > h->h.events.size()) return S2LC_EINVAL;
+  if (!h || (!out && n) || n > h->h.n_events()) return S2LC_EINVAL;
+  h->h.ensure_events();
   for (size_t i = 0; i < n; ++i) s2lc_history_get_event(h, i, &out[i]);
   return 0;
 }
@@ -343,7 +345,7 @@ int s2lc_history_get_events(const s2lc_history* h, s2lc_event* out, size_t n) {
 int s2lc_history_info_get(const s2lc_history* h, s2lc_history_info* out) {
   if (!h || !out) return S2LC_EINVAL;
   const History& H = h->h;
-  out->n_events = (uint32_t)H.events.size();
+  out->n_events = (uint32_t)H.n_events();
   out->n_ops = H.n_ops;
   out->n_chains = H.K;
   out->n_tokens = (uint32_t)H.tokens.size();
@@ -362,8 +364,10 @@ namespace {
 // out[0 .. B.n_hist). Every Ok witness must replay through s2Model.Step
 // (main.go:264-335); one that does not is a checker bug: that history becomes
 // Unknown (S2LC_R_WITNESS_INVALID) and the call returns S2LC_EWITNESS.
+// flat_ids (nullable): Ok witnesses go straight to flat_ids + flat_offs[i]
+// (no per-history allocation; out[i].witness stays null, witness_len is set).
 int collect_results(DevBatch& B, const RunStats& stats, bool witness_recorded, s2lc_result* out, int with_witness,
-                    std::string& err) {
+                    std::string& err, int64_t* flat_ids = nullptr, const uint64_t* flat_offs = nullptr) {
   const bool want_w = with_witness && witness_recorded;
   if (want_w && B.n_hist) {
     const int rc = batch_fetch_moves(B, err);
@@ -409,10 +413,18 @@ int collect_results(DevBatch& B, const RunStats& stats, bool witness_recorded, s
             invalid = 1;
             continue;
           }
+          if (flat_ids) {
+            int64_t* w = flat_ids + flat_offs[i];
+            for (size_t k = 0; k < order.size(); ++k) w[k] = H.op_ids[order[k]];
+            o.witness_len = (uint32_t)order.size();
+            continue;
+          }
           o.witness = (int64_t*)malloc(sizeof(int64_t) * (order.size() ? order.size() : 1));
           if (!o.witness) { oom = 1; continue; }
           for (size_t k = 0; k < order.size(); ++k) o.witness[k] = H.op_ids[order[k]];
           o.witness_len = (uint32_t)order.size();
+        } else if (flat_ids) {
+          continue;  // (the flat form carries no Illegal partials)
         } else if (rebuild_linearization(H, moves, n_moves, false, order, ident, true) &&
                    replay_prefix(H, order.data(), ident.data(), order.size())) {
           o.partial = (int64_t*)malloc(sizeof(int64_t) * (order.size() ? order.size() : 1));
@@ -551,31 +563,44 @@ int s2lc_batch_results_flat(s2lc_ctx* c, s2lc_batch* b, int32_t* verdicts, int32
   try {
     if (hipSetDevice(b->b.device) != hipSuccess) { c->err = "hipSetDevice failed"; return S2LC_EHIP; }
     const size_t n = b->b.n_hist;
+    DevBatch& B = b->b;
     std::vector<s2lc_result> res(std::max<size_t>(n, 1));
-    const int rc = collect_results(b->b, b->stats, b->witness, res.data(), witness_ids != nullptr, c->err);
-    if (rc && rc != S2LC_EWITNESS) return rc;
+    // offsets first: a certified Ok witness is every op of its history, so
+    // the witnesses are written in place by the certifying threads
+    const bool want = witness_ids != nullptr && b->witness;
     uint64_t total = 0;
     for (size_t i = 0; i < n; ++i) {
       witness_offs[i] = total;
-      total += res[i].witness ? res[i].witness_len : 0;
+      if (want && B.h_res[i].verdict == V_OK && B.h_res[i].has_witness == 1) total += B.src[i]->n_ops;
     }
     witness_offs[n] = total;
-    int out_rc = rc;
-    if (witness_ids && total > ids_cap) {
+    if (want && total > ids_cap) {
       c->err = "witness buffer too small";
-      out_rc = S2LC_EINVAL;
+      return S2LC_EINVAL;
     }
-    parallel_for(n, 256, [&](size_t i) {
-      s2lc_result& r = res[i];
+    const int rc = collect_results(B, b->stats, b->witness, res.data(), witness_ids != nullptr, c->err,
+                                   want ? witness_ids : nullptr, witness_offs);
+    if (rc && rc != S2LC_EWITNESS) return rc;
+    // a witness that failed certification (checker bug: rc = EWITNESS) has no
+    // ids: close its gap
+    if (want && rc == S2LC_EWITNESS) {
+      uint64_t w = 0;
+      for (size_t i = 0; i < n; ++i) {
+        const uint64_t o = witness_offs[i], len = res[i].witness_len;
+        if (w != o && len) memmove(witness_ids + w, witness_ids + o, sizeof(int64_t) * len);
+        witness_offs[i] = w;
+        w += len;
+      }
+      witness_offs[n] = w;
+    }
+    for (size_t i = 0; i < n; ++i) {
+      const s2lc_result& r = res[i];
       if (verdicts) verdicts[i] = r.verdict;
       if (reasons) reasons[i] = r.reason;
       if (configs) configs[i] = r.configs_explored;
       if (rounds) rounds[i] = r.rounds;
-      if (witness_ids && out_rc != S2LC_EINVAL && r.witness)
-        memcpy(witness_ids + witness_offs[i], r.witness, sizeof(int64_t) * r.witness_len);
-      s2lc_result_free(&r);
-    });
-    return out_rc;
+    }
+    return rc;
   } catch (const std::bad_alloc&) {
     c->err = "out of memory";
     return S2LC_ENOMEM;

@@ -38,6 +38,7 @@ static uint32_t classify(const Event& in, const Event& out) {
 }
 
 OpRec History::rec_of(uint32_t d) const {
+  ensure_events();
   const Event& in = events[op_call[d]];
   const Event& out = events[op_ret[d]];
   OpRec r{};

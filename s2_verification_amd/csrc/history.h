@@ -7,6 +7,8 @@
 #pragma once
 #include <stdint.h>
 
+#include <memory>
+#include <mutex>
 #include <string>
 #include <vector>
 
@@ -38,7 +40,9 @@ enum : uint16_t {
 
 struct History {
   // ---- porcupine events ----
-  std::vector<Event> events;
+  // (a history loaded from the binary cache builds this list on first use:
+  // the check reads only the records; use n_events() / ensure_events())
+  mutable std::vector<Event> events;
   std::vector<uint64_t> pool;         // record hashes
   std::vector<std::string> tokens;    // token id i+1 -> string
 
@@ -64,6 +68,12 @@ struct History {
   int finalize();
   // OpRec of dense op d built from its call/return events (sufmin unset).
   OpRec rec_of(uint32_t d) const;
+
+  // ---- binary cache (cache.cpp) ----
+  std::vector<int64_t> lazy_client;          // per event client id while `events` is not built
+  std::unique_ptr<std::once_flag> lazy_once;  // builds `events` once (thread-safe)
+  size_t n_events() const { return lazy_once ? lazy_client.size() : events.size(); }
+  void ensure_events() const;                 // no-op unless loaded from the cache
 };
 
 // JSONL loader (eventsFromReader, main.go:529-563). Returns 0 or S2LC_EDECODE.

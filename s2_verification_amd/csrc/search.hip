@@ -413,7 +413,13 @@ int batch_run(DevBatch& b, hipStream_t stream, const RunOpts& ro, RunStats& st, 
       pp.n_hist = n_l;
       pp.counter = b.counter + 12 + li;
       const uint32_t L = 8u << li;
-      const size_t smem = li == 0 ? pack_smem_bytes<8>() : li == 1 ? pack_smem_bytes<16>() : pack_smem_bytes<32>();
+      const size_t smem = li == 0 ? pack_lds_bytes<8>() : li == 1 ? pack_lds_bytes<16>() : pack_lds_bytes<32>();
+      if (!b.pack_attr[li]) {  // more than 64 KiB of dynamic LDS per workgroup
+        if (li == 0) HIPCHK(hipFuncSetAttribute((const void*)pack_kernel<8>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)smem));
+        else if (li == 1) HIPCHK(hipFuncSetAttribute((const void*)pack_kernel<16>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)smem));
+        else HIPCHK(hipFuncSetAttribute((const void*)pack_kernel<32>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)smem));
+        b.pack_attr[li] = true;
+      }
       int bpc = b.pack_bpc[li];  // resident blocks per CU (queried once per batch)
       if (bpc == 0) {
         if (li == 0) HIPCHK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&bpc, pack_kernel<8>, PACK_BLOCK, smem));

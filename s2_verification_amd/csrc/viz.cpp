@@ -82,6 +82,7 @@ extern "C" int s2lc_visualize(const s2lc_history* hh, const s2lc_result* r, cons
   if (!hh || !r || !path) return S2LC_EINVAL;
   const History& h = hh->h;
   if (h.status) return h.status;
+  h.ensure_events();
   FILE* f = fopen(path, "w");
   if (!f) return S2LC_EIO;
   try {
