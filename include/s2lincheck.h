@@ -182,6 +182,33 @@ typedef struct s2lc_result {
                                     the call returns S2LC_EWITNESS */
 #define S2LC_R_TIMEOUT 6         /* s2lc_opts.timeout_us expired before the verdict (Unknown) */
 
+/* ----- LinearizationInfo: per-op longest partial linearizations ------------
+ * porcupine.CheckEventsVerbose returns, beside the verdict, the longest
+ * partial linearization containing each op (its DFS records one at every
+ * backtrack; main.go:606), which Visualize renders (main.go:627).
+ *   Ok: the certified witness, for every op (as porcupine records on success).
+ *   Illegal: a second level search of the history with the pruning
+ *     reductions off (P1, P2, P4 and the indefinite deferral: porcupine's DFS
+ *     visits every reachable configuration of an Illegal history, and so must
+ *     this one for the lengths to be porcupine's), recording per op the
+ *     largest configuration that contains it. Each distinct one is rebuilt
+ *     from the device trace and certified like a witness (a real-time-closed
+ *     prefix whose every step the CPU model accepts).
+ *   exact = 0 when that search stopped at its budget (the context's
+ *     max_configs, else 2^22 configurations) or the device capacity: the
+ *     partials are certified but may be shorter than porcupine's.
+ * Free with s2lc_partials_free. */
+typedef struct s2lc_partials {
+  int32_t verdict;      /* the history's verdict (s2lc_verdict) */
+  uint32_t exact;
+  uint32_t n_ops;
+  uint32_t n_partials;  /* distinct partial linearizations */
+  int64_t* op_ids;      /* [n_ops] Event.Id of dense op d (first-appearance order) */
+  uint32_t* op_partial; /* [n_ops] index of op d's longest partial, UINT32_MAX: in none */
+  uint64_t* offs;       /* [n_partials + 1] */
+  int64_t* ids;         /* Event.Ids of partial k in linearization order: ids[offs[k] .. offs[k+1]) */
+} s2lc_partials;
+
 /* ----- context ----------------------------------------------------------- */
 s2lc_ctx* s2lc_create(const s2lc_opts* opts, int* status);
 void s2lc_destroy(s2lc_ctx* ctx);
@@ -239,7 +266,10 @@ int s2lc_history_info_get(const s2lc_history* h, s2lc_history_info* out);
 /* ----- checker (porcupine.CheckEventsVerbose, main.go:606) ------------------ */
 int s2lc_check(s2lc_ctx* ctx, const s2lc_history* h, s2lc_result* out);
 int s2lc_check_batch(s2lc_ctx* ctx, const s2lc_history* const* hs, size_t n, s2lc_result* out);
-void s2lc_result_free(s2lc_result* r); /* frees r->witness; r itself is caller storage */
+void s2lc_result_free(s2lc_result* r);
+/* LinearizationInfo (above) of one history; 0 or an s2lc_status. */
+int s2lc_check_partials(s2lc_ctx* ctx, const s2lc_history* h, s2lc_partials* out);
+void s2lc_partials_free(s2lc_partials* p); /* frees r->witness; r itself is caller storage */
 
 /* Device-resident batches: upload once, check many times (bench / DST loops). */
 int s2lc_batch_create(s2lc_ctx* ctx, const s2lc_history* const* hs, size_t n, s2lc_batch** out);
@@ -346,6 +376,10 @@ int s2lc_witness_from_moves(const s2lc_history* h, const uint32_t* moves, size_t
  * certified prefix (Illegal) with the powerset state after each op
  * (DescribeState). r is the s2lc_check result for h. */
 int s2lc_visualize(const s2lc_history* h, const s2lc_result* r, const char* path);
+/* The same page with LinearizationInfo (s2lc_check_partials): hovering an op
+ * outlines the longest partial linearization containing it, as porcupine's
+ * Visualize does; info may be NULL. */
+int s2lc_visualize_info(const s2lc_history* h, const s2lc_result* r, const s2lc_partials* info, const char* path);
 
 /* ----- distributed search of ONE history (BASELINE config C5) --------------
  * One rank per GPU; configurations are owned by a hash of their fingerprint.

@@ -206,8 +206,23 @@ static double now_s(void) {
 
 /* porcupine checkEvents -> renumber -> convertEntries (time = slice index)
  * -> checkSingle(model, entries, computePartial, kill). */
+static int check_wgl_impl(const or_event* ev, size_t n_ev, int compute_partial, double timeout_s,
+                          uint64_t max_entries, or_stats* st, int32_t* longest_out);
+
 int or_check_wgl(const or_event* ev, size_t n_ev, int compute_partial, double timeout_s,
                  uint64_t max_entries, or_stats* st) {
+  return check_wgl_impl(ev, n_ev, compute_partial, timeout_s, max_entries, st, NULL);
+}
+
+/* LinearizationInfo's lengths: longest_out[id] = length of the longest partial
+ * linearization porcupine records for dense op id (0: in none). */
+int or_check_wgl_longest(const or_event* ev, size_t n_ev, double timeout_s, uint64_t max_entries, or_stats* st,
+                         int32_t* longest_out) {
+  return check_wgl_impl(ev, n_ev, 1, timeout_s, max_entries, st, longest_out);
+}
+
+static int check_wgl_impl(const or_event* ev, size_t n_ev, int compute_partial, double timeout_s,
+                          uint64_t max_entries, or_stats* st, int32_t* longest_out) {
   or_stats local;
   memset(&local, 0, sizeof(local));
   double t0 = now_s();
@@ -254,7 +269,12 @@ int or_check_wgl(const or_event* ev, size_t n_ev, int compute_partial, double ti
   int result = OR_ILLEGAL;
   uint64_t iter = 0;
   for (;;) {
-    if (head->next == NULL) { result = OR_OK; break; }
+    if (head->next == NULL) {
+      result = OR_OK;
+      if (compute_partial) /* success: every op's longest partial is the linearization */
+        for (int id = 0; id < n; id++) longest[id].n = ncalls;
+      break;
+    }
     if ((++iter & 0xFFF) == 0 && timeout_s > 0 && now_s() - t0 > timeout_s) { result = OR_UNKNOWN; break; }
     if (entry->match) {
       node* matching = entry->match;
@@ -319,6 +339,8 @@ int or_check_wgl(const or_event* ev, size_t n_ev, int compute_partial, double ti
     }
   }
 
+  if (longest_out && longest)
+    for (int id = 0; id < n; id++) longest_out[id] = (int32_t)longest[id].n;
   /* free: cached sets own every state except init */
   for (size_t i = 0; i < c.cap; i++) if (c.b[i].used) {
     for (int k = 0; k < c.b[i].n; k++) { free(c.b[i].e[k].bits); free(c.b[i].e[k].st.v); }

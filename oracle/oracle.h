@@ -71,6 +71,11 @@ uint64_t or_fold(uint64_t stream_hash, const uint64_t* hashes, uint64_t n);
 /* porcupine.CheckEventsVerbose(s2Model.ToModel(), events, 0), restated. */
 int or_check_wgl(const or_event* ev, size_t n, int compute_partial, double timeout_s,
                  uint64_t max_entries, or_stats* st);
+/* The same search; longest_out[id] (n_ops entries, dense ids in first-appearance
+ * order) = length of the longest partial linearization containing op id that
+ * computePartial recorded (LinearizationInfo), 0 if none. */
+int or_check_wgl_longest(const or_event* ev, size_t n, double timeout_s, uint64_t max_entries, or_stats* st,
+                         int32_t* longest_out);
 /* Independent brute force: every real-time-respecting order, powerset model.
  * Only for small histories (n_ops <= 20). */
 int or_check_brute(const or_event* ev, size_t n, or_stats* st);

@@ -69,6 +69,9 @@ def lib():
         L.or_check_wgl.restype = ctypes.c_int
         L.or_check_wgl.argtypes = [ctypes.c_void_p, ctypes.c_size_t, ctypes.c_int, ctypes.c_double,
                                    ctypes.c_uint64, ctypes.POINTER(_Stats)]
+        L.or_check_wgl_longest.restype = ctypes.c_int
+        L.or_check_wgl_longest.argtypes = [ctypes.c_void_p, ctypes.c_size_t, ctypes.c_double, ctypes.c_uint64,
+                                           ctypes.POINTER(_Stats), ctypes.c_void_p]
         L.or_check_reduced.restype = ctypes.c_int
         L.or_check_reduced.argtypes = [ctypes.c_void_p, ctypes.c_size_t, ctypes.c_uint64, ctypes.c_uint32,
                                        ctypes.c_void_p, ctypes.c_size_t, ctypes.POINTER(_Stats)]
@@ -157,6 +160,18 @@ def check_wgl(events, compute_partial=True, timeout=0.0, max_entries=0):
     return _NAMES[r], {"cache_inserts": st.cache_inserts, "steps": st.steps,
                        "backtracks": st.backtracks, "max_state_set": st.max_state_set,
                        "seconds": st.seconds}
+
+
+def check_wgl_longest(events, timeout=0.0, max_entries=0):
+    """LinearizationInfo's lengths: (verdict, [length of the longest partial
+    linearization porcupine records containing dense op d, for d in 0..n-1])."""
+    ea = _as_array(events)
+    st = _Stats()
+    n_ops = len(ea) // 2 + 1
+    out = np.zeros(max(1, len(ea)), dtype=np.int32)
+    r = lib().or_check_wgl_longest(ea.ptr, len(ea), float(timeout), int(max_entries), ctypes.byref(st),
+                                   out.ctypes.data)
+    return _NAMES[r], out
 
 
 def check_brute(events):

@@ -127,6 +127,13 @@ def _np_field(t):
     return np.dtype(t)
 
 
+class c_partials(ctypes.Structure):
+    _fields_ = [("verdict", ctypes.c_int32), ("exact", ctypes.c_uint32), ("n_ops", ctypes.c_uint32),
+                ("n_partials", ctypes.c_uint32), ("op_ids", ctypes.POINTER(ctypes.c_int64)),
+                ("op_partial", ctypes.POINTER(ctypes.c_uint32)), ("offs", ctypes.POINTER(ctypes.c_uint64)),
+                ("ids", ctypes.POINTER(ctypes.c_int64))]
+
+
 class c_dist_info(ctypes.Structure):
     _fields_ = [("config_bytes", ctypes.c_uint64), ("n_chains", ctypes.c_uint32), ("round", ctypes.c_uint32),
                 ("frontier", ctypes.c_uint32), ("found_parent", ctypes.c_uint32), ("found_move", ctypes.c_uint32),
@@ -187,6 +194,9 @@ SIGNATURES = [
                                             ctypes.c_size_t, ctypes.c_int, ctypes.POINTER(_P),
                                             ctypes.POINTER(ctypes.c_size_t), ctypes.c_char_p, ctypes.c_size_t]),
     ("s2lc_visualize", ctypes.c_int, [_P, ctypes.POINTER(c_result), ctypes.c_char_p]),
+    ("s2lc_check_partials", ctypes.c_int, [_P, _P, ctypes.POINTER(c_partials)]),
+    ("s2lc_visualize_info", ctypes.c_int, [_P, ctypes.POINTER(c_result), ctypes.POINTER(c_partials), ctypes.c_char_p]),
+    ("s2lc_partials_free", None, [ctypes.POINTER(c_partials)]),
     ("s2lc_history_save_many", ctypes.c_int, [ctypes.POINTER(_P), ctypes.c_size_t,
                                               ctypes.POINTER(ctypes.POINTER(ctypes.c_uint8)),
                                               ctypes.POINTER(ctypes.c_size_t)]),
@@ -453,6 +463,17 @@ def load_file(path: str) -> History:
 
 
 @dataclass
+class LinearizationInfo:
+    """porcupine.LinearizationInfo for one partition (S2 has one): the distinct
+    partial linearizations (lists of Event.Id) and, per Event.Id, the index of
+    the longest one containing it (None: in none)."""
+    verdict: str
+    exact: bool
+    partial_linearizations: List[List[int]]
+    largest: dict
+
+
+@dataclass
 class CheckResult:
     verdict: str
     reason: str
@@ -628,6 +649,24 @@ class Checker:
         if rc:
             raise S2LCError(rc, self.last_error())
         return out
+
+    def partials(self, h: History) -> "LinearizationInfo":
+        """s2lc_check_partials: porcupine's LinearizationInfo for one history
+        (the longest certified partial linearization containing each op)."""
+        p = c_partials()
+        rc = lib().s2lc_check_partials(self._ctx, h._h, ctypes.byref(p))
+        if rc:
+            raise S2LCError(rc, self.last_error())
+        try:
+            n, k = p.n_ops, p.n_partials
+            offs = [p.offs[i] for i in range(k + 1)]
+            parts = [[p.ids[x] for x in range(offs[i], offs[i + 1])] for i in range(k)]
+            op_ids = [p.op_ids[d] for d in range(n)]
+            op_part = [p.op_partial[d] for d in range(n)]
+            largest = {op_ids[d]: (op_part[d] if op_part[d] != 0xFFFFFFFF else None) for d in range(n)}
+            return LinearizationInfo(_VERDICT[p.verdict], bool(p.exact), parts, largest)
+        finally:
+            lib().s2lc_partials_free(ctypes.byref(p))
 
     def device_fold(self, seeds, folds):
         """foldRecordHashes on the GPU (the search kernels' device routine):

@@ -13,6 +13,7 @@
 #include <string>
 #include <thread>
 #include <stdexcept>
+#include <unordered_map>
 #include <vector>
 
 #include "history.h"
@@ -757,6 +758,141 @@ int s2lc_device_fold(s2lc_ctx* c, const uint64_t* seeds, const uint64_t* pool, s
   if (!c || (n && (!seeds || !offs || !cnts || !out)) || (pool_len && !pool)) return S2LC_EINVAL;
   if (hipSetDevice(c->device) != hipSuccess) { c->err = "hipSetDevice failed"; return S2LC_EHIP; }
   return device_fold(seeds, pool, pool_len, offs, cnts, n, out, c->stream, c->err);
+}
+
+void s2lc_partials_free(s2lc_partials* p) {
+  if (!p) return;
+  free(p->op_ids);
+  free(p->op_partial);
+  free(p->offs);
+  free(p->ids);
+  memset(p, 0, sizeof *p);
+}
+
+int s2lc_check_partials(s2lc_ctx* c, const s2lc_history* h, s2lc_partials* out) {
+  if (!c || !h || !out) return S2LC_EINVAL;
+  memset(out, 0, sizeof *out);
+  const History& H = h->h;
+  if (H.status) { c->err = H.error; return H.status; }
+  s2lc_result r;
+  int rc = s2lc_check(c, h, &r);
+  if (rc) { s2lc_result_free(&r); return rc; }
+  out->verdict = r.verdict;
+  out->n_ops = H.n_ops;
+  out->exact = 1;
+  std::vector<uint32_t> op_part(H.n_ops, UINT32_MAX);
+  std::vector<uint64_t> offs{0};
+  std::vector<int64_t> ids;
+  try {
+    if (r.verdict == S2LC_OK && r.witness) {
+      // porcupine on success: every op's longest partial is the linearization
+      ids.assign(r.witness, r.witness + r.witness_len);
+      offs.push_back(ids.size());
+      std::fill(op_part.begin(), op_part.end(), 0u);
+    } else if (r.verdict == S2LC_ILLEGAL && !H.structural && H.n_ops) {
+      Shard& sh = shard_of(c, 0);
+      if (hipSetDevice(sh.device) != hipSuccess) { c->err = "hipSetDevice failed"; s2lc_result_free(&r); return S2LC_EHIP; }
+      DevBatch& B = sh.scratch;
+      std::vector<const History*> one{&H};
+      rc = batch_upload(B, one, S2LC_RED_P1 | S2LC_RED_P2 | S2LC_RED_P4 | S2LC_RED_IDEFER, sh.err);
+      unsigned long long* dmax = nullptr;
+      const size_t n_recs = H.recs.size();
+      if (!rc && hipMalloc(&dmax, n_recs * sizeof(unsigned long long)) != hipSuccess) { sh.err = "hipMalloc"; rc = S2LC_EHIP; }
+      if (!rc && hipMemsetAsync(dmax, 0, n_recs * sizeof(unsigned long long), sh.stream) != hipSuccess) rc = S2LC_EHIP;
+      if (!rc) {
+        RunOpts ro = c->run_opts();
+        ro.engine = S2LC_ENGINE_LEVEL;
+        ro.witness = true;
+        ro.round_counts = false;
+        ro.max_configs = c->max_configs ? c->max_configs : (1ull << 22);
+        ro.partial_max = dmax;
+        RunStats st;
+        rc = batch_run(B, sh.stream, ro, st, sh.err);
+      }
+      std::vector<unsigned long long> hmax(n_recs, 0);
+      std::vector<TraceEnt> tr;
+      if (!rc) {
+        unsigned long long th = 0;
+        if (hipMemcpy(hmax.data(), dmax, n_recs * sizeof(unsigned long long), hipMemcpyDeviceToHost) != hipSuccess ||
+            hipMemcpy(&th, B.trace_head, sizeof th, hipMemcpyDeviceToHost) != hipSuccess) {
+          sh.err = "hipMemcpy";
+          rc = S2LC_EHIP;
+        } else {
+          tr.resize(std::min<unsigned long long>(th, B.trace_cap));
+          if (!tr.empty() && hipMemcpy(tr.data(), B.trace, tr.size() * sizeof(TraceEnt), hipMemcpyDeviceToHost) != hipSuccess) {
+            sh.err = "hipMemcpy";
+            rc = S2LC_EHIP;
+          }
+        }
+      }
+      if (dmax) (void)hipFree(dmax);
+      if (rc) { c->err = sh.err; s2lc_result_free(&r); return rc; }
+      const uint32_t v2 = B.h_res[0].verdict;
+      if (v2 == V_OK) {  // the unreduced search disagrees with the verdict: a checker bug
+        c->err = "the unreduced search found a linearization of an Illegal history";
+        s2lc_result_free(&r);
+        return S2LC_EWITNESS;
+      }
+      out->exact = v2 == V_ILLEGAL ? 1u : 0u;
+      // per op: the largest configuration holding it = the suffix maximum of
+      // its chain's (count -> largest configuration) maxima past its position
+      std::vector<unsigned long long> best(H.n_ops, 0);
+      for (uint32_t q = 0; q < H.K; ++q) {
+        unsigned long long run = 0;
+        for (uint32_t pos = H.chain_start[q + 1] - 1; pos > H.chain_start[q]; --pos) {
+          run = std::max(run, hmax[pos]);  // configurations with count >= pos - start hold the op at pos - 1
+          best[H.rec_op[pos - 1]] = run;
+        }
+      }
+      // each distinct configuration: its path from the trace, rebuilt and certified
+      std::unordered_map<uint32_t, uint32_t> part_of;  // trace id -> partial index
+      std::vector<uint32_t> moves, order;
+      std::vector<uint8_t> ident;
+      for (uint32_t d = 0; d < H.n_ops; ++d) {
+        if (!best[d]) continue;
+        const uint32_t t = (uint32_t)best[d], len = (uint32_t)(best[d] >> 32);
+        auto it = part_of.find(t);
+        if (it != part_of.end()) { op_part[d] = it->second; continue; }
+        moves.clear();
+        bool ok = t != 0xFFFFFFFFu;
+        for (uint32_t x = t, steps = 0; ok && x != TRACE_NONE; ++steps) {
+          if (x >= tr.size() || steps > H.n_ops + 1) { ok = false; break; }
+          if (tr[x].move != 0xFFFFFFFFu) moves.push_back(tr[x].move);  // (LV_NONE: the initial configuration)
+          x = tr[x].parent;
+        }
+        std::reverse(moves.begin(), moves.end());
+        ok = ok && rebuild_linearization(H, moves.data(), (uint32_t)moves.size(), false, order, ident, true) &&
+             order.size() == len && replay_prefix(H, order.data(), ident.data(), order.size());
+        if (!ok) {
+          c->err = "a partial linearization failed CPU-model certification (checker bug)";
+          s2lc_result_free(&r);
+          return S2LC_EWITNESS;
+        }
+        const uint32_t k = (uint32_t)(offs.size() - 1);
+        part_of[t] = k;
+        op_part[d] = k;
+        for (uint32_t x : order) ids.push_back(H.op_ids[x]);
+        offs.push_back(ids.size());
+      }
+    }
+    s2lc_result_free(&r);
+    out->n_partials = (uint32_t)(offs.size() - 1);
+    out->op_ids = (int64_t*)malloc(sizeof(int64_t) * std::max<size_t>(1, H.n_ops));
+    out->op_partial = (uint32_t*)malloc(sizeof(uint32_t) * std::max<size_t>(1, H.n_ops));
+    out->offs = (uint64_t*)malloc(sizeof(uint64_t) * offs.size());
+    out->ids = (int64_t*)malloc(sizeof(int64_t) * std::max<size_t>(1, ids.size()));
+    if (!out->op_ids || !out->op_partial || !out->offs || !out->ids) { s2lc_partials_free(out); return S2LC_ENOMEM; }
+    if (H.n_ops) memcpy(out->op_ids, H.op_ids.data(), sizeof(int64_t) * H.n_ops);
+    if (H.n_ops) memcpy(out->op_partial, op_part.data(), sizeof(uint32_t) * H.n_ops);
+    memcpy(out->offs, offs.data(), sizeof(uint64_t) * offs.size());
+    if (!ids.empty()) memcpy(out->ids, ids.data(), sizeof(int64_t) * ids.size());
+    return 0;
+  } catch (const std::bad_alloc&) {
+    s2lc_result_free(&r);
+    s2lc_partials_free(out);
+    c->err = "out of memory";
+    return S2LC_ENOMEM;
+  }
 }
 
 void s2lc_result_free(s2lc_result* r) {

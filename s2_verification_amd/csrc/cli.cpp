@@ -142,7 +142,14 @@ int main(int argc, char** argv) {
       slog("ERROR", "failed to create temp file", ",\"err\":" + jstr(strerror(errno)));
     } else {
       close(fd);
-      if (s2lc_visualize(h, &r, path.data()) != 0) slog("ERROR", "failed to visualize", ",\"err\":\"write\"");
+      // Illegal: porcupine's LinearizationInfo (the longest partial
+      // linearization containing each op) for the page, as main.go:606-627
+      s2lc_partials info;
+      memset(&info, 0, sizeof info);
+      const bool have_info = r.verdict == S2LC_ILLEGAL && s2lc_check_partials(ctx, h, &info) == 0;
+      if (s2lc_visualize_info(h, &r, have_info ? &info : nullptr, path.data()) != 0)
+        slog("ERROR", "failed to visualize", ",\"err\":\"write\"");
+      s2lc_partials_free(&info);
       slog("INFO", "wrote visualization", ",\"file\":" + jstr(path.data()));
     }
   }

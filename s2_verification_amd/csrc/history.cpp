@@ -139,6 +139,7 @@ int History::finalize() {
   hflags |= H_P4 | H_IDEFER;
   if (nowrap) hflags |= H_NOWRAP;
   if (nowrap && !zero_with_hashes) hflags |= H_P2OK;
+  if (nowrap && total <= 0xFFFFFFFCull) hflags |= H_TAIL32;
 
   // Greedy interval colouring (ops by call order; reuse the chain that
   // finished earliest if it finished before this call): K = max overlap.

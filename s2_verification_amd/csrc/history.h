@@ -36,6 +36,7 @@ enum : uint16_t {
   H_P2OK = 0x2,    // P2: NOWRAP and no 0-record append carries hashes: equal tail => equal hash needed
   H_P4 = 0x4,      // P4: no pending observer left => complete
   H_IDEFER = 0x8,  // indefinite append's identity outcome only when it holds minret
+  H_TAIL32 = 0x10, // sum of all num_records < 2^32 - 3: every reachable tail fits 32 bits (packed kernels)
 };
 
 struct History {

@@ -242,10 +242,11 @@ int level_search(DevBatch& b, uint32_t h, hipStream_t st, const RunOpts& ro, int
   p.trace = b.trace; p.trace_cap = b.trace_cap;
   p.run = run; p.publish = d_pub; p.close_round = 1; p.publish_always = 1;
   p.rcounts = ro.round_counts ? b.rcounts + b.h_moves_off[h] : nullptr;
+  p.pmax = ro.partial_max;  // (every configuration goes through lv_insert: host-driven rounds, no fusion)
 
   // persistent narrow rounds (lv_persist): S2LC_NO_PERSIST=1 turns them off,
   // S2LC_PERSIST_NF sets the widest frontier they take (default: one wave each)
-  bool persist_on = L.grid_persist > 0 && !L.persist_refused && !getenv("S2LC_NO_PERSIST");
+  bool persist_on = L.grid_persist > 0 && !L.persist_refused && !getenv("S2LC_NO_PERSIST") && !ro.partial_max;
   uint32_t persist_nf = L.grid_persist * (LV_BLOCK / 64);
   if (const char* e = getenv("S2LC_PERSIST_NF")) persist_nf = (uint32_t)strtoul(e, nullptr, 10);
   LvPersist pq;
@@ -261,7 +262,7 @@ int level_search(DevBatch& b, uint32_t h, hipStream_t st, const RunOpts& ro, int
   // combined in L2); S2LC_WIDE_FUSED=1: lv_round inserts as it expands (CAS
   // first, so a duplicate is never written; measured slower on C5 / C5wide:
   // its write-through stores cost more HBM writes than the duplicates do)
-  const uint32_t fused_wide = getenv("S2LC_WIDE_FUSED") ? 1u : 0u;
+  const uint32_t fused_wide = (getenv("S2LC_WIDE_FUSED") && !ro.partial_max) ? 1u : 0u;
   {
     int dev = 0, khz = 100000;
     LVCHK(hipGetDevice(&dev));

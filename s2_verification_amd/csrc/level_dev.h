@@ -155,6 +155,10 @@ struct LvParams {
   uint8_t* send;         // bucketed configurations, owner-major
   uint64_t own_off[8];   // first configuration of each owner's bucket in send
   unsigned long long* prof;  // S2LC_PROF builds: lv_round phase cycles (nullable)
+  // per-op longest partial linearizations (s2lc_check_partials): for every
+  // inserted configuration c and chain j, pmax[cs[j] + cnt_c[j]] = max of
+  // (|c| << 32 | c's trace id), |c| = its linearized ops (nullable)
+  unsigned long long* pmax;
 };
 
 template <int NQ>
@@ -1212,6 +1216,12 @@ __global__ __launch_bounds__(LV_BLOCK) void lv_insert(LvParams p) {
       if (wit) {
         c->trace = p.tgid + tbase + n;
         p.trace[tbase + n] = TraceEnt{c->ptrace, c->move};
+      }
+      if (p.pmax) {  // LinearizationInfo: this configuration as the longest one holding each chain's prefix
+        uint32_t size = 0;
+        for (uint32_t j = 0; j < p.K; ++j) size += c->cnt[j];
+        const unsigned long long v = ((unsigned long long)size << 32) | (wit ? c->trace : 0xFFFFFFFFu);
+        for (uint32_t j = 0; j < p.K; ++j) atomicMax(&p.pmax[p.cs[j] + c->cnt[j]], v);
       }
     }
   }

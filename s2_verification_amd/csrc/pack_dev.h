@@ -60,9 +60,6 @@ constexpr size_t pack_group_bytes() { return 2 * PACK_F * sizeof(PCfg<L>); }
 
 template <int L>
 constexpr size_t pack_smem_bytes() { return (PACK_BLOCK / L) * pack_group_bytes<L>(); }
-// the frontiers, then every wave's record windows (ChainLane)
-template <int L>
-constexpr size_t pack_lds_bytes() { return pack_smem_bytes<L>() + (PACK_BLOCK / 64) * 4 * 4 * 1024; }
 
 // LDS accesses of one wave execute in program order; this keeps the compiler
 // from reordering them across lanes (a store by lane a, a load by lane b).
@@ -118,152 +115,118 @@ __device__ __forceinline__ uint64_t bcast_u64(uint64_t v, int src) {
   return ((uint64_t)bcast_u32((uint32_t)(v >> 32), src) << 32) | bcast_u32((uint32_t)v, src);
 }
 
-// Per-lane view of chain l of the group's history through a window of PACK_W
-// consecutive records held in LDS. A refill is PACK_W x 4 LDS-DMA loads
-// (global_load_lds_dwordx4: 16 bytes per lane straight into LDS, no VGPRs);
-// a closure pass then reads only the head's hot 48 bytes from LDS, where a
-// register window cost 64 VGPRs and a 48-instruction select per pass.
-// LDS image per wave: piece k (record slot k / 4, quarter k % 4) of lane l at
-// wv + k * 1024 + l * 16 (what one glds wave-instruction writes: lane-linear).
+// Per-lane view of chain l of the group's history with a register window of
+// PACK_W consecutive records. A closure that advances a chain by several
+// identity ops, and the next rounds' expansions, read them from registers: a
+// window refill issues PACK_W independent loads (one memory latency) where a
+// one-record cache paid one dependent latency per advanced op.
 constexpr int PACK_W = 4;
-constexpr uint32_t PACK_WIN_WAVE = PACK_W * 4 * 1024;  // LDS bytes per wave
-typedef __attribute__((address_space(3))) void lds_void_t;
-typedef __attribute__((address_space(1))) const void gbl_void_t;
-
-// The fields of a head record a closure pass reads (bytes 16..63 of OpRec).
-struct HotRec {
-  uint64_t out_tail, out_hash, sufmin;
-  uint32_t call_ev, ret_ev, hash_off, hash_cnt, toks, flags;
-};
-
 struct ChainLane {
   const OpRec* __restrict__ base;  // first record of chain l (valid iff on)
   bool on;                         // l < K
   uint32_t len;                    // records of chain l, its sentinel included
   uint32_t w0;                     // count of the window's first record
-  uint8_t* wv;                     // this wave's window image (wave-uniform)
-  uint32_t lo;                     // this lane's byte offset in a piece (lane * 16)
+  uint32_t cc;                     // count of r
+  uint4 wa[4], wb[4], wc[4], wd[4];  // window: records at counts w0 .. w0+3
+  OpRec r;                         // record at count cc (null record when !on)
 #ifdef S2LC_PROF
   bool refilled;                   // the last at() reloaded the window
 #endif
-  __device__ __forceinline__ void reset(const OpRec* b, bool on_, uint32_t len_, uint8_t* wv_, int lane) {
+  __device__ __forceinline__ void reset(const OpRec* b, bool on_, uint32_t len_) {
     base = b;
     on = on_;
     len = len_;
-    wv = wv_;
-    lo = (uint32_t)lane * 16u;
     w0 = 0xFFFF0000u;
-    if (!on) {
-      // a lane past K reads a null record at count 0 forever
-      w0 = 0;
-      uint4* q = reinterpret_cast<uint4*>(wv + lo);
-      q[0 * 64] = make_uint4(0, 0, 0, 0);
-      q[1 * 64] = make_uint4(0, 0, 0, 0);                                   // out_tail, out_hash
-      q[2 * 64] = make_uint4(0xFFFFFFFFu, 0xFFFFFFFFu, EV_INF, EV_INF);     // sufmin = REQ_NONE, call, ret
-      q[3 * 64] = make_uint4(0, 0, 0, OPF_SENTINEL);                        // hash_off, hash_cnt, toks, flags
-    }
+    cc = 0xFFFFFFFFu;
+    r.num_records = 0; r.msn = 0; r.out_tail = 0; r.out_hash = 0;
+    r.sufmin = REQ_NONE; r.call_ev = EV_INF; r.ret_ev = EV_INF;
+    r.hash_off = 0; r.hash_cnt = 0; r.batch_tok = 0; r.set_tok = 0;
+    r.flags = OPF_SENTINEL;
   }
-  // byte offset of count c's record (slot) in the image, refilling the window first if needed
-  __device__ __forceinline__ uint32_t at(uint32_t c) {
+  __device__ __forceinline__ void at(uint32_t c) {
 #ifdef S2LC_PROF
     refilled = false;
 #endif
+    if (!on || c == cc) return;
     uint32_t o = c - w0;
-    if (on && o >= (uint32_t)PACK_W) {
+    if (o >= (uint32_t)PACK_W) {
 #ifdef S2LC_PROF
       refilled = true;
 #endif
-      // records c .. c+3, clamped to the chain (its sentinel is its last record)
+      // clamp to the chain: a record past its sentinel is never selected
+      const OpRec* q = base + c;
       const uint32_t last = len - 1 - c;  // c < len always (sentinel included)
+      const uint4* qa = reinterpret_cast<const uint4*>(q);
+      const uint4* qb = reinterpret_cast<const uint4*>(q + min(1u, last));
+      const uint4* qc = reinterpret_cast<const uint4*>(q + min(2u, last));
+      const uint4* qd = reinterpret_cast<const uint4*>(q + min(3u, last));
 #pragma unroll
-      for (int k = 0; k < PACK_W; ++k) {
-        const uint8_t* q = reinterpret_cast<const uint8_t*>(base + c + min((uint32_t)k, last));
-#pragma unroll
-        for (int x = 0; x < 4; ++x)
-          __builtin_amdgcn_global_load_lds((gbl_void_t*)(q + 16 * x), (lds_void_t*)(wv + (4 * k + x) * 1024), 16, 0, 0);
-      }
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      for (int k = 0; k < 4; ++k) { wa[k] = qa[k]; wb[k] = qb[k]; wc[k] = qc[k]; wd[k] = qd[k]; }
       w0 = c;
       o = 0;
     }
-    return o * 4096u + lo;
-  }
-  __device__ __forceinline__ HotRec hot(uint32_t c) {
-    const uint32_t off = at(c);
-    const uint4 a = *reinterpret_cast<const uint4*>(wv + off + 1024);
-    const uint4 b = *reinterpret_cast<const uint4*>(wv + off + 2048);
-    const uint4 d = *reinterpret_cast<const uint4*>(wv + off + 3072);
-    HotRec r;
-    r.out_tail = (uint64_t)a.x | ((uint64_t)a.y << 32);
-    r.out_hash = (uint64_t)a.z | ((uint64_t)a.w << 32);
-    r.sufmin = (uint64_t)b.x | ((uint64_t)b.y << 32);
-    r.call_ev = b.z; r.ret_ev = b.w;
-    r.hash_off = d.x; r.hash_cnt = d.y; r.toks = d.z; r.flags = d.w;
-    return r;
-  }
-  __device__ __forceinline__ OpRec full(uint32_t c) {
-    const uint32_t off = at(c);
-    uint4 v[4];
+    // select dword-wise in registers (a struct-typed select goes through scratch)
+    uint4 sel[4];
 #pragma unroll
-    for (int x = 0; x < 4; ++x) v[x] = *reinterpret_cast<const uint4*>(wv + off + 1024 * x);
-    OpRec r;
-    __builtin_memcpy(&r, v, sizeof(OpRec));
-    return r;
+    for (int k = 0; k < 4; ++k) {
+      const uint4 A = wa[k], B = wb[k], C = wc[k], D = wd[k];
+      sel[k].x = o == 0 ? A.x : o == 1 ? B.x : o == 2 ? C.x : D.x;
+      sel[k].y = o == 0 ? A.y : o == 1 ? B.y : o == 2 ? C.y : D.y;
+      sel[k].z = o == 0 ? A.z : o == 1 ? B.z : o == 2 ? C.z : D.z;
+      sel[k].w = o == 0 ? A.w : o == 1 ? B.w : o == 2 ? C.w : D.w;
+    }
+    __builtin_memcpy(&r, sel, sizeof(OpRec));
+    cc = c;
   }
 };
 
-// One closure pass of one configuration (state s, lane count cnt) under
-// minimal, legal identity ops + P1/P2/P4: CL_MORE when some chain advanced
-// (cnt moved), else the closure's result CL_* with the exact minret.
-constexpr int CL_MORE = -1;
+// Group closure of one configuration (state s, lane count cnt) under minimal,
+// legal identity ops + P1/P2/P4; returns CL_* and the exact minret.
 template <int L>
-__device__ __forceinline__ int pack_pass(ChainLane& ch, uint32_t& cnt, const State& s, uint32_t hflags,
-                                         uint64_t gmask, uint32_t& minret_out, HotRec& r_out,
-                                         unsigned long long* prof_pass = nullptr) {
+__device__ __forceinline__ int pack_closure(ChainLane& ch, const uint64_t* __restrict__ pool, uint32_t& cnt,
+                                            const State& s, uint32_t hflags,
+                                            uint64_t gmask, uint32_t& minret_out,
+                                            unsigned long long* prof_pass = nullptr) {
   const bool nowrap = hflags & H_NOWRAP;
   const bool p2 = hflags & H_P2OK;
   const bool p4 = hflags & H_P4;
-  const HotRec r = ch.hot(cnt);
-#ifdef S2LC_PROF
-  if (prof_pass) {  // [0] passes, [1] passes that reloaded a window (the group waited on memory)
-    prof_pass[0]++;
-    if (__ballot(ch.refilled) & gmask) prof_pass[1]++;
-  }
-#endif
-  const uint32_t minret = gmin_u32<L>(r.ret_ev);
-  const uint64_t bound = gmin_u64<L>(r.sufmin);
-  const uint32_t f = r.flags;
-  const bool minimal_e = (f & OPF_CLS_E) && r.call_ev < minret;
-  bool legal = false, dead = false;
-  if (minimal_e) {
-    legal = true;
-    if ((f & OPF_KIND_MASK) != 0) {
-      const bool hash_bad = (f & OPF_HAS_HASH) && s.hash != r.out_hash;
-      const bool tail_bad = !(f & OPF_FAIL) && s.tail != r.out_tail;
-      legal = !hash_bad && !tail_bad;
-      // P2: a minimal successful read at this tail with another hash can never pass
-      dead = p2 && hash_bad && !(f & OPF_FAIL) && r.out_tail == s.tail;
-    }
-  }
-  minret_out = minret;
-  r_out = r;
-  if ((__ballot(dead) & gmask) || (nowrap && s.tail > bound)) return CL_DEAD;
-  if (!(__ballot(legal) & gmask)) {
-    if (minret == EV_INF) return CL_COMPLETE;
-    return (p4 && bound == REQ_NONE) ? CL_P4 : CL_ALIVE;
-  }
-  cnt += legal ? 1u : 0u;
-  return CL_MORE;
-}
-
-// The whole closure (round 0's initial configuration).
-template <int L>
-__device__ __forceinline__ int pack_closure(ChainLane& ch, uint32_t& cnt, const State& s, uint32_t hflags,
-                                            uint64_t gmask, uint32_t& minret_out) {
-  HotRec r;
   for (;;) {
-    const int cr = pack_pass<L>(ch, cnt, s, hflags, gmask, minret_out, r);
-    if (cr != CL_MORE) return cr;
+    ch.at(cnt);
+#ifdef S2LC_PROF
+    if (prof_pass) {  // [0] passes, [1] passes that reloaded a window (the group waited on memory)
+      prof_pass[0]++;
+      if (__ballot(ch.refilled) & gmask) prof_pass[1]++;
+    }
+#endif
+    const OpRec& r = ch.r;
+    const uint32_t minret = gmin_u32<L>(r.ret_ev);
+    // P1 bound in 32 bits (H_TAIL32 histories only: every reachable tail is
+    // below 2^32 - 3): REQ_NONE -> 0xFFFFFFFF, REQ_HASH_ONLY -> 0xFFFFFFFE, a
+    // larger requirement (never reachable) -> 0xFFFFFFFD; one DPP min per step
+    const uint32_t s_lo = (uint32_t)r.sufmin, s_hi = (uint32_t)(r.sufmin >> 32);
+    const uint32_t b32 = s_hi == 0 ? min(s_lo, 0xFFFFFFFDu)
+                         : s_hi == 0xFFFFFFFFu && s_lo >= 0xFFFFFFFEu ? s_lo : 0xFFFFFFFDu;
+    const uint32_t bound = gmin_u32<L>(b32);
+    const uint32_t f = r.flags;
+    const bool minimal_e = (f & OPF_CLS_E) && r.call_ev < minret;
+    bool legal = false, dead = false;
+    if (minimal_e) {
+      legal = true;
+      if ((f & OPF_KIND_MASK) != 0) {
+        const bool hash_bad = (f & OPF_HAS_HASH) && s.hash != r.out_hash;
+        const bool tail_bad = !(f & OPF_FAIL) && s.tail != r.out_tail;
+        legal = !hash_bad && !tail_bad;
+        // P2: a minimal successful read at this tail with another hash can never pass
+        dead = p2 && hash_bad && !(f & OPF_FAIL) && r.out_tail == s.tail;
+      }
+    }
+    minret_out = minret;
+    if ((__ballot(dead) & gmask) || (nowrap && s.tail > (uint64_t)bound)) return CL_DEAD;
+    if (!(__ballot(legal) & gmask)) {
+      if (minret == EV_INF) return CL_COMPLETE;
+      return (p4 && bound == 0xFFFFFFFFu) ? CL_P4 : CL_ALIVE;
+    }
+    cnt += legal ? 1u : 0u;
   }
 }
 
@@ -295,7 +258,6 @@ __global__ __launch_bounds__(PACK_BLOCK, S2LC_PACK_MINW) void pack_kernel(Params
   const int gbase = lane & ~(L - 1);       // first wave lane of the group
   const uint64_t gmask = (L == 64 ? ~0ull : ((1ull << L) - 1)) << gbase;
   C* const fr = reinterpret_cast<C*>(smem + (threadIdx.x / L) * pack_group_bytes<L>());
-  uint8_t* const wv = smem + pack_smem_bytes<L>() + (threadIdx.x / 64) * PACK_WIN_WAVE;  // this wave's record windows
 
   uint32_t tbase = 0, tleft = 0;  // group's trace chunk (uniform)
   for (;;) {
@@ -317,7 +279,7 @@ __global__ __launch_bounds__(PACK_BLOCK, S2LC_PACK_MINW) void pack_kernel(Params
     const uint32_t cs = on ? p.chain_start[hd.cs_base + gl] : 0u;
     const uint32_t ce = on ? p.chain_start[hd.cs_base + gl + 1] : 0u;
     ChainLane ch;
-    ch.reset(p.recs + cs, on, ce - cs, wv, lane);
+    ch.reset(p.recs + cs, on, ce - cs);
     bool witness_ok = p.witness != 0;
     // the first record hashes of this lane's head in the next round's first
     // configuration, loaded right after that configuration's closure so the
@@ -327,9 +289,13 @@ __global__ __launch_bounds__(PACK_BLOCK, S2LC_PACK_MINW) void pack_kernel(Params
     uint32_t pf_cc = 0xFFFFFFFFu;
     // witness moves: while every round leaves exactly one configuration the
     // path is the sequence of those configurations' moves, written as the
-    // rounds go; otherwise lane 0 walks the parent chain at the end
+    // rounds go (rounds 1 .. lin_len); from the first round that keeps several
+    // configurations on, their trace entries are written and lane 0 walks the
+    // parent chain at the end, down to round lin_len + 1. A history that stays
+    // linear (93 % of C4) writes no trace entry at all.
     uint32_t* const wout = p.moves ? p.moves + p.res[h].witness_off : nullptr;
     bool linear = wout != nullptr;
+    uint32_t lin_len = 0;
 
     uint32_t verdict = V_ILLEGAL, reason = S2LC_R_SEARCH_EXHAUSTED;
     uint32_t found_parent = TRACE_NONE, found_move = TRACE_NONE, found_p4 = 0;
@@ -343,7 +309,7 @@ __global__ __launch_bounds__(PACK_BLOCK, S2LC_PACK_MINW) void pack_kernel(Params
     {
       uint32_t cnt = 0, mr = 0;
       const State s0{0, 0, 0};
-      const int cr = pack_closure<L>(ch, cnt, s0, hd.flags, gmask, mr);
+      const int cr = pack_closure<L>(ch, p.pool, cnt, s0, hd.flags, gmask, mr);
       if (cr == CL_DEAD) {
         nf = 0;
       } else if (cr != CL_ALIVE) {
@@ -371,123 +337,98 @@ __global__ __launch_bounds__(PACK_BLOCK, S2LC_PACK_MINW) void pack_kernel(Params
       C* const nxt = fr + (1 - cur) * PACK_F;
       uint32_t nn = 0;
       bool found = false, overflow = false;
-      // The round is ONE loop of closure passes: a group goes on to its next
-      // child (or its next configuration) in the iteration after the current
-      // child's closure ends. The groups of a wave run in lockstep, so a wave
-      // pays the largest per-group SUM of passes, not (most children) x (most
-      // passes) as nested child / pass loops would.
-      uint32_t f = 0;
-      bool need_cfg = true, in_child = false;
-      State s{0, 0, 0}, opt{0, 0, 0}, ks{0, 0, 0};
-      uint32_t pmin = 0, ptrace = 0, pcnt = 0, cnt = 0, mv = 0;
-      uint64_t mo = 0, mi = 0;
-      for (;;) {
-        if (!need_cfg && !in_child) {
-          if ((mo | mi) == 0) {  // this configuration's children are done
-            ++f;
-            need_cfg = true;
+      for (uint32_t f = 0; f < nf && !found && !overflow; ++f) {
+        const C& pc = curf[f];
+        const State s{pc.tail, pc.hash, pc.tok};
+        const uint32_t pmin = pc.minret;
+        const uint32_t ptrace = pc.trace;
+        const uint32_t pcnt = on ? pc.cnt[gl] : 0u;
+        PK_T0();
+        // expand: lane l tries the head of chain l
+        ch.at(pcnt);
+        const OpRec& r = ch.r;
+        const bool cand = on && !(r.flags & (OPF_SENTINEL | OPF_CLS_E)) && r.call_ev < pmin;
+        bool take_opt = false, take_id = false;
+        State opt = s;
+        if (cand) {
+          const bool g = append_guards_ok(r, s);
+          opt.tail = s.tail + r.num_records;
+          opt.tok = r.set_tok ? r.set_tok : s.tok;
+          if (r.flags & OPF_CLS_D) {
+            take_opt = g && opt.tail == r.out_tail;
           } else {
-            // the next child, straight from the producing lane
-            const bool is_id = mo == 0;
-            const uint64_t m = is_id ? mi : mo;
-            const int src = __ffsll((unsigned long long)m) - 1;
-            if (is_id) mi &= mi - 1; else mo &= mo - 1;
-            const int j = src - gbase;
-            ks.tail = bcast_u64(is_id ? s.tail : opt.tail, src);
-            ks.hash = bcast_u64(is_id ? s.hash : opt.hash, src);
-            ks.tok = bcast_u32(is_id ? s.tok : opt.tok, src);
-            cnt = pcnt + (gl == j ? 1u : 0u);
-            mv = is_id ? ((uint32_t)j | MOVE_IDENT) : (uint32_t)j;
-            in_child = true;
+            take_opt = g;
           }
-        }
-        if (need_cfg) {
-          if (f >= nf || found || overflow) break;
-          const C& pc = curf[f];
-          s = State{pc.tail, pc.hash, pc.tok};
-          pmin = pc.minret;
-          ptrace = pc.trace;
-          pcnt = on ? pc.cnt[gl] : 0u;
-          PK_T0();
-        }
-        if (need_cfg) {
-          // expand: lane l tries the head of chain l (its children are taken
-          // from the next iteration on)
-          const OpRec r = ch.full(pcnt);
-          const bool cand = on && !(r.flags & (OPF_SENTINEL | OPF_CLS_E)) && r.call_ev < pmin;
-          bool take_opt = false, take_id = false;
-          opt = s;
-          if (cand) {
-            const bool g = append_guards_ok(r, s);
-            opt.tail = s.tail + r.num_records;
-            opt.tok = r.set_tok ? r.set_tok : s.tok;
-            if (r.flags & OPF_CLS_D) {
-              take_opt = g && opt.tail == r.out_tail;
-            } else {
-              take_opt = g;
-            }
-            if (take_opt) {
-              if (f == 0 && pcnt == pf_cc)
-                opt.hash = fold_hashes_pf(s.hash, pf, p.pool + r.hash_off, r.hash_cnt);
-              else
-                opt.hash = fold_hashes_blk(s.hash, p.pool + r.hash_off, r.hash_cnt);
-            }
-            if (r.flags & OPF_CLS_I) take_id = (!idefer || r.ret_ev == pmin) && !(g && state_eq(opt, s));
+          if (take_opt) {
+            if (f == 0 && pcnt == pf_cc)
+              opt.hash = fold_hashes_pf(s.hash, pf, p.pool + r.hash_off, r.hash_cnt);
+            else
+              opt.hash = fold_hashes_blk(s.hash, p.pool + r.hash_off, r.hash_cnt);
           }
-          PK_LAP(0);
-          mo = __ballot(take_opt) & gmask;
-          mi = __ballot(take_id) & gmask;
-          children += __popcll(mo) + __popcll(mi);
-          need_cfg = false;
-          continue;
+          if (r.flags & OPF_CLS_I) take_id = (!idefer || r.ret_ev == pmin) && !(g && state_eq(opt, s));
         }
-        uint32_t mr = 0;
-        HotRec hr;  // the head at cnt (the pass's)
+        PK_LAP(0);
+        uint64_t mo = __ballot(take_opt) & gmask;
+        uint64_t mi = __ballot(take_id) & gmask;
+        children += __popcll(mo) + __popcll(mi);
+        // consume the children one at a time: close, dedupe, insert
+        while ((mo | mi) && !found && !overflow) {
+          const bool is_id = mo == 0;
+          const uint64_t m = is_id ? mi : mo;
+          const int src = __ffsll((unsigned long long)m) - 1;
+          if (is_id) mi &= mi - 1; else mo &= mo - 1;
+          const int j = src - gbase;
+          State ks;
+          ks.tail = bcast_u64(is_id ? s.tail : opt.tail, src);
+          ks.hash = bcast_u64(is_id ? s.hash : opt.hash, src);
+          ks.tok = bcast_u32(is_id ? s.tok : opt.tok, src);
+          uint32_t cnt = pcnt + (gl == j ? 1u : 0u);
+          uint32_t mr = 0;
+          PK_LAP(2);
 #ifdef S2LC_PROF
-        const int cr = pack_pass<L>(ch, cnt, ks, hd.flags, gmask, mr, hr, pk_pass);
+          const int cr = pack_closure<L>(ch, p.pool, cnt, ks, hd.flags, gmask, mr, pk_pass);
 #else
-        const int cr = pack_pass<L>(ch, cnt, ks, hd.flags, gmask, mr, hr);
+          const int cr = pack_closure<L>(ch, p.pool, cnt, ks, hd.flags, gmask, mr);
 #endif
-        PK_LAP(1);
-        if (cr == CL_MORE) continue;
-        in_child = false;
-        if (cr == CL_ALIVE && nn == 0) {
-          // this child becomes the next round's first configuration: start
-          // loading its candidate heads' record hashes now
-          pf_cc = 0xFFFFFFFFu;
-          if (on && !(hr.flags & (OPF_SENTINEL | OPF_CLS_E)) && hr.call_ev < mr) {
-            const uint64_t* src = p.pool + hr.hash_off;
+          if (cr == CL_ALIVE && nn == 0) {
+            // this child becomes the next round's first configuration: start
+            // loading its candidate heads' record hashes now
+            const OpRec& hr = ch.r;  // the head at cnt (the closure's last pass selected it)
+            pf_cc = 0xFFFFFFFFu;
+            if (on && !(hr.flags & (OPF_SENTINEL | OPF_CLS_E)) && hr.call_ev < mr) {
+              const uint64_t* src = p.pool + hr.hash_off;
 #pragma unroll
-            for (int q = 0; q < PACK_PF; ++q) pf[q] = (uint32_t)q < hr.hash_cnt ? src[q] : 0ull;
-            pf_cc = cnt;
+              for (int q = 0; q < PACK_PF; ++q) pf[q] = (uint32_t)q < hr.hash_cnt ? src[q] : 0ull;
+              pf_cc = cnt;
+            }
           }
+          PK_LAP(1);
+          const uint32_t mv = is_id ? ((uint32_t)j | MOVE_IDENT) : (uint32_t)j;
+          if (cr == CL_COMPLETE || cr == CL_P4) {
+            found = true;
+            found_parent = ptrace; found_move = mv; found_p4 = cr == CL_P4;
+            break;
+          }
+          if (cr == CL_DEAD) continue;
+          // dedupe against the next frontier
+          bool dup = false;
+          for (uint32_t e = 0; e < nn; ++e) {
+            const C& o = nxt[e];
+            if (o.tail != ks.tail || o.hash != ks.hash || o.tok != ks.tok) continue;
+            const bool ne = on && o.cnt[gl] != (uint16_t)cnt;
+            if (!(__ballot(ne) & gmask)) { dup = true; break; }
+          }
+          if (dup) continue;
+          if (nn == PACK_F) { overflow = true; break; }
+          C& o = nxt[nn];
+          if (gl == 0) {
+            o.tail = ks.tail; o.hash = ks.hash; o.tok = ks.tok; o.minret = mr;
+            o.ptrace = ptrace; o.move = mv;
+          }
+          o.cnt[gl] = on ? (uint16_t)cnt : 0;
+          wave_lds_sync();
+          ++nn;
         }
-        if (cr == CL_COMPLETE || cr == CL_P4) {
-          found = true;
-          found_parent = ptrace; found_move = mv; found_p4 = cr == CL_P4;
-          need_cfg = true;  // (the next iteration leaves the round)
-          continue;
-        }
-        if (cr == CL_DEAD) continue;
-        // dedupe against the next frontier
-        bool dup = false;
-        for (uint32_t e = 0; e < nn; ++e) {
-          const C& o = nxt[e];
-          if (o.tail != ks.tail || o.hash != ks.hash || o.tok != ks.tok) continue;
-          const bool ne = on && o.cnt[gl] != (uint16_t)cnt;
-          if (!(__ballot(ne) & gmask)) { dup = true; break; }
-        }
-        if (dup) continue;
-        if (nn == PACK_F) { overflow = true; need_cfg = true; continue; }
-        C& o = nxt[nn];
-        if (gl == 0) {
-          o.tail = ks.tail; o.hash = ks.hash; o.tok = ks.tok; o.minret = mr;
-          o.ptrace = ptrace; o.move = mv;
-        }
-        o.cnt[gl] = on ? (uint16_t)cnt : 0;
-        wave_lds_sync();
-        ++nn;
-        PK_LAP(2);
       }
       PK_LAP(2);
       if (found) { verdict = V_OK; reason = 0; rounds++; break; }
@@ -495,6 +436,7 @@ __global__ __launch_bounds__(PACK_BLOCK, S2LC_PACK_MINW) void pack_kernel(Params
       rounds++;
       if (rc && gl == 0) rc[rounds] = nn;
       if (linear && nn == 1 && gl == 0) wout[rounds - 1] = nxt[0].move;
+      if (linear && nn == 1) lin_len = rounds;
       if (nn > 1) linear = false;
       if (nn == 0) {
         verdict = V_ILLEGAL; reason = S2LC_R_SEARCH_EXHAUSTED;
@@ -504,7 +446,7 @@ __global__ __launch_bounds__(PACK_BLOCK, S2LC_PACK_MINW) void pack_kernel(Params
       }
       // trace entries (parent, move) of the surviving configurations
       uint32_t tb = TRACE_NONE;
-      if (witness_ok) {
+      if (witness_ok && !linear) {
         if (tleft < nn) {
           unsigned long long b = 0;
           if (gl == 0) b = atomicAdd(p.trace_head, (unsigned long long)TRACE_CHUNK);
@@ -550,9 +492,11 @@ __global__ __launch_bounds__(PACK_BLOCK, S2LC_PACK_MINW) void pack_kernel(Params
       R.final_parent = (verdict == V_OK && witness_ok) ? found_parent : TRACE_NONE;
       R.final_move = found_move;
       R.witness_len = 0;
-      R.deep_trace = (verdict == V_ILLEGAL && witness_ok) ? deep_trace : TRACE_NONE;
+      // (a history linear to the end has its whole path in wout already: no trace entry)
+      const bool deep = verdict == V_ILLEGAL && witness_ok && (linear ? deep_len > 0 : deep_trace != TRACE_NONE);
+      R.deep_trace = deep ? (linear ? 0u : deep_trace) : TRACE_NONE;
       R.deep_len = deep_len;
-      const bool want = (verdict == V_OK || R.deep_trace != TRACE_NONE) && witness_ok;
+      const bool want = (verdict == V_OK || deep) && witness_ok;
       uint32_t hw = 0;
       if (want && wout) {
         // Ok: the completing move after the path to its parent; Illegal: the
@@ -572,12 +516,14 @@ __global__ __launch_bounds__(PACK_BLOCK, S2LC_PACK_MINW) void pack_kernel(Params
         if (linear) {
           pos = 0;  // rounds 1 .. len-1 (Ok) / 1 .. len (Illegal) were written as they closed
         } else {
-          while (pos > 0 && idx != TRACE_NONE) {
+          // rounds lin_len + 1 .. pos from the trace (the ones before were written as they closed)
+          while (pos > lin_len && idx != TRACE_NONE) {
             const TraceEnt e = p.trace[idx];
             wout[--pos] = e.move;
             idx = e.parent;
           }
         }
+        if (!linear && pos == lin_len) pos = 0;
         hw = pos == 0 ? 1u : 0u;
         R.witness_len = hw ? len : 0u;
       } else if (want) {

@@ -115,7 +115,6 @@ struct DevBatch {
   uint32_t n_pack8 = 0, n_pack16 = 0, n_pack32 = 0;  // packed-kernel lists (order[]: pack8 | pack16 | pack32)
   uint32_t pack8_kmax = 8;                            // K bound of the pack8 list (0: none)
   int pack_bpc[3] = {0, 0, 0};                        // resident pack_kernel<8/16/32> blocks per CU (0: not queried)
-  bool pack_attr[3] = {false, false, false};          // pack_kernel<8/16/32>: dynamic-LDS limit raised
   uint64_t n_ops_total = 0;                           // ops over the uploaded histories
   std::vector<uint32_t> lpt;        // searchable histories, longest (n_ops x K) first
   std::vector<uint64_t> h_in_bytes; // per history: input SoA bytes (48 per op + 8 per record hash)
@@ -148,6 +147,7 @@ struct RunOpts {
   bool round_counts = false;
   uint32_t engine = 0;               // s2lc_engine
   uint64_t timeout_us = 0;           // 0 = none
+  unsigned long long* partial_max = nullptr;  // level search only: per-record longest-partial maxima (LvParams::pmax)
 };
 
 struct RunStats {

@@ -277,12 +277,15 @@ int batch_upload(DevBatch& b, const std::vector<const History*>& hs, uint32_t re
       if (c < top32 && b.h_hist[i].K > k8 && b.h_hist[i].K <= 16) { to32[i] = 1; ++c; }
   }
   b.pack8_kmax = k8;
+  // (the packed kernels keep tail bounds in 32 bits: histories whose tails
+  // can pass 2^32 take the workgroup engine)
+  auto t32 = [&](uint32_t i) { return (b.h_hist[i].flags & H_TAIL32) != 0; };
   uint32_t no = 0;
-  for (uint32_t i : b.lpt) if (b.h_hist[i].K <= k8) s_order[no++] = i;
+  for (uint32_t i : b.lpt) if (b.h_hist[i].K <= k8 && t32(i)) s_order[no++] = i;
   b.n_pack8 = no;
-  for (uint32_t i : b.lpt) if (b.h_hist[i].K > k8 && b.h_hist[i].K <= 16 && !to32[i]) s_order[no++] = i;
+  for (uint32_t i : b.lpt) if (b.h_hist[i].K > k8 && b.h_hist[i].K <= 16 && !to32[i] && t32(i)) s_order[no++] = i;
   b.n_pack16 = no - b.n_pack8;
-  for (uint32_t i : b.lpt) if ((b.h_hist[i].K > 16 && b.h_hist[i].K <= 32) || to32[i]) s_order[no++] = i;
+  for (uint32_t i : b.lpt) if (((b.h_hist[i].K > 16 && b.h_hist[i].K <= 32) || to32[i]) && t32(i)) s_order[no++] = i;
   b.n_pack32 = no - b.n_pack8 - b.n_pack16;
   HIPCHK(hipMemcpy(b.arena, b.stage, stage_bytes, hipMemcpyHostToDevice));
   return 0;
@@ -385,7 +388,7 @@ int batch_run(DevBatch& b, hipStream_t stream, const RunOpts& ro, RunStats& st, 
   for (uint32_t i : b.lpt) {
     const uint32_t K = b.h_hist[i].K;
     if (engine == S2LC_ENGINE_LEVEL || K > 128 || (midk_level && K > 32)) level.push_back(i);
-    else if (!use_pack || K > 32) todo.push_back(i);
+    else if (!use_pack || K > 32 || !(b.h_hist[i].flags & H_TAIL32)) todo.push_back(i);
   }
   // histories settled by pack_kernel<8> / <16> (roofline accounting of those kernels)
   std::vector<uint8_t> pack_done(b.n_hist, 0);  // 8 or 16: the kernel that settled it
@@ -413,13 +416,7 @@ int batch_run(DevBatch& b, hipStream_t stream, const RunOpts& ro, RunStats& st, 
       pp.n_hist = n_l;
       pp.counter = b.counter + 12 + li;
       const uint32_t L = 8u << li;
-      const size_t smem = li == 0 ? pack_lds_bytes<8>() : li == 1 ? pack_lds_bytes<16>() : pack_lds_bytes<32>();
-      if (!b.pack_attr[li]) {  // more than 64 KiB of dynamic LDS per workgroup
-        if (li == 0) HIPCHK(hipFuncSetAttribute((const void*)pack_kernel<8>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)smem));
-        else if (li == 1) HIPCHK(hipFuncSetAttribute((const void*)pack_kernel<16>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)smem));
-        else HIPCHK(hipFuncSetAttribute((const void*)pack_kernel<32>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)smem));
-        b.pack_attr[li] = true;
-      }
+      const size_t smem = li == 0 ? pack_smem_bytes<8>() : li == 1 ? pack_smem_bytes<16>() : pack_smem_bytes<32>();
       int bpc = b.pack_bpc[li];  // resident blocks per CU (queried once per batch)
       if (bpc == 0) {
         if (li == 0) HIPCHK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&bpc, pack_kernel<8>, PACK_BLOCK, smem));
@@ -466,7 +463,7 @@ int batch_run(DevBatch& b, hipStream_t stream, const RunOpts& ro, RunStats& st, 
     std::vector<uint32_t> over;
     for (uint32_t i : b.lpt) {
       const uint32_t K = b.h_hist[i].K;
-      if (K > 32) continue;
+      if (K > 32 || !(b.h_hist[i].flags & H_TAIL32)) continue;
       if (b.h_res[i].verdict == V_UNKNOWN && b.h_res[i].reason == S2LC_R_FRONTIER) over.push_back(i);
       else if (K <= b.pack8_kmax) pack_done[i] = 8;
       else if (K <= 16) pack_done[i] = 16;

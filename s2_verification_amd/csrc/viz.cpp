@@ -78,7 +78,18 @@ std::string html_esc(const std::string& s) {
 
 using namespace s2lc;
 
+static int render(const s2lc_history* hh, const s2lc_result* r, const s2lc_partials* info, const char* path);
+
 extern "C" int s2lc_visualize(const s2lc_history* hh, const s2lc_result* r, const char* path) {
+  return render(hh, r, nullptr, path);
+}
+
+extern "C" int s2lc_visualize_info(const s2lc_history* hh, const s2lc_result* r, const s2lc_partials* info,
+                                   const char* path) {
+  return render(hh, r, info, path);
+}
+
+static int render(const s2lc_history* hh, const s2lc_result* r, const s2lc_partials* info, const char* path) {
   if (!hh || !r || !path) return S2LC_EINVAL;
   const History& h = hh->h;
   if (h.status) return h.status;
@@ -158,8 +169,12 @@ extern "C" int s2lc_visualize(const s2lc_history* hh, const s2lc_result* r, cons
       const char* cls = pos[d] >= 0 ? "lin" : (r->verdict == S2LC_OK ? "ok" : "out");
       std::string tip = "op " + std::to_string(h.op_ids[d]) + ": " + describe_op(h, d);
       if (pos[d] >= 0) tip += "\nlinearized #" + std::to_string(pos[d]) + ", state after: " + after[(size_t)pos[d]];
-      fprintf(f, "<g><title>%s</title><rect class=\"%s\" x=\"%.1f\" y=\"%d\" width=\"%.1f\" height=\"%d\"/>",
-              html_esc(tip).c_str(), cls, x0, y, std::max(1.0, x1 - x0), rh - 6);
+      const uint32_t lp = info && d < info->n_ops ? info->op_partial[d] : 0xFFFFFFFFu;
+      if (lp != 0xFFFFFFFFu)
+        tip += "\nlongest partial linearization containing it: #" + std::to_string(lp) + " (" +
+               std::to_string(info->offs[lp + 1] - info->offs[lp]) + " ops)";
+      fprintf(f, "<g onmouseenter=\"hl(%u)\" onmouseleave=\"hl(-1)\"><title>%s</title><rect id=\"op%u\" class=\"%s\" x=\"%.1f\" y=\"%d\" width=\"%.1f\" height=\"%d\"/>",
+              d, html_esc(tip).c_str(), d, cls, x0, y, std::max(1.0, x1 - x0), rh - 6);
       if (pos[d] >= 0) fprintf(f, "<text x=\"%.1f\" y=\"%d\">%d</text>", x0 + 1, y + 11, pos[d]);
       fprintf(f, "</g>\n");
     }
@@ -172,7 +187,38 @@ extern "C" int s2lc_visualize(const s2lc_history* hh, const s2lc_result* r, cons
               (long long)h.op_ids[d], (long long)h.events[h.op_call[d]].client_id, html_esc(describe_op(h, d)).c_str(),
               html_esc(after[k]).c_str());
     }
-    fprintf(f, "</table>\n</body></html>\n");
+    fprintf(f, "</table>\n");
+    // LinearizationInfo (porcupine's Visualize: hovering an op shows the
+    // longest partial linearization containing it)
+    fprintf(f, "<script>\nconst P=[");
+    if (info) {
+      for (uint32_t k = 0; k < info->n_partials; ++k) {
+        fprintf(f, "%s[", k ? "," : "");
+        for (uint64_t x = info->offs[k]; x < info->offs[k + 1]; ++x) {
+          auto it = dense.find(info->ids[x]);
+          fprintf(f, "%s%u", x > info->offs[k] ? "," : "", it != dense.end() ? it->second : 0u);
+        }
+        fprintf(f, "]");
+      }
+    }
+    fprintf(f, "];\nconst L=[");
+    for (uint32_t d = 0; d < h.n_ops; ++d)
+      fprintf(f, "%s%d", d ? "," : "", info && d < info->n_ops && info->op_partial[d] != 0xFFFFFFFFu ? (int)info->op_partial[d] : -1);
+    fprintf(f, "];\nfunction hl(d){document.querySelectorAll('rect').forEach(r=>r.style.stroke='');"
+               "if(d<0||L[d]<0)return;P[L[d]].forEach(o=>{const e=document.getElementById('op'+o);"
+               "if(e){e.style.stroke='#000';e.style.strokeWidth='2';}});}\n</script>\n");
+    if (info && info->n_partials) {
+      fprintf(f, "<h3>Longest partial linearizations (LinearizationInfo%s)</h3>\n<table><tr><th>#</th><th>ops</th>"
+                 "<th>ops whose longest it is</th></tr>\n", info->exact ? "" : ", search budget reached: lower bounds");
+      std::vector<uint32_t> owners(info->n_partials, 0);
+      for (uint32_t d = 0; d < info->n_ops; ++d)
+        if (info->op_partial[d] != 0xFFFFFFFFu) owners[info->op_partial[d]]++;
+      for (uint32_t k = 0; k < info->n_partials; ++k)
+        fprintf(f, "<tr><td>%u</td><td>%llu</td><td>%u</td></tr>\n", k,
+                (unsigned long long)(info->offs[k + 1] - info->offs[k]), owners[k]);
+      fprintf(f, "</table>\n");
+    }
+    fprintf(f, "</body></html>\n");
   } catch (...) {
     fclose(f);
     return S2LC_ENOMEM;

@@ -33,3 +33,39 @@ def test_bench_line_contract():
     assert cb["kind"] == "port" and cb["cores"] >= 1 and cb["value"] > 0
     assert cb["parity"]["verdict_mismatches"] == 0 and cb["parity"]["checked"] > 0
     assert d["verdicts"]["Unknown"] == 0 and d["verdicts"]["Ok"] + d["verdicts"]["Illegal"] == 2000
+
+
+@pytest.mark.gpu
+def test_bench_two_gloo_ranks_on_one_gpu():
+    """The driver's multi-GPU bench path, rehearsed with 2 ranks sharing the one
+    GPU over gloo (S2LC_BENCH_GLOO=1): the weak C4 line, the strong split of
+    the BASELINE C4 batch (10,000 histories in total: the committed CPU
+    verdict counts), and the distributed C5 / C5wide legs (verdicts against
+    the committed reduced search, witnesses certified)."""
+    import random
+    sys.path.insert(0, os.path.join(ROOT, "tests"))
+    from helpers import golden
+    port = random.randint(20000, 40000)
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
+           "--master-addr", "127.0.0.1", "--master-port", str(port), os.path.join(ROOT, "bench.py"),
+           "--gpus", "2", "--steps", "2", "--warmup", "1", "--no-e2e", "--c5-reps", "1"]
+    env = dict(os.environ, S2LC_BENCH_GLOO="1")
+    p = subprocess.run(cmd, capture_output=True, text=True, timeout=600, cwd=ROOT, env=env)
+    assert p.returncode == 0, p.stderr[-4000:]
+    lines = [x for x in p.stdout.splitlines() if x.startswith("{")]
+    assert len(lines) == 1, p.stdout[-2000:]
+    d = json.loads(lines[0])
+    assert d["n_gpus"] == 2 and d["scaling"] == "weak" and d["verdicts"]["Unknown"] == 0
+    c4 = golden("c4_verdicts.json")
+    ss = d["strong_split"]
+    assert ss["histories_total"] == 10000 and ss["histories_per_gpu"] == 5000
+    assert ss["verdicts"] == {"Ok": sum(1 for r in c4["rows"] if r[0] == "O"),
+                              "Illegal": sum(1 for r in c4["rows"] if r[0] == "I"), "Unknown": 0}
+    hard = golden("hard_reduced.json")
+    c5 = d["c5"]
+    assert "error" not in c5, c5
+    assert c5["verdict"] == hard["C5"]["verdict"] and c5["witness_replayed"], c5
+    assert c5["bad_variant_verdict"] == hard["C5bad"]["verdict"]
+    assert c5["replicated_only"]["verdict"] == c5["verdict"]
+    w = c5["c5wide"]
+    assert w["verdict"] == hard["C5wide"]["verdict"] and w["witness_replayed"], w

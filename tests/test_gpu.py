@@ -147,6 +147,8 @@ def test_cli_verdicts_and_exit_codes(tmp_path):
             assert p.returncode == 0 and line["msg"] == "passed: is linearizable", (c["name"], p.stderr)
         else:
             assert p.returncode == 1 and line["msg"] == "failed: is NOT linearizable" and line["res"] == "Illegal"
+            # porcupine's LinearizationInfo on the page (main.go:606-627)
+            assert "Longest partial linearizations (LinearizationInfo" in html and "const L=[" in html
     # Unknown (a staging array too small for H174's widest rounds): its own
     # message and exit code, never read as a violation
     from s2_verification_amd import workloads as W
