@@ -55,7 +55,18 @@ static void slog(const char* level, const std::string& msg, const std::string& e
           jstr(msg).c_str(), extra.c_str());
 }
 
+// S2LC_CLI_TIMING=1: one stderr line with the process's phases (ms since start)
+static double ms_since(const struct timespec& t0) {
+  struct timespec t;
+  clock_gettime(CLOCK_MONOTONIC, &t);
+  return 1e3 * (double)(t.tv_sec - t0.tv_sec) + 1e-6 * (double)(t.tv_nsec - t0.tv_nsec);
+}
+
 int main(int argc, char** argv) {
+  struct timespec t_start;
+  clock_gettime(CLOCK_MONOTONIC, &t_start);
+  const bool timing = getenv("S2LC_CLI_TIMING") != nullptr;
+  double t_load = 0, t_ctx = 0, t_check = 0, t_viz = 0;
   const char* file = nullptr;
   bool version = false;
   for (int i = 1; i < argc; ++i) {  // Go flag syntax: -flag, --flag, -flag=value, -flag value
@@ -93,6 +104,7 @@ int main(int argc, char** argv) {
     fprintf(stderr, "failed to decode history: %s\n", err);
     return 1;
   }
+  t_load = ms_since(t_start);
   s2lc_opts o;
   memset(&o, 0, sizeof o);
   o.struct_size = sizeof o;
@@ -104,9 +116,11 @@ int main(int argc, char** argv) {
     s2lc_history_free(h);
     return 1;
   }
+  t_ctx = ms_since(t_start);
   s2lc_result r;
   memset(&r, 0, sizeof r);
   rc = s2lc_check(ctx, h, &r);
+  t_check = ms_since(t_start);
   if (rc == S2LC_EWITNESS) {
     // the GPU found a linearization that failed CPU-model certification: a
     // checker bug, never a verdict (exit 3, distinct from 0 / 1)
@@ -153,6 +167,7 @@ int main(int argc, char** argv) {
       slog("INFO", "wrote visualization", ",\"file\":" + jstr(path.data()));
     }
   }
+  t_viz = ms_since(t_start);
   const bool ok = r.verdict == S2LC_OK;
   int code = 0;
   if (ok) {
@@ -175,5 +190,8 @@ int main(int argc, char** argv) {
   s2lc_result_free(&r);
   s2lc_destroy(ctx);
   s2lc_history_free(h);
+  if (timing)
+    fprintf(stderr, "{\"cli_timing_ms\":{\"decode\":%.2f,\"create\":%.2f,\"check\":%.2f,\"viz\":%.2f,\"exit\":%.2f}}\n",
+            t_load, t_ctx - t_load, t_check - t_ctx, t_viz - t_check, ms_since(t_start) - t_viz);
   return code;
 }

@@ -425,7 +425,16 @@ int batch_run(DevBatch& b, hipStream_t stream, const RunOpts& ro, RunStats& st, 
         bpc = std::max(1, bpc);
         b.pack_bpc[li] = bpc;
       }
-      const uint32_t groups = PACK_BLOCK / L;
+      const uint32_t gpw_all = 64 / L;
+      uint32_t gpw = gpw_all;
+      if (const char* e = getenv("S2LC_PACK_GPW")) gpw = std::max<uint32_t>(1, std::min<uint32_t>(gpw_all, (uint32_t)atoi(e)));
+      pp.gpw = gpw < gpw_all ? gpw : 0u;
+      // S2LC_PACK_SOLO_N: the first n histories of the LPT order one per wave
+      uint32_t solo_n = 0;
+      if (const char* e = getenv("S2LC_PACK_SOLO_N")) solo_n = std::min<uint32_t>(n_l, (uint32_t)atoi(e));
+      pp.solo_n = solo_n;
+      pp.counter_solo = b.counter + 9 + li;  // (zeroed with the counters each run)
+      const uint32_t groups = (PACK_BLOCK / 64) * gpw;
       const uint32_t grid = std::max<uint32_t>(
           1, std::min<uint32_t>((n_l + groups - 1) / groups, (uint32_t)n_cu * (uint32_t)std::max(1, bpc)));
       HIPCHK(hipEventRecord(b.ev[2 * li], stream));

@@ -155,14 +155,17 @@ class _Exchange:
         if not self.same_stream:
             torch.cuda.current_stream(self.device).synchronize()  # the library reads on its own stream
 
-    def counts(self, counts, found: bool, staged: int):
-        """All-to-all of (count for the receiver, found, staged total) triples."""
+    def counts(self, counts, found: bool, staged: int, frontier: int = 0):
+        """All-to-all of (count for the receiver, found, staged total, the
+        sender's frontier after the previous round) rows: the round's sizes,
+        its termination and the previous round's global frontier in one
+        collective."""
         w = self.world
-        send = torch.tensor([[c, int(found), staged] for c in counts], dtype=torch.int64, device=self.tdev)
-        recv = torch.empty((w, 3), dtype=torch.int64, device=self.tdev)
+        send = torch.tensor([[c, int(found), staged, frontier] for c in counts], dtype=torch.int64, device=self.tdev)
+        recv = torch.empty((w, 4), dtype=torch.int64, device=self.tdev)
         dist.all_to_all_single(recv, send, group=self.group)
         r = recv.cpu().tolist()
-        return [x[0] for x in r], any(x[1] for x in r), sum(x[2] for x in r)
+        return [x[0] for x in r], any(x[1] for x in r), sum(x[2] for x in r), sum(x[3] for x in r)
 
     def payload(self, send: torch.Tensor, in_bytes, out_bytes) -> torch.Tensor:
         total = int(sum(out_bytes))
@@ -274,6 +277,8 @@ def check_distributed(checker, history: History, group=None, witness: bool = Tru
     rounds = 0
     configs = 0
     part_rounds = 0
+    phase_rounds = 0  # partitioned rounds since the last switch to them
+    nn_local = 0      # this rank's frontier after the last partitioned round (reported with the next counts)
     replicated = wide > 0  # wide = 0: every round partitioned (also on one rank: a self-exchange)
     t0 = time.perf_counter()
     first = True  # round 0 closes the initial configuration; rounds counts the ones after it
@@ -303,7 +308,12 @@ def check_distributed(checker, history: History, group=None, witness: bool = Tru
                     replicated = False
                 continue
             counts, found = ds.expand()
-            recv_counts, found_any, staged_total = ex.counts(counts, found, sum(counts))
+            # (the previous round's global frontier travels with this round's
+            # counts: no collective of its own; an empty frontier shows up here
+            # as nothing staged anywhere)
+            recv_counts, found_any, staged_total, prev_total = ex.counts(counts, found, sum(counts), nn_local)
+            if phase_rounds:
+                configs += prev_total
             if found_any:
                 verdict = Ok
                 break
@@ -317,23 +327,30 @@ def check_distributed(checker, history: History, group=None, witness: bool = Tru
             sent_bytes += sum(b for w, b in enumerate(in_b) if w != rank)
             recv = ex.payload(send[:sum(in_b)], in_b, out_b)
             nn = ds.insert(recv, sum(recv_counts))
+            nn_local = nn
             keep = [recv]
             part_rounds += 1
-            total = ex.sum(nn)
-            configs += total
-            if total == 0:
-                verdict = Illegal
-                break
-            if wide > 0 and total < wide // 4:
-                # narrow again: every rank takes the whole frontier
-                sizes = [x[0] * cb for x in ex.gather_small([nn])]
-                mine = torch.empty(max(1, nn * cb), dtype=torch.uint8, device=device)
-                if nn:
-                    ds.frontier_pack(mine)
-                full = ex.gather_frontier(mine, sizes)
-                ds.frontier_load(full, total)
-                keep = [full]
-                replicated = True
+            phase_rounds += 1
+            if wide > 0 and phase_rounds > 1 and prev_total < wide // 4:
+                # the frontier was narrow a round ago: the exact sizes of this
+                # one (an all-gather the switch needs anyway) decide
+                sizes_n = [x[0] for x in ex.gather_small([nn])]
+                total = sum(sizes_n)
+                if total < wide // 4:
+                    # narrow again: every rank takes the whole frontier
+                    configs += total
+                    nn_local = 0
+                    phase_rounds = 0
+                    mine = torch.empty(max(1, nn * cb), dtype=torch.uint8, device=device)
+                    if nn:
+                        ds.frontier_pack(mine)
+                    full = ex.gather_frontier(mine, [x * cb for x in sizes_n])
+                    ds.frontier_load(full, total)
+                    keep = [full]
+                    replicated = True
+                    if total == 0:
+                        verdict = Illegal
+                        break
         wall = time.perf_counter() - t0
         info = ds.info()
         stats = ex.gather_small([int(found and verdict == Ok), info.found_parent, info.found_move, info.found_p4,

@@ -25,7 +25,8 @@ def exchange_worker(rank, world, port, q):
         dist = _init(rank, world, port, "gloo")
         ex = _Exchange(None, torch.device("cpu"))
         counts = [10 * rank + w for w in range(world)]  # rank -> w
-        recv, found_any, staged = ex.counts(counts, rank == world - 1, sum(counts))
+        recv, found_any, staged, front = ex.counts(counts, rank == world - 1, sum(counts), 100 + rank)
+        assert front == sum(100 + r for r in range(world))
         tr = np.array([[0xFFFFFFFF, 0xFFFFFFFF], [(rank << 29) | 0, rank + 1]], dtype=np.uint32)
         traces = ex.gather_traces(tr)
         q.put((rank, recv, found_any, staged, [t.tolist() for t in traces]))
