@@ -259,35 +259,17 @@ __global__ __launch_bounds__(PACK_BLOCK, S2LC_PACK_MINW) void pack_kernel(Params
   const uint64_t gmask = (L == 64 ? ~0ull : ((1ull << L) - 1)) << gbase;
   C* const fr = reinterpret_cast<C*>(smem + (threadIdx.x / L) * pack_group_bytes<L>());
 
-  // S2LC_PACK_GPW (diagnostics): only the first gpw groups of each wave take
-  // histories (fewer histories in lockstep per wave)
+  // Only the first gpw groups of each wave take histories: the groups of a
+  // wave run in lockstep (every round costs the wave the most any of its
+  // groups spends), so fewer histories per wave shorten every round, at the
+  // price of fewer histories in flight (the host picks gpw from the batch)
   if (p.gpw && (uint32_t)(lane / L) >= p.gpw) return;
   uint32_t tbase = 0, tleft = 0;  // group's trace chunk (uniform)
-  // The longest histories (the LPT order's first solo_n) run one per wave:
-  // the groups of a wave run in lockstep, so a history alone in its wave has
-  // the shortest rounds, and the launch ends with its longest history. Then
-  // each group takes histories on its own (gpw groups per wave).
-  bool solo = p.solo_n > 0;
   for (;;) {
     uint32_t hi = 0;
-    bool mine = true;
-    if (solo) {
-      uint32_t x = 0;
-      if (lane == 0) x = atomicAdd(p.counter_solo, 1u);
-      x = __shfl((int)x, 0, 64);  // the whole wave takes one history
-      if (x < p.solo_n) {
-        hi = x;
-        mine = lane < L;  // group 0's
-      } else {
-        solo = false;
-      }
-    }
-    if (!solo) {
-      if (gl == 0) hi = p.solo_n + atomicAdd(p.counter, 1u);
-      hi = bcast_u32(hi, gbase);
-    }
+    if (gl == 0) hi = atomicAdd(p.counter, 1u);
+    hi = bcast_u32(hi, gbase);
     if (hi >= p.n_hist) break;
-    if (!mine) continue;  // (the other groups wait at the loop's end for group 0)
     const uint32_t h = p.order[hi];
     const HistDesc hd = p.hist[h];
     const int K = hd.K;

@@ -251,13 +251,21 @@ int batch_upload(DevBatch& b, const std::vector<const History*>& hs, uint32_t re
     R.witness_off = b.h_moves_off[i];
   });
   for (size_t i = 0; i < n; ++i) b.algo_bytes_inputs += b.h_in_bytes[i];
-  // longest-first processing order (LPT): work ~ ops x chains
+  // LPT order, longest first. A history's search runs one round per
+  // non-identity op it linearizes (appends: n_ops - n_ident), a dependent
+  // chain whatever the engine, so that count leads the key; n_ops x K breaks
+  // ties (a round's width). On C4 this order ends the packed launch 16 %
+  // sooner than n_ops x K alone, which ties every history with the same
+  // client count (tools/pack_sweep.py).
   b.lpt.clear();
-  for (uint32_t i = 0; i < n; ++i)
-    if (!b.forced[i]) b.lpt.push_back(i);
-  std::stable_sort(b.lpt.begin(), b.lpt.end(), [&](uint32_t x, uint32_t y) {
-    return (uint64_t)b.h_hist[x].n_ops * b.h_hist[x].K > (uint64_t)b.h_hist[y].n_ops * b.h_hist[y].K;
-  });
+  std::vector<uint64_t> key(n, 0);
+  for (uint32_t i = 0; i < n; ++i) {
+    if (b.forced[i]) continue;
+    b.lpt.push_back(i);
+    const History& h = *hs[i];
+    key[i] = ((uint64_t)(h.n_ops - h.n_ident) << 40) | ((uint64_t)h.n_ops * h.K & ((1ull << 40) - 1));
+  }
+  std::stable_sort(b.lpt.begin(), b.lpt.end(), [&](uint32_t x, uint32_t y) { return key[x] > key[y]; });
   // the packed-kernel lists (engine AUTO): K <= 16, 16 < K <= 32, and with
   // S2LC_PACK8=1 the K <= 8 histories in 8-lane groups first. Off by default:
   // at C4's 10k histories a launch lasts about one history's chain of rounds
@@ -425,15 +433,18 @@ int batch_run(DevBatch& b, hipStream_t stream, const RunOpts& ro, RunStats& st, 
         bpc = std::max(1, bpc);
         b.pack_bpc[li] = bpc;
       }
+      // lane groups per wave that take histories: the fewest (1, 2, 4, ...)
+      // with at most ~2.5 histories per group over the resident waves. The
+      // groups of a wave run in lockstep, so fewer per wave give shorter
+      // rounds; past that, more groups keep more histories in flight. C4
+      // sweep (tools/gpw_sweep.sh, profiles/r03): 1,000 histories 1.58 / 1.93 /
+      // 2.42 ms at 1 / 2 / 4 groups, 10,000: 2.66 / 2.02 / 2.59 ms.
       const uint32_t gpw_all = 64 / L;
-      uint32_t gpw = gpw_all;
+      const uint64_t waves = (uint64_t)n_cu * (uint64_t)bpc * (PACK_BLOCK / 64);
+      uint32_t gpw = 1;
+      while (gpw < gpw_all && (uint64_t)n_l * 2 > waves * gpw * 5) gpw *= 2;
       if (const char* e = getenv("S2LC_PACK_GPW")) gpw = std::max<uint32_t>(1, std::min<uint32_t>(gpw_all, (uint32_t)atoi(e)));
       pp.gpw = gpw < gpw_all ? gpw : 0u;
-      // S2LC_PACK_SOLO_N: the first n histories of the LPT order one per wave
-      uint32_t solo_n = 0;
-      if (const char* e = getenv("S2LC_PACK_SOLO_N")) solo_n = std::min<uint32_t>(n_l, (uint32_t)atoi(e));
-      pp.solo_n = solo_n;
-      pp.counter_solo = b.counter + 9 + li;  // (zeroed with the counters each run)
       const uint32_t groups = (PACK_BLOCK / 64) * gpw;
       const uint32_t grid = std::max<uint32_t>(
           1, std::min<uint32_t>((n_l + groups - 1) / groups, (uint32_t)n_cu * (uint32_t)std::max(1, bpc)));

@@ -104,8 +104,6 @@ struct Params {
   uint32_t* rcounts;               // per-round unique configurations at res[h].witness_off (nullable)
   const unsigned long long* deadline;  // wall_clock64() value after which histories give Unknown (nullable)
   uint32_t gpw;                    // pack kernels: lane groups per wave that take histories (0 = all)
-  uint32_t solo_n;                 // pack kernels: order[0 .. solo_n) run one history per wave (LPT head)
-  uint32_t* counter_solo;          // their work counter
 };
 
 // The run's deadline in device wall-clock ticks (written once per run, read by
