@@ -4,7 +4,8 @@
 # 1. bench.py (default run)                       -> gpurun_out/<tag>/bench.json
 # 2. rocprofv3 --kernel-trace --stats, C4 only     -> gpurun_out/<tag>/stats/
 # 3. two PMC passes (FETCH_SIZE, WRITE_SIZE)       -> gpurun_out/<tag>/pmc_*/
-#    summarised for pack_kernel<8>                 -> gpurun_out/<tag>/pmc_c4.json
+#    summarised for pack_kernel<16>                -> gpurun_out/<tag>/pmc_c4.json
+# 4. rocprofv3 --kernel-trace --stats of C5        -> gpurun_out/<tag>/c5stats/
 # Every GPU step has its own time limit; the first failure ends the script.
 set -euo pipefail
 TAG=${1:-run}
@@ -19,7 +20,6 @@ timeout -s KILL 120 rocprofv3 --pmc FETCH_SIZE --output-format csv -d "$OUT/pmc_
   python3 bench.py $SHORT > "$OUT/pmc_fetch_bench.json" 2> "$OUT/pmc_fetch.err"
 timeout -s KILL 120 rocprofv3 --pmc WRITE_SIZE --output-format csv -d "$OUT/pmc_write" -o c4 -- \
   python3 bench.py $SHORT > "$OUT/pmc_write_bench.json" 2> "$OUT/pmc_write.err"
-python3 profiles/pmc_summary.py "$OUT/pmc_fetch" "$OUT/pmc_write" "$OUT/pmc_c4.json" "pack_kernel<8>"
-# 4. the level search on the single hard history (C5)      -> gpurun_out/<tag>/c5stats/
+python3 profiles/pmc_summary.py "$OUT/pmc_fetch" "$OUT/pmc_write" "$OUT/pmc_c4.json" "pack_kernel<16>" "$OUT/pmc_fetch_bench.json"
 timeout -k 10 200 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/c5stats" -o c5 -- \
   python3 tools/c5run.py C5 > "$OUT/c5run.log" 2> "$OUT/c5stats.err"

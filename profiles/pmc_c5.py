@@ -12,6 +12,7 @@ import sys
 
 sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
 from pmc_sq import load  # noqa: E402
+from kernel_digest import src_digest  # noqa: E402
 
 SEARCHES = 2
 
@@ -32,6 +33,7 @@ def main():
     out = {
         "workload": "C5 (tools/c5run.py C5: two searches, cold + warm)",
         "kernels": "lv_persist + lv_round + lv_insert",
+        "src_digest": src_digest("c5"),
         "hbm_bytes_per_search": round((2 * fb + wb) * 1024 / SEARCHES, 1),
         "tcc_ea_atomics_per_search": round(lv_total(atom, "TCC_EA0_ATOMIC") / SEARCHES, 1),
         "tcc_atomics_per_search": round(lv_total(atom, "TCC_ATOMIC") / SEARCHES, 1),

@@ -1,7 +1,8 @@
 """Summarise rocprofv3 PMC passes for one kernel into profiles/pmc_c4.json.
 
-Usage: python profiles/pmc_summary.py <fetch_dir> <write_dir> <out.json> [kernel]
-(kernel: a substring of the kernel name, default "pack_kernel<16>")
+Usage: python profiles/pmc_summary.py <fetch_dir> <write_dir> <out.json> [kernel] [bench.json]
+(kernel: a substring of the kernel name, default "pack_kernel<16>"; bench.json:
+the profiled bench.py run's line, for the launch's history count)
 
 HBM bytes per launch = (2 * FETCH_SIZE + WRITE_SIZE) * 1024, following
 MI355X_MICROARCH.md §HBM: FETCH_SIZE (KiB) counts 64 B per 128-B request for
@@ -14,6 +15,9 @@ import json
 import os
 import sys
 from collections import defaultdict
+
+sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+from kernel_digest import src_digest  # noqa: E402
 
 
 def per_dispatch(d, counter, kernel):
@@ -32,6 +36,11 @@ def per_dispatch(d, counter, kernel):
 def main():
     fetch_dir, write_dir, out = sys.argv[1:4]
     kernel = sys.argv[4] if len(sys.argv) > 4 else "pack_kernel<16>"
+    hist = None
+    if len(sys.argv) > 5:
+        with open(sys.argv[5]) as fh:
+            line = [x for x in fh if x.startswith("{")][-1]
+        hist = json.loads(line)["roofline"]["histories_per_launch"]
     fetch = per_dispatch(fetch_dir, "FETCH_SIZE", kernel)
     write = per_dispatch(write_dir, "WRITE_SIZE", kernel)
     if not fetch or not write:
@@ -43,6 +52,8 @@ def main():
         "dispatches": {"fetch_pass": len(fetch), "write_pass": len(write)},
         "FETCH_SIZE_KiB": f, "WRITE_SIZE_KiB": w,
         "hbm_bytes_per_launch": int((2 * f + w) * 1024),
+        "src_digest": src_digest("c4"),
+        "histories_per_launch": hist,
         "correction": "FETCH_SIZE doubled per MI355X_MICROARCH.md (gfx950 counts 64 B per 128-B read request)",
     }
     with open(out, "w") as fh:
