@@ -13,11 +13,19 @@
  * Written from the design, not from search_dev.h: plain arrays, a
  * std-free open-addressing set, sets of ops as per-chain counters.
  */
+#include <stdio.h>
 #include <stdlib.h>
 #include <string.h>
 #include <time.h>
 
 #include "oracle.h"
+
+/* allocation failure in the search loop: fail loudly (an exploded ablation
+ * must not read as a verdict) */
+static void* r_chk(void* p) {
+  if (!p) { fprintf(stderr, "oracle/reduced.c: out of memory in the round loop\n"); abort(); }
+  return p;
+}
 
 typedef struct rop {
   const or_event* in;
@@ -234,22 +242,22 @@ int or_check_reduced(const or_event* ev, size_t n_ev, uint64_t max_configs, uint
   /* BFS by rounds */
   size_t cw = (size_t)(K ? K : 1);
   size_t fcap = 1024, nf = 0;
-  uint16_t* fcnt = (uint16_t*)calloc(fcap * cw, sizeof(uint16_t));
-  rst* fst = (rst*)calloc(fcap, sizeof(rst));
+  uint16_t* fcnt = (uint16_t*)r_chk(calloc(fcap * cw, sizeof(uint16_t)));
+  rst* fst = (rst*)r_chk(calloc(fcap, sizeof(rst)));
   rst s0 = {0, 0, 0};
   int r0 = r_close(&c, fcnt, &s0);
   if (r0 == 2) result = OR_OK;
   else if (r0 == 0) { fst[0] = s0; nf = 1; if (rc_out && rc_cap > 0) rc_out[0] = 1; }
   size_t round = 0;
-  uint16_t* tmp = (uint16_t*)malloc(sizeof(uint16_t) * cw);
+  uint16_t* tmp = (uint16_t*)r_chk(malloc(sizeof(uint16_t) * cw));
   while (result != OR_OK && nf > 0) {
     size_t ncap = 1024, nn = 0;
-    uint16_t* ncnt = (uint16_t*)malloc(ncap * cw * sizeof(uint16_t));
-    rst* nst = (rst*)malloc(ncap * sizeof(rst));
+    uint16_t* ncnt = (uint16_t*)r_chk(malloc(ncap * cw * sizeof(uint16_t)));
+    rst* nst = (rst*)r_chk(malloc(ncap * sizeof(rst)));
     rset set;
     set.cap = 4096; set.n = 0;
-    set.fp = (uint64_t*)calloc(set.cap, sizeof(uint64_t));
-    set.idx = (int32_t*)malloc(set.cap * sizeof(int32_t));
+    set.fp = (uint64_t*)r_chk(calloc(set.cap, sizeof(uint64_t)));
+    set.idx = (int32_t*)r_chk(malloc(set.cap * sizeof(int32_t)));
     for (size_t i = 0; i < nf && result != OR_OK; i++) {
       const uint16_t* pc = fcnt + i * cw;
       const rst* ps = &fst[i];
@@ -284,8 +292,8 @@ int or_check_reduced(const or_event* ev, size_t n_ev, uint64_t max_configs, uint
             size_t oc = set.cap;
             uint64_t* of = set.fp; int32_t* oi = set.idx;
             set.cap *= 2;
-            set.fp = (uint64_t*)calloc(set.cap, sizeof(uint64_t));
-            set.idx = (int32_t*)malloc(set.cap * sizeof(int32_t));
+            set.fp = (uint64_t*)r_chk(calloc(set.cap, sizeof(uint64_t)));
+            set.idx = (int32_t*)r_chk(malloc(set.cap * sizeof(int32_t)));
             for (size_t z = 0; z < oc; z++) if (of[z]) {
               size_t j = of[z] & (set.cap - 1);
               while (set.fp[j]) j = (j + 1) & (set.cap - 1);
@@ -305,8 +313,8 @@ int or_check_reduced(const or_event* ev, size_t n_ev, uint64_t max_configs, uint
           if (dup) continue;
           if (nn == ncap) {
             ncap *= 2;
-            ncnt = (uint16_t*)realloc(ncnt, ncap * cw * sizeof(uint16_t));
-            nst = (rst*)realloc(nst, ncap * sizeof(rst));
+            ncnt = (uint16_t*)r_chk(realloc(ncnt, ncap * cw * sizeof(uint16_t)));
+            nst = (rst*)r_chk(realloc(nst, ncap * sizeof(rst)));
           }
           memcpy(ncnt + nn * cw, tmp, cw * sizeof(uint16_t));
           nst[nn] = kids[k];

@@ -85,6 +85,8 @@ const char* s2lc_version(void) { return "s2lincheck 0.2.0 (gfx950, ABI 2)"; }
 
 s2lc_ctx* s2lc_create(const s2lc_opts* opts, int* status) {
   s2lc_ctx* c = nullptr;
+  static const bool timing = getenv("S2LC_CREATE_TIMING") != nullptr;  // diagnostics
+  const int64_t t0 = timing ? steady_ns() : 0;
   try {
     int n = 0;
     if (hipGetDeviceCount(&n) != hipSuccess || n <= 0) {
@@ -121,6 +123,7 @@ s2lc_ctx* s2lc_create(const s2lc_opts* opts, int* status) {
       }
     }
     if (c->devices.empty()) c->devices.push_back(dev);
+    const int64_t t1 = timing ? steady_ns() : 0;
     if (!c->stream) {
       if (hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess) {
         delete c;
@@ -129,6 +132,9 @@ s2lc_ctx* s2lc_create(const s2lc_opts* opts, int* status) {
       }
       c->own_stream = true;
     }
+    if (timing)
+      fprintf(stderr, "{\"s2lc_create_ms\":{\"runtime_init\":%.2f,\"stream\":%.2f}}\n", 1e-6 * (t1 - t0),
+              1e-6 * (steady_ns() - t1));
   } catch (...) {
     delete c;
     if (status) *status = S2LC_ENOMEM;

@@ -317,9 +317,30 @@ void batch_release(DevBatch& b) {
   b.slab = nullptr; b.slab_cap = 0;
 }
 
+// Wait for the stream. S2LC_SYNC=spin polls an event recorded at its end
+// instead of the blocking hipStreamSynchronize (measured on C4: the blocking
+// wait returns ~23 us after the kernel; polling made the next step's enqueue
+// 200 us slower, so blocking is the default).
+static hipError_t stream_wait(hipStream_t stream, hipEvent_t ev) {
+  static const int mode = [] {
+    const char* e = getenv("S2LC_SYNC");
+    return e && !strcmp(e, "spin") ? 0 : 1;
+  }();
+  if (mode == 0 && ev) {
+    hipError_t e = hipEventRecord(ev, stream);
+    if (e != hipSuccess) return e;
+    while ((e = hipEventQuery(ev)) == hipErrorNotReady) {
+    }
+    if (e != hipSuccess) return e;
+  }
+  return hipStreamSynchronize(stream);
+}
+
 int batch_run(DevBatch& b, hipStream_t stream, const RunOpts& ro, RunStats& st, std::string& err) {
   st = RunStats{};
   const int64_t t0 = steady_ns();
+  static const bool step_timing = getenv("S2LC_STEP_TIMING") != nullptr;
+  int64_t t_enq = 0, t_wait = 0, t_ev = 0, t_over = 0, t_tail = 0;
   const int64_t deadline_ns = ro.timeout_us ? t0 + (int64_t)std::min<uint64_t>(ro.timeout_us, 1ull << 40) * 1000 : 0;
   const bool witness = ro.witness;
   int dev = 0;
@@ -459,7 +480,9 @@ int batch_run(DevBatch& b, hipStream_t stream, const RunOpts& ro, RunStats& st, 
     }
     // (pack_kernel resolves its histories' witnesses itself: no walk here)
     HIPCHK(hipMemcpyAsync(b.h_res, b.res, b.n_hist * sizeof(HistResult), hipMemcpyDeviceToHost, stream));
-    HIPCHK(hipStreamSynchronize(stream));
+    t_enq = steady_ns();
+    HIPCHK(stream_wait(stream, b.ev[6]));
+    t_wait = steady_ns();
     for (int li = 0; li < 3; ++li) {
       if (!launched[li]) continue;
       float ms = 0;
@@ -469,6 +492,7 @@ int batch_run(DevBatch& b, hipStream_t stream, const RunOpts& ro, RunStats& st, 
       if (li == 0) st.pack8_ms = ms;
       if (li == 1) st.pack16_ms = ms;
     }
+    t_ev = steady_ns();
 #ifdef S2LC_PROF
     {
       unsigned long long gp[16];
@@ -480,17 +504,25 @@ int batch_run(DevBatch& b, hipStream_t stream, const RunOpts& ro, RunStats& st, 
     }
 #endif
     // histories that outgrew the packed frontier go on to the workgroup passes
+    // (in history order: h_hist / h_res are pinned host memory, slow to read
+    // in LPT order — 180-240 us per C4 step — and fast sequentially)
     std::vector<uint32_t> over;
-    for (uint32_t i : b.lpt) {
-      const uint32_t K = b.h_hist[i].K;
-      if (K > 32 || !(b.h_hist[i].flags & H_TAIL32)) continue;
+    for (uint32_t i = 0; i < b.n_hist; ++i) {
+      const HistDesc& hd = b.h_hist[i];
+      if (hd.K > 32 || !(hd.flags & H_TAIL32) || b.forced[i]) continue;
       if (b.h_res[i].verdict == V_UNKNOWN && b.h_res[i].reason == S2LC_R_FRONTIER) over.push_back(i);
-      else if (K <= b.pack8_kmax) pack_done[i] = 8;
-      else if (K <= 16) pack_done[i] = 16;
+      else if (hd.K <= b.pack8_kmax) pack_done[i] = 8;
+      else if (hd.K <= 16) pack_done[i] = 16;
+    }
+    if (over.size() > 1) {  // back to LPT order for the workgroup passes
+      std::vector<uint32_t> rank(b.n_hist);
+      for (uint32_t k = 0; k < (uint32_t)b.lpt.size(); ++k) rank[b.lpt[k]] = k;
+      std::sort(over.begin(), over.end(), [&](uint32_t x, uint32_t y) { return rank[x] < rank[y]; });
     }
     st.n_overflow = (uint32_t)over.size();
     over.insert(over.end(), todo.begin(), todo.end());
     todo.swap(over);
+    t_over = steady_ns();
   }
   const uint32_t lds_fcap = 8;
   const uint32_t lds_stage = 32;
@@ -536,7 +568,7 @@ int batch_run(DevBatch& b, hipStream_t stream, const RunOpts& ro, RunStats& st, 
     HIPCHK(hipEventRecord(b.ev[5], stream));
     st.launches++;
     HIPCHK(hipMemcpyAsync(b.h_res, b.res, b.n_hist * sizeof(HistResult), hipMemcpyDeviceToHost, stream));
-    HIPCHK(hipStreamSynchronize(stream));
+    HIPCHK(stream_wait(stream, b.ev[6]));
 #ifdef S2LC_GUARD
     {
       uint32_t gg[8];
@@ -592,11 +624,16 @@ int batch_run(DevBatch& b, hipStream_t stream, const RunOpts& ro, RunStats& st, 
   }
   if (b.n_hist && (other_work || !(b.n_pack8 + b.n_pack16 + b.n_pack32)))
     HIPCHK(hipMemcpyAsync(b.h_res, b.res, b.n_hist * sizeof(HistResult), hipMemcpyDeviceToHost, stream));
+  bool tail_work = false;
+  if (witness && b.n_hist && other_work) tail_work = true;
+  if (b.n_hist && (other_work || !(b.n_pack8 + b.n_pack16 + b.n_pack32))) tail_work = true;
   if (ro.round_counts) {  // every engine wrote its rounds' counts on the device
     b.h_rcounts.resize(std::max<uint64_t>(b.moves_cap, 1));
     HIPCHK(hipMemcpyAsync(b.h_rcounts.data(), b.rcounts, b.moves_cap * sizeof(uint32_t), hipMemcpyDeviceToHost, stream));
+    tail_work = true;
   }
-  HIPCHK(hipStreamSynchronize(stream));
+  if (tail_work) HIPCHK(stream_wait(stream, b.ev[6]));
+  t_tail = steady_ns();
   for (uint32_t i = 0; i < b.n_hist; ++i) {
     if (b.forced[i]) {
       b.h_res[i] = HistResult{};
@@ -622,7 +659,13 @@ int batch_run(DevBatch& b, hipStream_t stream, const RunOpts& ro, RunStats& st, 
   }
   b.rc_valid = ro.round_counts;
   st.algo_bytes += b.algo_bytes_inputs;
-  st.total_ms = (double)(steady_ns() - t0) * 1e-6;
+  const int64_t t_end = steady_ns();
+  st.total_ms = (double)(t_end - t0) * 1e-6;
+  if (step_timing && t_enq)
+    fprintf(stderr, "[s2lc step] enqueue %.1f us, wait %.1f us (kernel %.1f us), after %.1f us: events %.1f, overflow scan %.1f, "
+            "tail %.1f, stats %.1f\n", 1e-3 * (t_enq - t0), 1e-3 * (t_wait - t_enq), 1e3 * st.pack_ms,
+            1e-3 * (t_end - t_wait), 1e-3 * (t_ev - t_wait), 1e-3 * (t_over - t_ev), 1e-3 * (t_tail - t_over),
+            1e-3 * (t_end - t_tail));
   return 0;
 }
 

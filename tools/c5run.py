@@ -2,7 +2,6 @@
 (first run: level buffers allocated) and warm; one JSON line per history.
     python tools/c5run.py C5 C5bad H212"""
 import json
-import os
 import sys
 import time
 
@@ -26,10 +25,7 @@ for name in sys.argv[1:]:
                       **{k: st[k] for k in ("kernel_ms", "level_ms", "level_rounds", "level_configs", "level_children",
                                             "level_max_frontier")}}), flush=True)
 
-# Leave without running the libraries' exit-time destructors: under rocprofv3
-# --kernel-trace the HIP module destructor of the level-search code object
-# faulted inside the HIP runtime after the profiler had finalized and written
-# its output (gpurun_out/r03a/c5stats.err); the results above are complete.
-sys.stdout.flush()
-del ck
-os._exit(0)
+# release the batches and the context while the HIP runtime is fully up
+del b, ck
+import gc  # noqa: E402
+gc.collect()
