@@ -707,6 +707,10 @@ def check_events_verbose(model, events, timeout: float = 0):
     """
     key = float(timeout or 0)
     if key not in _checkers:
+        # a context holds device scratch sized from free HBM: keep the last
+        # two timeouts' contexts, not one per distinct value
+        while len(_checkers) >= 2:
+            _checkers.pop(next(iter(_checkers)))
         _checkers[key] = Checker(timeout=key)
     h = events if isinstance(events, History) else History.from_events(events)
     r = _checkers[key].check(h)

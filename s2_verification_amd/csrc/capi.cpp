@@ -689,6 +689,7 @@ int s2lc_batch_round_counts(const s2lc_batch* b, size_t i, uint32_t* out, size_t
 // the verdicts land in out[] in input order.
 int s2lc_check_batch(s2lc_ctx* c, const s2lc_history* const* hs, size_t n, s2lc_result* out) {
   if (!c || (!hs && n) || (!out && n)) return S2LC_EINVAL;
+  if (n) memset(out, 0, n * sizeof *out);  // (an error below frees whatever was filled in)
   try {
     std::vector<const History*> v(n);
     for (size_t i = 0; i < n; ++i) {
@@ -700,6 +701,10 @@ int s2lc_check_batch(s2lc_ctx* c, const s2lc_history* const* hs, size_t n, s2lc_
       Shard& sh = shard_of(c, 0);
       const int rc = shard_check(c, sh, v, out);
       if (rc) c->err = sh.err;
+      // like the sharded path: on an error other than a failed certificate
+      // nothing is returned, so nothing stays allocated
+      if (rc && rc != S2LC_EWITNESS)
+        for (size_t i = 0; i < n; ++i) s2lc_result_free(&out[i]);
       return rc;
     }
     // LPT placement

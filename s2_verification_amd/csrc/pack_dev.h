@@ -30,7 +30,10 @@ namespace s2lc {
 namespace {
 
 constexpr int PACK_F = 8;       // frontier capacity per group (configurations)
-constexpr int PACK_PF = 8;      // record hashes prefetched per lane for the next round's first expansion
+#ifndef S2LC_PACK_PF
+#define S2LC_PACK_PF 8
+#endif
+constexpr int PACK_PF = S2LC_PACK_PF;  // record hashes prefetched per lane for the next round's first expansion
 
 // fold with the first PACK_PF hashes already in registers
 __device__ __forceinline__ uint64_t fold_hashes_pf(uint64_t h, const uint64_t (&pf)[PACK_PF],
@@ -120,14 +123,17 @@ __device__ __forceinline__ uint64_t bcast_u64(uint64_t v, int src) {
 // identity ops, and the next rounds' expansions, read them from registers: a
 // window refill issues PACK_W independent loads (one memory latency) where a
 // one-record cache paid one dependent latency per advanced op.
-constexpr int PACK_W = 4;
+#ifndef S2LC_PACK_W
+#define S2LC_PACK_W 4
+#endif
+constexpr int PACK_W = S2LC_PACK_W;
 struct ChainLane {
   const OpRec* __restrict__ base;  // first record of chain l (valid iff on)
   bool on;                         // l < K
   uint32_t len;                    // records of chain l, its sentinel included
   uint32_t w0;                     // count of the window's first record
   uint32_t cc;                     // count of r
-  uint4 wa[4], wb[4], wc[4], wd[4];  // window: records at counts w0 .. w0+3
+  uint4 w[PACK_W][4];              // window: records at counts w0 .. w0+PACK_W-1
   OpRec r;                         // record at count cc (null record when !on)
 #ifdef S2LC_PROF
   bool refilled;                   // the last at() reloaded the window
@@ -156,12 +162,12 @@ struct ChainLane {
       // clamp to the chain: a record past its sentinel is never selected
       const OpRec* q = base + c;
       const uint32_t last = len - 1 - c;  // c < len always (sentinel included)
-      const uint4* qa = reinterpret_cast<const uint4*>(q);
-      const uint4* qb = reinterpret_cast<const uint4*>(q + min(1u, last));
-      const uint4* qc = reinterpret_cast<const uint4*>(q + min(2u, last));
-      const uint4* qd = reinterpret_cast<const uint4*>(q + min(3u, last));
 #pragma unroll
-      for (int k = 0; k < 4; ++k) { wa[k] = qa[k]; wb[k] = qb[k]; wc[k] = qc[k]; wd[k] = qd[k]; }
+      for (int i = 0; i < PACK_W; ++i) {
+        const uint4* qi = reinterpret_cast<const uint4*>(q + min((uint32_t)i, last));
+#pragma unroll
+        for (int k = 0; k < 4; ++k) w[i][k] = qi[k];
+      }
       w0 = c;
       o = 0;
     }
@@ -169,11 +175,15 @@ struct ChainLane {
     uint4 sel[4];
 #pragma unroll
     for (int k = 0; k < 4; ++k) {
-      const uint4 A = wa[k], B = wb[k], C = wc[k], D = wd[k];
-      sel[k].x = o == 0 ? A.x : o == 1 ? B.x : o == 2 ? C.x : D.x;
-      sel[k].y = o == 0 ? A.y : o == 1 ? B.y : o == 2 ? C.y : D.y;
-      sel[k].z = o == 0 ? A.z : o == 1 ? B.z : o == 2 ? C.z : D.z;
-      sel[k].w = o == 0 ? A.w : o == 1 ? B.w : o == 2 ? C.w : D.w;
+      sel[k] = w[0][k];
+#pragma unroll
+      for (int i = 1; i < PACK_W; ++i) {
+        const bool t = o == (uint32_t)i;
+        sel[k].x = t ? w[i][k].x : sel[k].x;
+        sel[k].y = t ? w[i][k].y : sel[k].y;
+        sel[k].z = t ? w[i][k].z : sel[k].z;
+        sel[k].w = t ? w[i][k].w : sel[k].w;
+      }
     }
     __builtin_memcpy(&r, sel, sizeof(OpRec));
     cc = c;

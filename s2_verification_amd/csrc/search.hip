@@ -17,6 +17,7 @@
 // (configuration, chain) candidate. Frontier, staging and table live in a
 // per-workgroup HBM slab (L2-resident at these sizes); chain offsets in LDS.
 #include <hip/hip_runtime.h>
+#include <hip/hip_ext.h>
 #include <stdio.h>
 #include <stdlib.h>
 #include <string.h>
@@ -382,11 +383,10 @@ int batch_run(DevBatch& b, hipStream_t stream, const RunOpts& ro, RunStats& st, 
   prm.n_recs = b.n_recs; prm.n_pool = b.n_pool; prm.n_res = b.n_hist;
   prm.rcounts = ro.round_counts ? b.rcounts : nullptr;
 
-  HIPCHK(hipMemsetAsync(b.counter, 0, 32 * sizeof(uint32_t), stream));
-  if (b.n_hist) {
-    hipLaunchKernelGGL(reset_results_kernel, dim3((b.n_hist + 255) / 256), dim3(256), 0, stream, b.res, b.n_hist);
-    HIPCHK(hipGetLastError());
-  }
+  // one dispatch resets the results and zeroes the work counters
+  hipLaunchKernelGGL(reset_results_kernel, dim3(std::max<uint32_t>(1, (b.n_hist + 255) / 256)), dim3(256), 0, stream,
+                     b.res, b.n_hist, b.counter);
+  HIPCHK(hipGetLastError());
   if (deadline_ns) {
     int rate_khz = 100000;  // device wall clock (s_memrealtime); 100 MHz on gfx950
     (void)hipDeviceGetAttribute(&rate_khz, hipDeviceAttributeWallClockRate, dev);
@@ -469,12 +469,14 @@ int batch_run(DevBatch& b, hipStream_t stream, const RunOpts& ro, RunStats& st, 
       const uint32_t groups = (PACK_BLOCK / 64) * gpw;
       const uint32_t grid = std::max<uint32_t>(
           1, std::min<uint32_t>((n_l + groups - 1) / groups, (uint32_t)n_cu * (uint32_t)std::max(1, bpc)));
-      HIPCHK(hipEventRecord(b.ev[2 * li], stream));
-      if (li == 0) hipLaunchKernelGGL(pack_kernel<8>, dim3(grid), dim3(PACK_BLOCK), smem, stream, pp);
-      else if (li == 1) hipLaunchKernelGGL(pack_kernel<16>, dim3(grid), dim3(PACK_BLOCK), smem, stream, pp);
-      else hipLaunchKernelGGL(pack_kernel<32>, dim3(grid), dim3(PACK_BLOCK), smem, stream, pp);
+      // start / stop timestamps taken by the dispatch itself (no marker packets
+      // around it: with hipEventRecord the launch started 20-30 us after the
+      // previous kernel ended, rocprofv3 trace r03a)
+      hipEvent_t e0 = b.ev[2 * li], e1 = b.ev[2 * li + 1];
+      if (li == 0) hipExtLaunchKernelGGL(pack_kernel<8>, dim3(grid), dim3(PACK_BLOCK), smem, stream, e0, e1, 0, pp);
+      else if (li == 1) hipExtLaunchKernelGGL(pack_kernel<16>, dim3(grid), dim3(PACK_BLOCK), smem, stream, e0, e1, 0, pp);
+      else hipExtLaunchKernelGGL(pack_kernel<32>, dim3(grid), dim3(PACK_BLOCK), smem, stream, e0, e1, 0, pp);
       HIPCHK(hipGetLastError());
-      HIPCHK(hipEventRecord(b.ev[2 * li + 1], stream));
       launched[li] = true;
       st.launches++;
     }

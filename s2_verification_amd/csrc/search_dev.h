@@ -112,8 +112,9 @@ __global__ __attribute__((unused)) void deadline_kernel(unsigned long long* d, u
 
 // Every history of the batch starts a run undecided (a history that no engine
 // reaches in this run, e.g. after a timeout, must not keep a stale verdict).
-__global__ __attribute__((unused)) void reset_results_kernel(HistResult* res, uint32_t n) {
+__global__ __attribute__((unused)) void reset_results_kernel(HistResult* res, uint32_t n, uint32_t* counter) {
   const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (counter && i < 32) counter[i] = 0;  // work counters, deadline, trace head
   if (i >= n) return;
   HistResult& r = res[i];
   r.verdict = V_UNKNOWN;

@@ -5,10 +5,17 @@ the same verdict AND the same count in every completed round (tests/
 test_engines.py): same reductions => same configuration set per round, so
 this pins the search itself, not only its final bit.
 
-Which ablations: only those whose search stays small on these histories.
-Switching P1, P4 (on the Ok histories) or the indefinite deferral off makes
-them explode (tens of millions of configurations); those switches are
-exercised on the mid-size histories instead, live in the test.
+Which ablations: complete searches for those that stay small on these
+histories (all on, P2 off, P4 off on C5bad). Switching P1 or the indefinite
+deferral off makes them explode: with P1 off, H174 passes 66 M unique
+configurations by round 1,037 of ~10,300 (frontier 7.4 M) and C5bad 61 M by
+round 668; with the deferral off neither passes round ~1,000 within 30 CPU
+minutes. For those (PREFIX) the search runs under a configuration budget
+(or_check_reduced's max_configs) and the fixture keeps the counts of every
+round completed before it ran out ("complete": false): the GPU, under a
+smaller budget, must reproduce that prefix round by round. The whole-search
+P1 / deferral ablations are exercised on the mid-size histories, live in the
+test.
 
 Run here (not on the GPU box): python tests/golden/make_round_counts.py
 """
@@ -26,6 +33,8 @@ from s2_verification_amd import workloads as W  # noqa: E402
 from helpers import config_digest  # noqa: E402
 
 CASES = {"H174": [0, 2], "H212": [0, 2], "C5bad": [0, 2, 4], "C5wide": [0]}
+# (reductions_off, configuration budget): prefix fixtures of exploding ablations
+PREFIX = {"H174": [(1, 60_000_000), (8, 30_000_000)], "C5bad": [(1, 60_000_000), (8, 30_000_000)]}
 
 
 def main(names):
@@ -42,6 +51,13 @@ def main(names):
             out[name][str(off)] = {"verdict": v, "rounds": st["rounds"], "configs": st["configs"],
                                    "counts": st["round_counts"], "cpu_seconds": round(time.time() - t, 1)}
             print(name, off, v, st["rounds"], st["configs"], flush=True)
+        for off, budget in PREFIX.get(name, []):
+            t = time.time()
+            v, st = orc.check_reduced(ea, reductions_off=off, round_counts=True, max_configs=budget)
+            out[name][f"{off}p"] = {"verdict": v, "budget": budget, "complete": v != "Unknown",
+                                     "rounds": st["rounds"], "configs": st["configs"], "max_frontier": st["max_frontier"],
+                                     "counts": st["round_counts"], "cpu_seconds": round(time.time() - t, 1)}
+            print(name, f"{off}p", v, st["rounds"], st["configs"], flush=True)
     with open(path, "w") as f:
         json.dump(out, f, sort_keys=True, separators=(",", ":"))
 

@@ -234,6 +234,31 @@ def test_hard_round_counts(name, off, mode, monkeypatch):
         assert st["level_solo_rounds"] > r.rounds // 2, st
 
 
+@pytest.mark.parametrize("mode", ["default", "no_persist"])
+@pytest.mark.parametrize("name,off", [("H174", 1), ("H174", 8), ("C5bad", 1), ("C5bad", 8)])
+def test_hard_exploding_ablation_prefix(name, off, mode, monkeypatch):
+    """P1 or the indefinite deferral switched off on the hard histories: the
+    search explodes (tens of millions of configurations; make_round_counts.py),
+    so the fixture holds the CPU reduced search's counts for every round it
+    completed within a budget. Under a smaller budget the GPU must stop with
+    Unknown (budget) and reproduce that prefix round by round."""
+    from s2_verification_amd import workloads as W
+    _set_mode(monkeypatch, mode)
+    ref = golden("hard_round_counts.json")[name]
+    assert config_digest(name) == ref["digest"], "simulator output changed: regenerate the fixture"
+    want = ref[f"{off}p"]
+    assert not want["complete"] and want["verdict"] == "Unknown"
+    h = W.config_history(name)
+    c = s2.Checker(round_counts=True, reductions_off=off, max_configs=2_000_000, engine=s2.ENGINE_LEVEL)
+    b = c.batch([h])
+    r = b.check(with_witness=False)[0]
+    assert r.verdict == s2.Unknown and r.reason == "budget", r
+    got = b.round_counts(0)
+    assert 50 < len(got) < len(want["counts"]), (len(got), len(want["counts"]))
+    bad = [k for k, (x, y) in enumerate(zip(got[:-1], want["counts"])) if x != y]
+    assert not bad, (name, off, mode, bad[:5])
+
+
 @pytest.mark.parametrize("mode", ["default", "no_solo", "all_persist"])
 @pytest.mark.parametrize("abl", ["all_on", "no_p2", "no_idefer"])
 def test_level_persist_round_counts_match_reduced_search(mode, abl, monkeypatch):
