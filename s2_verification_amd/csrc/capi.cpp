@@ -376,6 +376,10 @@ namespace {
 int collect_results(DevBatch& B, const RunStats& stats, bool witness_recorded, s2lc_result* out, int with_witness,
                     std::string& err, int64_t* flat_ids = nullptr, const uint64_t* flat_offs = nullptr) {
   const bool want_w = with_witness && witness_recorded;
+  {
+    const int rc = batch_host_results(B, err);
+    if (rc) return rc;
+  }
   if (want_w && B.n_hist) {
     const int rc = batch_fetch_moves(B, err);
     if (rc) return rc;
@@ -575,6 +579,7 @@ int s2lc_batch_results_flat(s2lc_ctx* c, s2lc_batch* b, int32_t* verdicts, int32
     // offsets first: a certified Ok witness is every op of its history, so
     // the witnesses are written in place by the certifying threads
     const bool want = witness_ids != nullptr && b->witness;
+    if (const int rc0 = batch_host_results(B, c->err)) return rc0;
     uint64_t total = 0;
     for (size_t i = 0; i < n; ++i) {
       witness_offs[i] = total;

@@ -44,6 +44,9 @@ __device__ __forceinline__ uint64_t fold_hashes_pf(uint64_t h, const uint64_t (&
   return n > (uint32_t)PACK_PF ? fold_hashes_blk(h, rs + PACK_PF, n - PACK_PF) : h;
 }
 constexpr int PACK_BLOCK = 256; // threads per workgroup
+// per-launch totals (Params::agg[0..7]): the run's statistics without reading
+// every history's result back (batch_run's fast path)
+enum { PACK_AGG_CONFIGS, PACK_AGG_CHILDREN, PACK_AGG_ROUNDS, PACK_AGG_SEARCH_BYTES, PACK_AGG_OVERFLOW, PACK_AGG_SETTLED };
 
 template <int L>
 struct __attribute__((aligned(8))) PCfg {
@@ -122,9 +125,12 @@ __device__ __forceinline__ uint64_t bcast_u64(uint64_t v, int src) {
 // PACK_W consecutive records. A closure that advances a chain by several
 // identity ops, and the next rounds' expansions, read them from registers: a
 // window refill issues PACK_W independent loads (one memory latency) where a
-// one-record cache paid one dependent latency per advanced op.
+// one-record cache paid one dependent latency per advanced op. Two records
+// (161 VGPRs: 3 waves per SIMD) beat four (193: 2 waves) on C4 by 1-4 %
+// (tools/variant_sweep.sh, profiles/r03/pack_variants.txt); every record a
+// pass selects costs 16 v_cndmask per extra window slot.
 #ifndef S2LC_PACK_W
-#define S2LC_PACK_W 4
+#define S2LC_PACK_W 2
 #endif
 constexpr int PACK_W = S2LC_PACK_W;
 struct ChainLane {
@@ -275,6 +281,8 @@ __global__ __launch_bounds__(PACK_BLOCK, S2LC_PACK_MINW) void pack_kernel(Params
   // price of fewer histories in flight (the host picks gpw from the batch)
   if (p.gpw && (uint32_t)(lane / L) >= p.gpw) return;
   uint32_t tbase = 0, tleft = 0;  // group's trace chunk (uniform)
+  // this group's totals (lane gl == 0), added to p.agg once at the end
+  unsigned long long a_cfg = 0, a_ch = 0, a_rounds = 0, a_bytes = 0, a_ovf = 0, a_set = 0;
   for (;;) {
     uint32_t hi = 0;
     if (gl == 0) hi = atomicAdd(p.counter, 1u);
@@ -497,6 +505,13 @@ __global__ __launch_bounds__(PACK_BLOCK, S2LC_PACK_MINW) void pack_kernel(Params
     }
 #endif
     if (gl == 0) {
+      if (verdict == V_UNKNOWN && reason == S2LC_R_FRONTIER) {
+        ++a_ovf;
+      } else {
+        const uint64_t S = 8 * ((2 * (uint64_t)K + 20 + 7) / 8);  // DESIGN.md §5 accounting
+        a_cfg += configs; a_ch += children; a_rounds += rounds; ++a_set;
+        a_bytes += 2 * S * configs + 8 * children;
+      }
       HistResult& R = p.res[h];
       R.verdict = verdict;
       R.reason = reason;
@@ -546,6 +561,14 @@ __global__ __launch_bounds__(PACK_BLOCK, S2LC_PACK_MINW) void pack_kernel(Params
       }
       R.has_witness = hw;
     }
+  }
+  if (p.agg && gl == 0 && (a_set | a_ovf)) {
+    atomicAdd(p.agg + PACK_AGG_CONFIGS, a_cfg);
+    atomicAdd(p.agg + PACK_AGG_CHILDREN, a_ch);
+    atomicAdd(p.agg + PACK_AGG_ROUNDS, a_rounds);
+    atomicAdd(p.agg + PACK_AGG_SEARCH_BYTES, a_bytes);
+    atomicAdd(p.agg + PACK_AGG_SETTLED, a_set);
+    if (a_ovf) atomicAdd(p.agg + PACK_AGG_OVERFLOW, a_ovf);
   }
 }
 

@@ -135,6 +135,13 @@ struct DevBatch {
   size_t h_moves_cap = 0;
   std::vector<uint32_t> h_rcounts;   // host copy of rcounts after a run with round counts
   bool rc_valid = false;
+  // h_res not read back by the last run (every history settled by the packed
+  // kernels: the run read their per-launch totals only); batch_host_results
+  // copies it on first use
+  bool h_res_stale = false;
+  unsigned long long* agg = nullptr;   // device: per packed launch, 8 totals (pack_kernel PackAgg)
+  unsigned long long* h_agg = nullptr; // pinned copy
+  uint64_t in_bytes_list[3] = {0, 0, 0};  // input SoA bytes of each packed list
   std::vector<const History*> src;   // host histories (not owned)
   std::vector<uint32_t> forced;      // per history: 0 search, else verdict fixed on host
   uint64_t algo_bytes_inputs = 0;
@@ -171,6 +178,8 @@ int batch_upload(DevBatch& b, const std::vector<const History*>& hs, uint32_t re
 void batch_release(DevBatch& b);
 // Copy the witness moves of the last run into b.h_moves (pinned).
 int batch_fetch_moves(DevBatch& b, std::string& err);
+// h_res valid on the host (copies it if the last run left it on the device)
+int batch_host_results(DevBatch& b, std::string& err);
 // out[i] = fold_hashes_blk(seeds[i], pool[offs[i] ..+ cnts[i]]) on the device.
 int device_fold(const uint64_t* seeds, const uint64_t* pool, size_t pool_len, const uint32_t* offs, const uint32_t* cnts,
                 size_t n, uint64_t* out, hipStream_t stream, std::string& err);

@@ -296,12 +296,25 @@ int batch_upload(DevBatch& b, const std::vector<const History*>& hs, uint32_t re
   b.n_pack16 = no - b.n_pack8;
   for (uint32_t i : b.lpt) if (((b.h_hist[i].K > 16 && b.h_hist[i].K <= 32) || to32[i]) && t32(i)) s_order[no++] = i;
   b.n_pack32 = no - b.n_pack8 - b.n_pack16;
+  {
+    const uint32_t lim[3] = {b.n_pack8, b.n_pack8 + b.n_pack16, no};
+    uint32_t k = 0;
+    for (int li = 0; li < 3; ++li) {
+      b.in_bytes_list[li] = 0;
+      for (; k < lim[li]; ++k) b.in_bytes_list[li] += b.h_in_bytes[s_order[k]];
+    }
+  }
+  b.h_res_stale = false;
   HIPCHK(hipMemcpy(b.arena, b.stage, stage_bytes, hipMemcpyHostToDevice));
   return 0;
 }
 
 void batch_release(DevBatch& b) {
   level_release(b);
+  if (b.agg) (void)hipFree(b.agg);
+  if (b.h_agg) (void)hipHostFree(b.h_agg);
+  b.agg = nullptr;
+  b.h_agg = nullptr;
   void* dptrs[] = {b.arena, b.counter, b.trace, b.slab};  // trace_head lives inside counter
   for (void* q : dptrs) if (q) (void)hipFree(q);
   if (b.stage) (void)hipHostFree(b.stage);
@@ -384,8 +397,13 @@ int batch_run(DevBatch& b, hipStream_t stream, const RunOpts& ro, RunStats& st, 
   prm.rcounts = ro.round_counts ? b.rcounts : nullptr;
 
   // one dispatch resets the results and zeroes the work counters
+  if (!b.agg) {
+    HIPCHK(hipMalloc(&b.agg, 32 * sizeof(unsigned long long)));
+    HIPCHK(hipHostMalloc(&b.h_agg, 32 * sizeof(unsigned long long), hipHostMallocDefault));
+  }
+  b.h_res_stale = false;
   hipLaunchKernelGGL(reset_results_kernel, dim3(std::max<uint32_t>(1, (b.n_hist + 255) / 256)), dim3(256), 0, stream,
-                     b.res, b.n_hist, b.counter);
+                     b.res, b.n_hist, b.counter, b.agg);
   HIPCHK(hipGetLastError());
   if (deadline_ns) {
     int rate_khz = 100000;  // device wall clock (s_memrealtime); 100 MHz on gfx950
@@ -444,6 +462,7 @@ int batch_run(DevBatch& b, hipStream_t stream, const RunOpts& ro, RunStats& st, 
       pp.order = b.order + first[li];
       pp.n_hist = n_l;
       pp.counter = b.counter + 12 + li;
+      pp.agg = b.agg + 8 * li;
       const uint32_t L = 8u << li;
       const size_t smem = li == 0 ? pack_smem_bytes<8>() : li == 1 ? pack_smem_bytes<16>() : pack_smem_bytes<32>();
       int bpc = b.pack_bpc[li];  // resident blocks per CU (queried once per batch)
@@ -481,10 +500,50 @@ int batch_run(DevBatch& b, hipStream_t stream, const RunOpts& ro, RunStats& st, 
       st.launches++;
     }
     // (pack_kernel resolves its histories' witnesses itself: no walk here)
-    HIPCHK(hipMemcpyAsync(b.h_res, b.res, b.n_hist * sizeof(HistResult), hipMemcpyDeviceToHost, stream));
+    // Fast path: every history of the batch is in a packed list and no
+    // round counts are wanted. The run then reads back only the launches'
+    // totals; the per-history results stay on the device until asked for
+    // (batch_host_results). A history that outgrew its packed frontier sends
+    // the run down the full path (results read back, overflow scan).
+    uint32_t n_forced = 0;
+    for (uint32_t i = 0; i < b.n_hist; ++i) n_forced += b.forced[i] ? 1u : 0u;
+    const bool fast = todo.empty() && level.empty() && !ro.round_counts && n_packed + n_forced == b.n_hist;
+    if (fast)
+      HIPCHK(hipMemcpyAsync(b.h_agg, b.agg, 24 * sizeof(unsigned long long), hipMemcpyDeviceToHost, stream));
+    else
+      HIPCHK(hipMemcpyAsync(b.h_res, b.res, b.n_hist * sizeof(HistResult), hipMemcpyDeviceToHost, stream));
     t_enq = steady_ns();
     HIPCHK(stream_wait(stream, b.ev[6]));
     t_wait = steady_ns();
+    if (fast && b.h_agg[PACK_AGG_OVERFLOW] + b.h_agg[8 + PACK_AGG_OVERFLOW] + b.h_agg[16 + PACK_AGG_OVERFLOW] == 0) {
+      for (int li = 0; li < 3; ++li) {
+        if (!launched[li]) continue;
+        float ms = 0;
+        HIPCHK(hipEventElapsedTime(&ms, b.ev[2 * li], b.ev[2 * li + 1]));
+        st.kernel_ms += ms;
+        st.pack_ms += ms;
+        if (li == 0) st.pack8_ms = ms;
+        if (li == 1) st.pack16_ms = ms;
+        const unsigned long long* a = b.h_agg + 8 * li;
+        st.configs += a[PACK_AGG_CONFIGS];
+        st.children += a[PACK_AGG_CHILDREN];
+        st.rounds += a[PACK_AGG_ROUNDS];
+        st.algo_bytes += a[PACK_AGG_SEARCH_BYTES];
+        // (S2LC_PACK8 lists settle in pack_kernel<8>; the 32-lane list is not a roofline line)
+        if (li == 0) { st.pack8_algo_bytes = a[PACK_AGG_SEARCH_BYTES] + b.in_bytes_list[0]; st.pack8_histories = (uint32_t)a[PACK_AGG_SETTLED]; }
+        if (li == 1) { st.pack16_algo_bytes = a[PACK_AGG_SEARCH_BYTES] + b.in_bytes_list[1]; st.pack16_histories = (uint32_t)a[PACK_AGG_SETTLED]; }
+      }
+      st.algo_bytes += b.algo_bytes_inputs;
+      b.h_res_stale = true;
+      const int64_t t_end = steady_ns();
+      st.total_ms = (double)(t_end - t0) * 1e-6;
+      if (step_timing)
+        fprintf(stderr, "[s2lc step] enqueue %.1f us, wait %.1f us (kernel %.1f us), after %.1f us (totals only)\n",
+                1e-3 * (t_enq - t0), 1e-3 * (t_wait - t_enq), 1e3 * st.pack_ms, 1e-3 * (t_end - t_wait));
+      return 0;
+    }
+    if (fast)  // a packed frontier overflowed: the full path needs every result
+      HIPCHK(hipMemcpy(b.h_res, b.res, b.n_hist * sizeof(HistResult), hipMemcpyDeviceToHost));
     for (int li = 0; li < 3; ++li) {
       if (!launched[li]) continue;
       float ms = 0;
@@ -671,6 +730,20 @@ int batch_run(DevBatch& b, hipStream_t stream, const RunOpts& ro, RunStats& st, 
   return 0;
 }
 
+
+int batch_host_results(DevBatch& b, std::string& err) {
+  if (!b.h_res_stale) return 0;
+  HIPCHK(hipMemcpy(b.h_res, b.res, b.n_hist * sizeof(HistResult), hipMemcpyDeviceToHost));
+  for (uint32_t i = 0; i < b.n_hist; ++i)
+    if (b.forced[i]) {
+      b.h_res[i] = HistResult{};
+      b.h_res[i].verdict = V_ILLEGAL;
+      b.h_res[i].reason = S2LC_R_UNMATCHED;
+      b.h_res[i].witness_off = b.h_moves_off[i];
+    }
+  b.h_res_stale = false;
+  return 0;
+}
 
 int batch_fetch_moves(DevBatch& b, std::string& err) {
   if (grow_pinned(reinterpret_cast<uint8_t**>(&b.h_moves), b.h_moves_cap, std::max<uint64_t>(b.moves_cap, 1) * sizeof(uint32_t),

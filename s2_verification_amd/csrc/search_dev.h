@@ -104,6 +104,7 @@ struct Params {
   uint32_t* rcounts;               // per-round unique configurations at res[h].witness_off (nullable)
   const unsigned long long* deadline;  // wall_clock64() value after which histories give Unknown (nullable)
   uint32_t gpw;                    // pack kernels: lane groups per wave that take histories (0 = all)
+  unsigned long long* agg;         // pack kernels: this launch's totals (PACK_AGG_*; nullable)
 };
 
 // The run's deadline in device wall-clock ticks (written once per run, read by
@@ -112,9 +113,11 @@ __global__ __attribute__((unused)) void deadline_kernel(unsigned long long* d, u
 
 // Every history of the batch starts a run undecided (a history that no engine
 // reaches in this run, e.g. after a timeout, must not keep a stale verdict).
-__global__ __attribute__((unused)) void reset_results_kernel(HistResult* res, uint32_t n, uint32_t* counter) {
+__global__ __attribute__((unused)) void reset_results_kernel(HistResult* res, uint32_t n, uint32_t* counter,
+                                                             unsigned long long* agg) {
   const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
   if (counter && i < 32) counter[i] = 0;  // work counters, deadline, trace head
+  if (agg && i < 32) agg[i] = 0;          // packed launches' totals
   if (i >= n) return;
   HistResult& r = res[i];
   r.verdict = V_UNKNOWN;
