@@ -332,7 +332,8 @@ template <int NQ>
 __device__ __forceinline__ int lv_closure(LvHot (&H)[NQ], uint32_t (&d)[NQ], const uint32_t (&cnt)[NQ],
                                           const uint32_t* s_cs, const LvHeadsLds<NQ>& PL, int lane, const State& s,
                                           uint32_t hflags, uint32_t minret_seed, const OpRec* __restrict__ recs,
-                                          uint32_t& minret_out, const LvHeadsLds<NQ>* NX = nullptr) {
+                                          uint32_t& minret_out, const LvHeadsLds<NQ>* NX = nullptr,
+                                          unsigned long long* prof = nullptr) {
   const bool nowrap = hflags & H_NOWRAP;
   const bool p2 = hflags & H_P2OK;
   const bool p4 = hflags & H_P4;
@@ -355,6 +356,11 @@ __device__ __forceinline__ int lv_closure(LvHot (&H)[NQ], uint32_t (&d)[NQ], con
     }
     const uint32_t minret = wave_min_u32(mr);
     const uint64_t bound = wave_min_u64(bd);
+#ifdef S2LC_PROF
+    if (prof && lane == 0) atomicAdd(prof, 1ull);  // passes
+#else
+    (void)prof;
+#endif
     if (__ballot(dead) || (nowrap && s.tail > bound)) return CL_DEAD;
     const bool changed = __ballot(adv != 0) != 0;
     if (!changed && minret == minret_prev) {
@@ -371,6 +377,9 @@ __device__ __forceinline__ int lv_closure(LvHot (&H)[NQ], uint32_t (&d)[NQ], con
           H[q].fl = fl | HB_KNOWN | lv_legal_bits(fl, NX->otail[q][lane], NX->ohash[q][lane], s);
         } else {
           H[q] = lv_load_child_head(recs + s_cs[64 * q + lane] + cnt[q] + d[q], s);
+#ifdef S2LC_PROF
+          if (prof) atomicAdd(prof + 1, 1ull);  // head loads from memory (per lane)
+#endif
         }
       }
     }
@@ -482,6 +491,7 @@ __device__ __forceinline__ void lv_drain() { asm volatile("s_waitcnt vmcnt(0)" :
 // slices per configuration, and (fused insert) the round's trace base.
 struct LvRoundIn {
   uint32_t f0, nf;  // frontier positions [f0, f0 + nf) of cur_idx (init: the initial configuration)
+  uint32_t par;     // solo rounds: the round's counter slot (LvSolo::c)
   uint32_t S;       // slices per configuration
   uint32_t tbase;   // trace index of the round's first winner (fused insert)
   uint32_t wit;     // record trace entries (fused insert)
@@ -615,12 +625,17 @@ struct LvSolo {
   uint64_t tail, hash, chx;        // the configuration: state, XOR of its chain terms
   uint64_t ktail, khash, kchx;     // the kept child
   uint32_t tok, pmin, ptrace, ktok, kmr, kmv, cs_end;
-  uint32_t alive, found, fpar, fmov, fp4, ovf, tbase, wit;
-  unsigned long long kids;
+  uint32_t tbase, wit;
+  // the round's outcome, by round parity: round n counts into c[n & 1] while
+  // its close zeroes c[(n + 1) & 1] (no barrier between reading and resetting)
+  struct Ctr {
+    uint32_t alive, found, fpar, fmov, fp4, ovf;
+    unsigned long long kids;
+  } c[2];
   uint64_t wx[LV_BLOCK / 64];
 #ifdef S2LC_PROF
   unsigned long long pt[8];  // wave 0 phase cycles: [0] start [1] setup [2] pre [3] moves [4] close [5] next; [7] last stamp
-  unsigned long long pc[4];  // closure cycles (ALIVE, other), ALIVE closures, stage cycles (all waves)
+  unsigned long long pc[6];  // closure cycles (ALIVE, other), ALIVE closures, stage cycles (all waves), closure passes, closure head loads
 #endif
 };
 
@@ -940,7 +955,12 @@ __device__ __forceinline__ bool lv_expand(const LvParams& p, const LvRoundIn& in
         const unsigned long long tc0_ = clock64();
 #endif
         ++closed;
+#ifdef S2LC_PROF
+        const int cr = lv_closure<NQ>(H, d, cnt, s_cs, PL, lane, cs_, p.hflags, pmin, p.recs, mr, SOLO ? NX : nullptr,
+                                      SOLO ? &sol->pc[4] : nullptr);
+#else
         const int cr = lv_closure<NQ>(H, d, cnt, s_cs, PL, lane, cs_, p.hflags, pmin, p.recs, mr, SOLO ? NX : nullptr);
+#endif
 #ifdef S2LC_PROF
         if (SOLO && lane == 0) {  // closure cycles: [8] ALIVE, [9] others; [10] ALIVE count; [11] stage cycles
           asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -953,10 +973,10 @@ __device__ __forceinline__ bool lv_expand(const LvParams& p, const LvRoundIn& in
         LV_LAP(3);
         if (cr == CL_COMPLETE || cr == CL_P4) {
           if (SOLO) {
-            if (lane == 0 && atomicCAS(&sol->found, 0u, 1u) == 0u) {
-              sol->fpar = ptrace;
-              sol->fmov = mv;
-              sol->fp4 = cr == CL_P4 ? 1u : 0u;
+            if (lane == 0 && atomicCAS(&sol->c[in.par].found, 0u, 1u) == 0u) {
+              sol->c[in.par].fpar = ptrace;
+              sol->c[in.par].fmov = mv;
+              sol->c[in.par].fp4 = cr == CL_P4 ? 1u : 0u;
             }
           } else if (lane == 0 && atomicCAS(&p.ctl->found, 0u, 1u) == 0u) {
             atomicExch(&p.ctl->found_parent, ptrace);
@@ -976,7 +996,7 @@ __device__ __forceinline__ bool lv_expand(const LvParams& p, const LvRoundIn& in
             // distinct children: staging slot = arrival order; the first one is
             // kept in LDS in case it turns out to be the round's only survivor
             uint32_t k = 0;
-            if (lane == 0) k = atomicAdd(&sol->alive, 1u);
+            if (lane == 0) k = atomicAdd(&sol->c[in.par].alive, 1u);
             k = rl(k, 0);
             // the first survivor stays in LDS only: it is written to the
             // staging array after the round if it is not the only one
@@ -990,7 +1010,7 @@ __device__ __forceinline__ bool lv_expand(const LvParams& p, const LvRoundIn& in
             } else if (k < p.scs) {
               lv_solo_put<NQ>(p, k, cs_, fp, mr, ptrace, mv, in.tbase, in.wit, cnt, d);
             } else if (lane == 0) {
-              sol->ovf = 1u;
+              sol->c[in.par].ovf = 1u;
             }
 #ifdef S2LC_PROF
             if (lane == 0) atomicAdd(&sol->pc[3], clock64() - ts0_);
@@ -1022,7 +1042,7 @@ __device__ __forceinline__ bool lv_expand(const LvParams& p, const LvRoundIn& in
   }
 #endif
   if (MODE == 0 && rleft) lv_release<NQ>(p, stripe, rk, rleft);
-  if (lane == 0 && kids) atomicAdd(SOLO ? &sol->kids : &p.ctl->children, kids);
+  if (lane == 0 && kids) atomicAdd(SOLO ? &sol->c[in.par].kids : &p.ctl->children, kids);
   if (!SOLO && lane == 0 && closed) atomicAdd(&p.ctl->closed, closed);
   return wave_id < items;
 }
@@ -1038,6 +1058,7 @@ __global__ __launch_bounds__(LV_BLOCK) void lv_round(LvParams p) {
   for (uint32_t x = threadIdx.x; x < 64u * NQ; x += LV_BLOCK) s_cs[x] = x < p.K ? p.cs[x] : 0u;
   __syncthreads();
   LvRoundIn in;
+  in.par = 0;
   in.f0 = p.f0;
   in.nf = p.f1 == LV_NONE ? p.run->nf : p.f1 - p.f0;
   if (p.f1 == LV_NONE) in.f0 = 0;
@@ -1431,66 +1452,74 @@ __device__ void lv_solo_rounds(const LvParams& p, const LvPersist& q, LvRun& R, 
   uint32_t n_solo = 0;
 #endif
 #ifdef S2LC_PROF
-  if (threadIdx.x == 0) { for (int i_ = 0; i_ < 8; ++i_) S.pt[i_] = 0; for (int i_ = 0; i_ < 4; ++i_) S.pc[i_] = 0; S.pt[7] = clock64(); }
+  if (threadIdx.x == 0) { for (int i_ = 0; i_ < 8; ++i_) S.pt[i_] = 0; for (int i_ = 0; i_ < 6; ++i_) S.pc[i_] = 0; S.pt[7] = clock64(); }
 #define LV_SOLO_T(i) do { if (threadIdx.x == 0) { const unsigned long long t_ = clock64(); S.pt[i] += t_ - S.pt[7]; S.pt[7] = t_; } } while (0)
 #else
 #define LV_SOLO_T(i) do { } while (0)
 #endif
+  if (threadIdx.x == 0) {
+    for (int i = 0; i < 2; ++i) S.c[i] = typename LvSolo<NQ>::Ctr{0, 0, 0, 0, 0, 0, 0ull};
+    S.tbase = (uint32_t)R.tnext; S.wit = R.witness;
+  }
+  lv_sync_lds();
+  // Two workgroup barriers per round: after the expansion (its outcome is
+  // final), and after the close. When the round's only survivor carries on,
+  // its advanced heads are reloaded right after the first barrier, in the
+  // shadow of thread 0's close of the run state.
   for (uint32_t n = 0; n < max_rounds; ++n) {
     const uint32_t r = R.round + 1;
+    const uint32_t par = n & 1u;
 #ifdef S2LC_PROF
     ++n_solo;
 #endif
-    if (threadIdx.x == 0) {
-      S.alive = 0; S.found = 0; S.ovf = 0; S.kids = 0;
-      S.tbase = (uint32_t)R.tnext; S.wit = R.witness;
-    }
-    lv_sync_lds();
     LvParams rp = p;
     rp.round = r;
     rp.stg = q.stg[r & 1];
     rp.nxt_idx = q.idx[r & 1];
     LvRoundIn in;
-    in.f0 = 0; in.nf = 1; in.S = LV_BLOCK / 64; in.tbase = S.tbase; in.wit = S.wit;
+    in.f0 = 0; in.nf = 1; in.par = par; in.S = LV_BLOCK / 64; in.tbase = S.tbase; in.wit = S.wit;
     LV_SOLO_T(0);
     (void)lv_expand<NQ, 2>(rp, in, PL, s_cs, &S, NX, FR);
     LV_SOLO_T(3);
     lv_sync_lds();
-    if (threadIdx.x == 0) {
-      LvCounts k;
-      k.nn = S.alive; k.ovf = S.ovf; k.fnd = S.found;
-      k.fpar = S.fpar; k.fmov = S.fmov; k.fp4 = S.fp4; k.ch = S.kids; k.closed = 0;
-      lv_close_state(R, k, r, p.rcounts, p.scap, p.trace_cap);
-      R.solo_rounds++;
-      // the first survivor's trace entry (it was not staged)
-      if (!S.found && !S.ovf && S.alive && S.wit) p.trace[S.tbase] = TraceEnt{S.ptrace, S.kmv};
-    }
-    lv_sync_lds();
-    if (S.ovf && !S.found) {
-      // the host re-runs round r from its frontier: this configuration, in
-      // the staging array the round read its frontier from
-      lv_solo_write<NQ>(S, false, q.stg[(r + 1) & 1], q.idx[(r + 1) & 1], p.tgid, S.ptrace, K);
-    } else if (!S.found && S.alive >= 2) {
-      lv_solo_write<NQ>(S, true, q.stg[r & 1], q.idx[r & 1], p.tgid, S.wit ? p.tgid + S.tbase : TRACE_NONE, K);
-    }
-    LV_SOLO_T(4);
-    if (R.done != LVR_RUNNING || R.nf != 1) break;
-    // the only survivor (staging slot 0) is the next round's configuration:
-    // reload the heads of the chains it advanced
-    for (uint32_t j = threadIdx.x; j < 64u * NQ; j += LV_BLOCK) {
-      const uint32_t dj = S.keep[j];
-      if (dj) {
-        const uint32_t c = S.cnt[j] + dj;
-        S.cnt[j] = (uint16_t)c;
-        lv_solo_head<NQ>(p, p.recs + s_cs[j] + c, chain_end(j), j, dj == 1, PL, *NX, FR, S);
+    const uint32_t alive = S.c[par].alive, found = S.c[par].found, ovf = S.c[par].ovf;
+    const bool carry = !found && !ovf && alive == 1;  // the only survivor is the next configuration
+    if (carry) {
+      for (uint32_t j = threadIdx.x; j < 64u * NQ; j += LV_BLOCK) {
+        const uint32_t dj = S.keep[j];
+        if (dj) {
+          const uint32_t c = S.cnt[j] + dj;
+          S.cnt[j] = (uint16_t)c;
+          lv_solo_head<NQ>(p, p.recs + s_cs[j] + c, chain_end(j), j, dj == 1, PL, *NX, FR, S);
+        }
       }
     }
     if (threadIdx.x == 0) {
-      S.tail = S.ktail; S.hash = S.khash; S.tok = S.ktok; S.chx = S.kchx; S.pmin = S.kmr;
-      S.ptrace = S.wit ? p.tgid + S.tbase : TRACE_NONE;
+      LvCounts k;
+      k.nn = alive; k.ovf = ovf; k.fnd = found;
+      k.fpar = S.c[par].fpar; k.fmov = S.c[par].fmov; k.fp4 = S.c[par].fp4; k.ch = S.c[par].kids; k.closed = 0;
+      lv_close_state(R, k, r, p.rcounts, p.scap, p.trace_cap);
+      R.solo_rounds++;
+      // the first survivor's trace entry (it was not staged)
+      if (!found && !ovf && alive && in.wit) p.trace[in.tbase] = TraceEnt{S.ptrace, S.kmv};
+      if (carry) {
+        S.tail = S.ktail; S.hash = S.khash; S.tok = S.ktok; S.chx = S.kchx; S.pmin = S.kmr;
+        S.ptrace = in.wit ? p.tgid + in.tbase : TRACE_NONE;
+      }
+      S.tbase = (uint32_t)R.tnext; S.wit = R.witness;
+      S.c[par ^ 1u] = typename LvSolo<NQ>::Ctr{0, 0, 0, 0, 0, 0, 0ull};
     }
+    LV_SOLO_T(4);
     lv_sync_lds();
     LV_SOLO_T(5);
+    if (ovf && !found) {
+      // the host re-runs round r from its frontier: this configuration, in
+      // the staging array the round read its frontier from
+      lv_solo_write<NQ>(S, false, q.stg[(r + 1) & 1], q.idx[(r + 1) & 1], p.tgid, S.ptrace, K);
+    } else if (!found && alive >= 2) {
+      lv_solo_write<NQ>(S, true, q.stg[r & 1], q.idx[r & 1], p.tgid, in.wit ? p.tgid + in.tbase : TRACE_NONE, K);
+    }
+    if (R.done != LVR_RUNNING || R.nf != 1) break;
     if (n + 1 == max_rounds)  // leaving with one configuration: the next round's frontier
       lv_solo_write<NQ>(S, false, q.stg[r & 1], q.idx[r & 1], p.tgid, S.ptrace, K);
   }
@@ -1499,7 +1528,7 @@ __device__ void lv_solo_rounds(const LvParams& p, const LvPersist& q, LvRun& R, 
     atomicAdd(&p.prof[7], (unsigned long long)n_solo);
     atomicAdd(&p.prof[8], wall_clock64() - t_solo);
     for (int i_ = 0; i_ < 6; ++i_) atomicAdd(&p.prof[16 + i_], S.pt[i_]);
-    for (int i_ = 0; i_ < 4; ++i_) atomicAdd(&p.prof[22 + i_], S.pc[i_]);
+    for (int i_ = 0; i_ < 6; ++i_) atomicAdd(&p.prof[22 + i_], S.pc[i_]);
   }
 #endif
 #undef LV_SOLO_T
@@ -1572,6 +1601,7 @@ __global__ __launch_bounds__(LV_BLOCK) void lv_persist(LvParams p, LvPersist q) 
       for (uint32_t i = threadIdx.x; i < sizeof(LvCtl) / 4; i += LV_BLOCK) st_wt32(z + i, 0u);
     }
     LvRoundIn in;
+    in.par = 0;
     in.f0 = 0;
     in.nf = s_run.nf;
     in.S = lv_slices(p.K, in.nf, nwaves, s_run.last_nf, s_run.last_closed);
