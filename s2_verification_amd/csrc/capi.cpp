@@ -672,6 +672,8 @@ int s2lc_batch_stats_get(const s2lc_batch* b, s2lc_batch_stats* out) {
   out->pack8_algo_bytes = b->stats.pack8_algo_bytes;
   out->pack8_histories = b->stats.pack8_histories;
   out->level_persist_fallbacks = b->stats.level.persist_fallbacks;
+  out->level_narrow_ms = b->stats.level.narrow_ms;
+  out->level_wide_ms = b->stats.level.wide_ms;
   return 0;
 }
 

@@ -452,6 +452,8 @@ int level_search(DevBatch& b, uint32_t h, hipStream_t st, const RunOpts& ro, int
             " | closures %llu: %.2f passes and %.2f head loads (lanes) each\n",
             g[24], g[22] / (g[24] ? (double)g[24] : 1.0), g[23] / ns, g[25] / (g[24] ? (double)g[24] : 1.0), g[14],
             g[26] / (g[14] ? (double)g[14] : 1.0), g[27] / (g[14] ? (double)g[14] : 1.0));
+    fprintf(stderr, "[s2lc lvprof] solo precheck per round: P1 min2 %.0f cycles (wave 0), (wave, slot) iterations with a fold %.2f,"
+            " folding lanes %.2f, candidate lanes in the slice %.2f\n", g[31] / ns, g[28] / ns, g[29] / ns, g[30] / ns);
   }
 #endif
   // clear the tables for the next search
@@ -491,6 +493,14 @@ int level_search(DevBatch& b, uint32_t h, hipStream_t st, const RunOpts& ro, int
   }
   LVCHK(hipStreamSynchronize(st));
   ls.ms += ms;
+  {
+    int khz = 100000;  // device wall clock
+    int dev_ = 0;
+    (void)hipGetDevice(&dev_);
+    (void)hipDeviceGetAttribute(&khz, hipDeviceAttributeWallClockRate, dev_);
+    ls.narrow_ms += (double)fin.narrow_ticks / std::max(1, khz);
+    ls.wide_ms += (double)fin.wide_ticks / std::max(1, khz);
+  }
   ls.rounds += R.rounds;
   ls.configs += fin.configs;
   ls.children += fin.children;

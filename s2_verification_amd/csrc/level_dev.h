@@ -109,8 +109,13 @@ struct LvRun {
   unsigned long long last_closed;  // children it closed (slices per configuration)
   uint32_t solo_rounds;    // rounds run as solo rounds (LvSolo)
   uint32_t _pad;
+  // wall-clock ticks of the rounds by their frontier (the configurations they
+  // expand): narrower than LV_WIDE_NF (the rounds the distributed search
+  // replicates) or not (the ones it partitions); t_last = the last close
+  unsigned long long t_last, narrow_ticks, wide_ticks, _pad2;
 };
-static_assert(sizeof(LvRun) == 96, "LvRun layout");
+static_assert(sizeof(LvRun) == 128, "LvRun layout");
+constexpr uint32_t LV_WIDE_NF = 4096;  // (distributed.py's default `wide`)
 
 struct LvParams {
   const OpRec* __restrict__ recs;
@@ -810,6 +815,9 @@ __device__ __forceinline__ bool lv_expand(const LvParams& p, const LvRoundIn& in
     const bool p1 = PRE && (p.hflags & H_NOWRAP);
     uint64_t b_min = REQ_NONE, b_2nd = REQ_NONE;
     if (p1) wave_min2_hot<NQ>(H, b_min, b_2nd);
+#ifdef S2LC_PROF
+    if (SOLO && threadIdx.x == 0) { const unsigned long long t_ = clock64(); sol->pt[6] += t_ - sol->pt[7]; sol->pt[7] = t_; }
+#endif
 #pragma unroll
     for (int q = 0; q < NP; ++q) {
       mv_tail[q] = ps.tail;
@@ -831,6 +839,16 @@ __device__ __forceinline__ bool lv_expand(const LvParams& p, const LvRoundIn& in
         // the fold: for a live opt child, or for an indefinite append's
         // identity test (opt == s needs equal tails)
         const bool fold = (to && !p1dead) || ((r.flags & OPF_CLS_I) && g && opt.tail == ps.tail);
+#ifdef S2LC_PROF
+        if (SOLO && p.prof) {  // [28] (wave, slot) iterations with a fold, [29] folding lanes, [30] candidate lanes
+          const uint64_t fb = __ballot(fold);
+          if (lane == __ffsll((unsigned long long)__ballot(1)) - 1) {
+            if (fb) atomicAdd(&p.prof[28], 1ull);
+            atomicAdd(&p.prof[29], (unsigned long long)__popcll(fb));
+            atomicAdd(&p.prof[30], (unsigned long long)__popcll(__ballot(1)));
+          }
+        }
+#endif
         if (fold) {
           if (SOLO) {  // the first LV_SOLO_HP record hashes are in LDS
             uint64_t h = ps.hash;
@@ -1113,6 +1131,11 @@ __device__ __forceinline__ LvCounts lv_read_counts(LvCtl* c) {
 // the decision (found / empty / budget / overflow / witness off).
 __device__ __forceinline__ void lv_close_state(LvRun& R, const LvCounts& k, uint32_t rnd, uint32_t* rcounts,
                                                uint32_t scap, uint64_t trace_cap) {
+  {
+    const unsigned long long now = wall_clock64();
+    if (rnd > 0) (R.nf >= LV_WIDE_NF ? R.wide_ticks : R.narrow_ticks) += now - R.t_last;
+    R.t_last = now;
+  }
   R.children += k.ch;
   R.last_nf = rnd == 0 ? 0u : R.nf;
   R.last_closed = k.closed;
@@ -1528,6 +1551,7 @@ __device__ void lv_solo_rounds(const LvParams& p, const LvPersist& q, LvRun& R, 
     atomicAdd(&p.prof[7], (unsigned long long)n_solo);
     atomicAdd(&p.prof[8], wall_clock64() - t_solo);
     for (int i_ = 0; i_ < 6; ++i_) atomicAdd(&p.prof[16 + i_], S.pt[i_]);
+    atomicAdd(&p.prof[31], S.pt[6]);
     for (int i_ = 0; i_ < 6; ++i_) atomicAdd(&p.prof[22 + i_], S.pc[i_]);
   }
 #endif
@@ -1652,6 +1676,7 @@ __global__ __attribute__((unused)) void lv_run_init(LvRun* R, unsigned long long
   R->found_parent = TRACE_NONE; R->found_move = LV_NONE; R->found_p4 = 0;
   R->witness = witness; R->deep_trace = TRACE_NONE; R->deep_len = 0; R->last_tbase = TRACE_NONE;
   R->last_nf = 0; R->last_closed = 0; R->solo_rounds = 0;
+  R->t_last = wall_clock64(); R->narrow_ticks = 0; R->wide_ticks = 0;
 }
 
 // ---- distributed: owner of a configuration ---------------------------------
