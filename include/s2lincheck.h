@@ -339,12 +339,14 @@ typedef struct s2lc_batch_stats {
    * resident: another process holding CUs). Not an error: same verdict. */
   uint32_t level_persist_fallbacks;
   uint32_t _pad4;
-  /* level search wall time (host clock, launch to sync) by round width: rounds
+  /* level search time by round width (device wall clock, per round): rounds
    * on frontiers narrower than 4,096 configurations (persistent, solo and
    * host-driven narrow rounds: the part the distributed search replicates on
    * every rank) and wider ones (the part it partitions) */
   double level_narrow_ms;
   double level_wide_ms;
+  double level_solo_ms;      /* of level_narrow_ms: the one-configuration (solo) rounds */
+  double _pad5;
 } s2lc_batch_stats;
 int s2lc_batch_stats_get(const s2lc_batch* b, s2lc_batch_stats* out);
 /* With S2LC_F_ROUND_COUNTS: the unique-configuration count of each completed

@@ -110,7 +110,8 @@ class c_batch_stats(ctypes.Structure):
                 ("n_ops_total", ctypes.c_uint64), ("pack8_ms", ctypes.c_double),
                 ("pack8_algo_bytes", ctypes.c_uint64), ("pack8_histories", ctypes.c_uint32), ("_pad3", ctypes.c_uint32),
                 ("level_persist_fallbacks", ctypes.c_uint32), ("_pad4", ctypes.c_uint32),
-                ("level_narrow_ms", ctypes.c_double), ("level_wide_ms", ctypes.c_double)]
+                ("level_narrow_ms", ctypes.c_double), ("level_wide_ms", ctypes.c_double),
+                ("level_solo_ms", ctypes.c_double), ("_pad5", ctypes.c_double)]
 
 
 class c_sim_params(ctypes.Structure):

@@ -674,6 +674,7 @@ int s2lc_batch_stats_get(const s2lc_batch* b, s2lc_batch_stats* out) {
   out->level_persist_fallbacks = b->stats.level.persist_fallbacks;
   out->level_narrow_ms = b->stats.level.narrow_ms;
   out->level_wide_ms = b->stats.level.wide_ms;
+  out->level_solo_ms = b->stats.level.solo_ms;
   return 0;
 }
 

@@ -446,14 +446,14 @@ int level_search(DevBatch& b, uint32_t h, hipStream_t st, const RunOpts& ro, int
     fprintf(stderr, "[s2lc lvprof] solo rounds %llu: %.2f us/round | closures run %llu, opt children dropped by the P1 "
             "precheck %llu\n", g[7], g[8] * us / (g[7] ? (double)g[7] : 1.0), g[14], g[15]);
     const double ns = g[7] ? (double)g[7] : 1.0;
-    fprintf(stderr, "[s2lc lvprof] solo cycles/round (wave 0): start %.0f setup %.0f pre %.0f moves %.0f wait+reload+close %.0f barrier %.0f\n",
+    fprintf(stderr, "[s2lc lvprof] solo cycles/round (wave 0): start %.0f setup %.0f pre %.0f moves %.0f reload+close %.0f barrier %.0f\n",
             g[16] / ns, g[17] / ns, g[18] / ns, g[19] / ns, g[20] / ns, g[21] / ns);
     fprintf(stderr, "[s2lc lvprof] solo closures: ALIVE %llu at %.0f cycles, others %.0f cycles/round; stage %.0f cycles per ALIVE"
             " | closures %llu: %.2f passes and %.2f head loads (lanes) each\n",
             g[24], g[22] / (g[24] ? (double)g[24] : 1.0), g[23] / ns, g[25] / (g[24] ? (double)g[24] : 1.0), g[14],
             g[26] / (g[14] ? (double)g[14] : 1.0), g[27] / (g[14] ? (double)g[14] : 1.0));
-    fprintf(stderr, "[s2lc lvprof] solo precheck per round: P1 min2 %.0f cycles (wave 0), (wave, slot) iterations with a fold %.2f,"
-            " folding lanes %.2f, candidate lanes in the slice %.2f\n", g[31] / ns, g[28] / ns, g[29] / ns, g[30] / ns);
+    fprintf(stderr, "[s2lc lvprof] solo round: slowest wave's expansion %.0f cycles, wave 0's wait at the first barrier %.0f\n",
+            g[28] / ns, g[31] / ns);
   }
 #endif
   // clear the tables for the next search
@@ -500,6 +500,7 @@ int level_search(DevBatch& b, uint32_t h, hipStream_t st, const RunOpts& ro, int
     (void)hipDeviceGetAttribute(&khz, hipDeviceAttributeWallClockRate, dev_);
     ls.narrow_ms += (double)fin.narrow_ticks / std::max(1, khz);
     ls.wide_ms += (double)fin.wide_ticks / std::max(1, khz);
+    ls.solo_ms += (double)fin.solo_ticks / std::max(1, khz);
   }
   ls.rounds += R.rounds;
   ls.configs += fin.configs;

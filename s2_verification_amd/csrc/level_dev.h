@@ -112,7 +112,7 @@ struct LvRun {
   // wall-clock ticks of the rounds by their frontier (the configurations they
   // expand): narrower than LV_WIDE_NF (the rounds the distributed search
   // replicates) or not (the ones it partitions); t_last = the last close
-  unsigned long long t_last, narrow_ticks, wide_ticks, _pad2;
+  unsigned long long t_last, narrow_ticks, wide_ticks, solo_ticks;  // (solo rounds: part of narrow)
 };
 static_assert(sizeof(LvRun) == 128, "LvRun layout");
 constexpr uint32_t LV_WIDE_NF = 4096;  // (distributed.py's default `wide`)
@@ -198,6 +198,18 @@ __device__ __forceinline__ uint32_t wave_max_u32(uint32_t v) {
   return max(max(rl(v, 0), rl(v, 16)), max(rl(v, 32), rl(v, 48)));
 }
 __device__ __forceinline__ uint64_t lv_min64(uint64_t a, uint64_t b) { return a < b ? a : b; }
+// P1 bounds in 32 bits for H_TAIL32 histories (every reachable tail is below
+// 2^32 - 3): a monotone map, so minima commute with it, and every comparison
+// the search makes against a reachable tail (and P4's "no bound left") gives
+// the same answer: a real requirement at or above 2^32 - 3 -> 0xFFFFFFFD,
+// REQ_HASH_ONLY -> 0xFFFFFFFE, REQ_NONE -> 0xFFFFFFFF (as pack_closure).
+__device__ __forceinline__ uint32_t suf32(uint64_t v) {
+  const uint32_t lo = (uint32_t)v, hi = (uint32_t)(v >> 32);
+  return hi == 0 ? min(lo, 0xFFFFFFFDu) : (hi == 0xFFFFFFFFu && lo >= 0xFFFFFFFEu) ? lo : 0xFFFFFFFDu;
+}
+__device__ __forceinline__ uint64_t suf64_of32(uint32_t b) {
+  return b == 0xFFFFFFFFu ? REQ_NONE : b == 0xFFFFFFFEu ? REQ_HASH_ONLY : (uint64_t)b;
+}
 template <int CTRL>
 __device__ __forceinline__ uint64_t lv_dpp64(uint64_t v) {
   return ((uint64_t)lv_dpp<CTRL>((uint32_t)(v >> 32)) << 32) | lv_dpp<CTRL>((uint32_t)v);
@@ -342,17 +354,20 @@ __device__ __forceinline__ int lv_closure(LvHot (&H)[NQ], uint32_t (&d)[NQ], con
   const bool nowrap = hflags & H_NOWRAP;
   const bool p2 = hflags & H_P2OK;
   const bool p4 = hflags & H_P4;
+  const bool t32 = hflags & H_TAIL32;  // the P1 bound reduces in 32 bits (suf32)
   uint32_t minret_prev = minret_seed;
   for (;;) {
     uint32_t mr = EV_INF;
     uint64_t bd = REQ_NONE;
+    uint32_t bd32 = 0xFFFFFFFFu;
     uint32_t adv = 0;
     bool dead = false;
 #pragma unroll
     for (int q = 0; q < NQ; ++q) {
       const LvHot& h = H[q];
       mr = min(mr, h.ret);
-      bd = lv_min64(bd, h.suf);
+      if (t32) bd32 = min(bd32, suf32(h.suf));
+      else bd = lv_min64(bd, h.suf);
       if (!(h.fl & OPF_CLS_E) || h.call >= minret_prev) continue;
       uint32_t bits = h.fl;
       if (!(bits & HB_KNOWN)) bits = lv_legal_bits(h.fl, PL.otail[q][lane], PL.ohash[q][lane], s);
@@ -360,7 +375,7 @@ __device__ __forceinline__ int lv_closure(LvHot (&H)[NQ], uint32_t (&d)[NQ], con
       else if (p2 && (bits & HB_P2DEAD)) dead = true;
     }
     const uint32_t minret = wave_min_u32(mr);
-    const uint64_t bound = wave_min_u64(bd);
+    const uint64_t bound = t32 ? suf64_of32(wave_min_u32(bd32)) : wave_min_u64(bd);
 #ifdef S2LC_PROF
     if (prof && lane == 0) atomicAdd(prof, 1ull);  // passes
 #else
@@ -620,7 +635,27 @@ __device__ __forceinline__ void lv_stage_insert(const LvParams& p, const LvRound
 // would drain those too). Solo rounds share only LDS between their waves.
 __device__ __forceinline__ void lv_sync_lds() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); }
 
-constexpr int LV_SOLO_HP = 4;  // record hashes of each head kept in LDS
+constexpr int LV_SOLO_HP = 4;  // record hashes of each head kept in LvSolo
+constexpr int LV_SOLO_HP2 = 4; // the next ones, in LvSoloExt (8 in LDS: 91 % of C5's appends)
+
+// Solo rounds' per-head data kept beside PL / NX in the space the grid rounds
+// use for waves 2 and 3 (s_heads[2..3]): the move's fields PL does not hold
+// (32 bytes per chain, not the whole 64-byte record) and record hashes
+// LV_SOLO_HP .. LV_SOLO_HP + LV_SOLO_HP2 - 1 of each head, so that a move
+// whose append carries up to 8 record hashes folds them from LDS (round 2:
+// 4 in LDS, the rest loaded on the round's critical path for 60 % of C5's
+// appends).
+struct LvMoveRec {
+  uint64_t num_records, msn;
+  uint32_t hash_off, hash_cnt;
+  uint32_t toks;  // batch_tok | set_tok << 16 (OpRec bytes 56..59)
+  uint32_t _pad;
+};
+template <int NQ>
+struct LvSoloExt {
+  LvMoveRec mr[64 * NQ];
+  uint64_t hp2[LV_SOLO_HP2][64 * NQ];
+};
 template <int NQ>
 struct LvSolo {
   uint64_t hp[LV_SOLO_HP][64 * NQ];  // the heads' first record hashes
@@ -641,6 +676,7 @@ struct LvSolo {
 #ifdef S2LC_PROF
   unsigned long long pt[8];  // wave 0 phase cycles: [0] start [1] setup [2] pre [3] moves [4] close [5] next; [7] last stamp
   unsigned long long pc[6];  // closure cycles (ALIVE, other), ALIVE closures, stage cycles (all waves), closure passes, closure head loads
+  unsigned long long pw[2];  // [0] sum over rounds of the slowest wave's expansion cycles, [1] this round's max
 #endif
 };
 
@@ -671,6 +707,35 @@ __device__ __forceinline__ void wave_min2_hot(const LvHot (&H)[NQ], uint64_t& m1
     const uint64_t ra = rl64(a, 16 * row), rb = rl64(b, 16 * row);
     const uint64_t lo = lv_min64(m1, ra), hi = m1 < ra ? ra : m1;
     m2 = lv_min64(hi, lv_min64(m2, rb));
+    m1 = lo;
+  }
+}
+
+template <int CTRL>
+__device__ __forceinline__ void lv_min2_step32(uint32_t& a, uint32_t& b) {
+  const uint32_t oa = lv_dpp<CTRL>(a), ob = lv_dpp<CTRL>(b);
+  const uint32_t lo = min(a, oa), hi = max(a, oa);
+  b = min(hi, min(b, ob));
+  a = lo;
+}
+template <int NQ>
+__device__ __forceinline__ void wave_min2_hot32(const LvHot (&H)[NQ], uint32_t& m1, uint32_t& m2) {
+  uint32_t a = 0xFFFFFFFFu, b = 0xFFFFFFFFu;
+#pragma unroll
+  for (int q = 0; q < NQ; ++q) {
+    const uint32_t v = suf32(H[q].suf);
+    if (v < a) { b = a; a = v; } else if (v < b) { b = v; }
+  }
+  lv_min2_step32<0xB1>(a, b);
+  lv_min2_step32<0x4E>(a, b);
+  lv_min2_step32<0x124>(a, b);
+  lv_min2_step32<0x128>(a, b);
+  m1 = 0xFFFFFFFFu; m2 = 0xFFFFFFFFu;
+#pragma unroll
+  for (int row = 0; row < 4; ++row) {
+    const uint32_t ra = rl(a, 16 * row), rb = rl(b, 16 * row);
+    const uint32_t lo = min(m1, ra), hi = max(m1, ra);
+    m2 = min(hi, min(m2, rb));
     m1 = lo;
   }
 }
@@ -712,7 +777,7 @@ __device__ __forceinline__ uint64_t ld_suf(const OpRec* r) {
 template <int NQ, int MODE>
 __device__ __forceinline__ bool lv_expand(const LvParams& p, const LvRoundIn& in, LvHeadsLds<NQ>& PL,
                                           const uint32_t* s_cs, LvSolo<NQ>* sol = nullptr,
-                                          LvHeadsLds<NQ>* NX = nullptr, const OpRec* FR = nullptr) {
+                                          LvHeadsLds<NQ>* NX = nullptr, const LvSoloExt<NQ>* FR = nullptr) {
   constexpr bool FUSED = MODE == 1, SOLO = MODE == 2;
   const int lane = (int)(threadIdx.x & 63);
   const uint32_t K = p.K;
@@ -813,11 +878,14 @@ __device__ __forceinline__ bool lv_expand(const LvParams& p, const LvRoundIn& in
     // opt child past it dies in its closure's first pass, and is counted but
     // not closed (most children of a hard history end this way)
     const bool p1 = PRE && (p.hflags & H_NOWRAP);
+    const bool t32 = p.hflags & H_TAIL32;
     uint64_t b_min = REQ_NONE, b_2nd = REQ_NONE;
-    if (p1) wave_min2_hot<NQ>(H, b_min, b_2nd);
-#ifdef S2LC_PROF
-    if (SOLO && threadIdx.x == 0) { const unsigned long long t_ = clock64(); sol->pt[6] += t_ - sol->pt[7]; sol->pt[7] = t_; }
-#endif
+    uint32_t b_min32 = 0xFFFFFFFFu, b_2nd32 = 0xFFFFFFFFu;
+    if (p1) {
+      if (t32) wave_min2_hot32<NQ>(H, b_min32, b_2nd32);
+      else wave_min2_hot<NQ>(H, b_min, b_2nd);
+    }
+
 #pragma unroll
     for (int q = 0; q < NP; ++q) {
       mv_tail[q] = ps.tail;
@@ -829,26 +897,29 @@ __device__ __forceinline__ bool lv_expand(const LvParams& p, const LvRoundIn& in
         const uint64_t nx_suf = SOLO ? NX->suf[q][lane] : (p1 ? ld_suf(hp + 1) : REQ_NONE);
         // the head: solo rounds keep the heads' whole records in LDS; grid
         // rounds just loaded its hot part (cached)
-        const OpRec r = SOLO ? FR[64 * q + lane] : load_rec(hp);
+        OpRec r;
+        if (SOLO) {  // PL's fields + the move fields of LvSoloExt
+          const LvMoveRec& m_ = FR->mr[64 * q + lane];
+          r.num_records = m_.num_records; r.msn = m_.msn;
+          r.out_tail = PL.otail[q][lane]; r.out_hash = PL.ohash[q][lane]; r.sufmin = PL.suf[q][lane];
+          r.call_ev = PL.call[q][lane]; r.ret_ev = PL.ret[q][lane];
+          r.hash_off = m_.hash_off; r.hash_cnt = m_.hash_cnt;
+          r.batch_tok = (uint16_t)m_.toks; r.set_tok = (uint16_t)(m_.toks >> 16);
+          r.flags = PL.fl[q][lane];
+        } else {
+          r = load_rec(hp);
+        }
         const bool g = append_guards_ok(r, ps);
         State opt = ps;
         opt.tail = ps.tail + r.num_records;
         opt.tok = r.set_tok ? r.set_tok : ps.tok;
         bool to = (r.flags & OPF_CLS_D) ? (g && opt.tail == r.out_tail) : g;
-        const bool p1dead = p1 && to && opt.tail > lv_min64(H[q].suf == b_min ? b_2nd : b_min, nx_suf);
+        const uint64_t others = t32 ? suf64_of32(suf32(H[q].suf) == b_min32 ? b_2nd32 : b_min32)
+                                    : (H[q].suf == b_min ? b_2nd : b_min);
+        const bool p1dead = p1 && to && opt.tail > lv_min64(others, nx_suf);
         // the fold: for a live opt child, or for an indefinite append's
         // identity test (opt == s needs equal tails)
         const bool fold = (to && !p1dead) || ((r.flags & OPF_CLS_I) && g && opt.tail == ps.tail);
-#ifdef S2LC_PROF
-        if (SOLO && p.prof) {  // [28] (wave, slot) iterations with a fold, [29] folding lanes, [30] candidate lanes
-          const uint64_t fb = __ballot(fold);
-          if (lane == __ffsll((unsigned long long)__ballot(1)) - 1) {
-            if (fb) atomicAdd(&p.prof[28], 1ull);
-            atomicAdd(&p.prof[29], (unsigned long long)__popcll(fb));
-            atomicAdd(&p.prof[30], (unsigned long long)__popcll(__ballot(1)));
-          }
-        }
-#endif
         if (fold) {
           if (SOLO) {  // the first LV_SOLO_HP record hashes are in LDS
             uint64_t h = ps.hash;
@@ -856,8 +927,12 @@ __device__ __forceinline__ bool lv_expand(const LvParams& p, const LvRoundIn& in
 #pragma unroll
             for (int k = 0; k < LV_SOLO_HP; ++k)
               if ((uint32_t)k < r.hash_cnt) h = chain_hash(h, sol->hp[k][j]);
-            if (r.hash_cnt > (uint32_t)LV_SOLO_HP)
-              h = fold_hashes_blk(h, p.pool + r.hash_off + LV_SOLO_HP, r.hash_cnt - LV_SOLO_HP);
+#pragma unroll
+            for (int k = 0; k < LV_SOLO_HP2; ++k)
+              if ((uint32_t)(LV_SOLO_HP + k) < r.hash_cnt) h = chain_hash(h, FR->hp2[k][j]);
+            if (r.hash_cnt > (uint32_t)(LV_SOLO_HP + LV_SOLO_HP2))
+              h = fold_hashes_blk(h, p.pool + r.hash_off + LV_SOLO_HP + LV_SOLO_HP2,
+                                  r.hash_cnt - LV_SOLO_HP - LV_SOLO_HP2);
             opt.hash = h;
           } else {
             opt.hash = fold_hashes_blk(ps.hash, p.pool + r.hash_off, r.hash_cnt);
@@ -1361,23 +1436,28 @@ __device__ __forceinline__ bool lv_grid_sync(LvBar* B, uint32_t e, unsigned long
 // the hash loads go out with the record loads instead of after them.
 template <int NQ>
 __device__ __forceinline__ void lv_solo_head(const LvParams& p, const OpRec* h, const OpRec* end, uint32_t j,
-                                             bool known, LvHeadsLds<NQ>& PL, LvHeadsLds<NQ>& NX, OpRec* FR,
+                                             bool known, LvHeadsLds<NQ>& PL, LvHeadsLds<NQ>& NX, LvSoloExt<NQ>* FR,
                                              LvSolo<NQ>& S) {
+  constexpr int HP = LV_SOLO_HP + LV_SOLO_HP2;
   const uint4* a = reinterpret_cast<const uint4*>(h);
   const uint4* b = reinterpret_cast<const uint4*>(h + 1 < end ? h + 1 : h);  // (the sentinel has no next record)
   const uint4 x0 = a[0], x1 = a[1], x2 = a[2], x3 = a[3];
   const uint4 y1 = b[1], y2 = b[2], y3 = b[3];
-  uint64_t hv[LV_SOLO_HP];
+  uint64_t hv[HP];
   if (known) {
     const uint32_t ho = S.nx_hoff[j], hc = S.nx_hcnt[j];
 #pragma unroll
-    for (int k = 0; k < LV_SOLO_HP; ++k) hv[k] = (uint32_t)k < hc ? p.pool[ho + k] : 0ull;
+    for (int k = 0; k < HP; ++k) hv[k] = (uint32_t)k < hc ? p.pool[ho + k] : 0ull;
   } else {
 #pragma unroll
-    for (int k = 0; k < LV_SOLO_HP; ++k) hv[k] = (uint32_t)k < x3.y ? p.pool[x3.x + k] : 0ull;
+    for (int k = 0; k < HP; ++k) hv[k] = (uint32_t)k < x3.y ? p.pool[x3.x + k] : 0ull;
   }
-  uint4* f = reinterpret_cast<uint4*>(FR + j);
-  f[0] = x0; f[1] = x1; f[2] = x2; f[3] = x3;
+  LvMoveRec& m = FR->mr[j];
+  m.num_records = (uint64_t)x0.x | ((uint64_t)x0.y << 32);
+  m.msn = (uint64_t)x0.z | ((uint64_t)x0.w << 32);
+  m.hash_off = x3.x;
+  m.hash_cnt = x3.y;
+  m.toks = x3.z;
   const int q = (int)(j >> 6), l = (int)(j & 63);
   PL.otail[q][l] = (uint64_t)x1.x | ((uint64_t)x1.y << 32);
   PL.ohash[q][l] = (uint64_t)x1.z | ((uint64_t)x1.w << 32);
@@ -1395,6 +1475,8 @@ __device__ __forceinline__ void lv_solo_head(const LvParams& p, const OpRec* h, 
   S.nx_hcnt[j] = y3.y;
 #pragma unroll
   for (int k = 0; k < LV_SOLO_HP; ++k) S.hp[k][j] = hv[k];
+#pragma unroll
+  for (int k = 0; k < LV_SOLO_HP2; ++k) FR->hp2[k][j] = hv[LV_SOLO_HP + k];
 }
 
 // The whole workgroup writes a solo configuration held in LDS (counts
@@ -1432,7 +1514,7 @@ __device__ void lv_solo_write(const LvSolo<NQ>& S, bool child, uint8_t* stg, uin
 // state; every round is closed on it exactly as a grid round is.
 template <int NQ>
 __device__ void lv_solo_rounds(const LvParams& p, const LvPersist& q, LvRun& R, LvHeadsLds<NQ>& PL,
-                               LvHeadsLds<NQ>* NX, OpRec* FR, const uint32_t* s_cs, LvSolo<NQ>& S,
+                               LvHeadsLds<NQ>* NX, LvSoloExt<NQ>* FR, const uint32_t* s_cs, LvSolo<NQ>& S,
                                uint32_t max_rounds) {
   const uint32_t K = p.K;
   // end of chain j's records (its sentinel's index + 1)
@@ -1475,7 +1557,7 @@ __device__ void lv_solo_rounds(const LvParams& p, const LvPersist& q, LvRun& R, 
   uint32_t n_solo = 0;
 #endif
 #ifdef S2LC_PROF
-  if (threadIdx.x == 0) { for (int i_ = 0; i_ < 8; ++i_) S.pt[i_] = 0; for (int i_ = 0; i_ < 6; ++i_) S.pc[i_] = 0; S.pt[7] = clock64(); }
+  if (threadIdx.x == 0) { for (int i_ = 0; i_ < 8; ++i_) S.pt[i_] = 0; for (int i_ = 0; i_ < 6; ++i_) S.pc[i_] = 0; S.pw[0] = S.pw[1] = 0; S.pt[7] = clock64(); }
 #define LV_SOLO_T(i) do { if (threadIdx.x == 0) { const unsigned long long t_ = clock64(); S.pt[i] += t_ - S.pt[7]; S.pt[7] = t_; } } while (0)
 #else
 #define LV_SOLO_T(i) do { } while (0)
@@ -1502,9 +1584,16 @@ __device__ void lv_solo_rounds(const LvParams& p, const LvPersist& q, LvRun& R, 
     LvRoundIn in;
     in.f0 = 0; in.nf = 1; in.par = par; in.S = LV_BLOCK / 64; in.tbase = S.tbase; in.wit = S.wit;
     LV_SOLO_T(0);
+#ifdef S2LC_PROF
+    const unsigned long long tw0_ = clock64();
+#endif
     (void)lv_expand<NQ, 2>(rp, in, PL, s_cs, &S, NX, FR);
+#ifdef S2LC_PROF
+    if ((threadIdx.x & 63) == 0) atomicMax(&S.pw[1], clock64() - tw0_);
+#endif
     LV_SOLO_T(3);
     lv_sync_lds();
+    LV_SOLO_T(6);
     const uint32_t alive = S.c[par].alive, found = S.c[par].found, ovf = S.c[par].ovf;
     const bool carry = !found && !ovf && alive == 1;  // the only survivor is the next configuration
     if (carry) {
@@ -1521,8 +1610,10 @@ __device__ void lv_solo_rounds(const LvParams& p, const LvPersist& q, LvRun& R, 
       LvCounts k;
       k.nn = alive; k.ovf = ovf; k.fnd = found;
       k.fpar = S.c[par].fpar; k.fmov = S.c[par].fmov; k.fp4 = S.c[par].fp4; k.ch = S.c[par].kids; k.closed = 0;
+      const unsigned long long t_prev = R.t_last;
       lv_close_state(R, k, r, p.rcounts, p.scap, p.trace_cap);
       R.solo_rounds++;
+      R.solo_ticks += R.t_last - t_prev;
       // the first survivor's trace entry (it was not staged)
       if (!found && !ovf && alive && in.wit) p.trace[in.tbase] = TraceEnt{S.ptrace, S.kmv};
       if (carry) {
@@ -1531,6 +1622,10 @@ __device__ void lv_solo_rounds(const LvParams& p, const LvPersist& q, LvRun& R, 
       }
       S.tbase = (uint32_t)R.tnext; S.wit = R.witness;
       S.c[par ^ 1u] = typename LvSolo<NQ>::Ctr{0, 0, 0, 0, 0, 0, 0ull};
+#ifdef S2LC_PROF
+      S.pw[0] += S.pw[1];
+      S.pw[1] = 0;
+#endif
     }
     LV_SOLO_T(4);
     lv_sync_lds();
@@ -1552,6 +1647,7 @@ __device__ void lv_solo_rounds(const LvParams& p, const LvPersist& q, LvRun& R, 
     atomicAdd(&p.prof[8], wall_clock64() - t_solo);
     for (int i_ = 0; i_ < 6; ++i_) atomicAdd(&p.prof[16 + i_], S.pt[i_]);
     atomicAdd(&p.prof[31], S.pt[6]);
+    atomicAdd(&p.prof[28], S.pw[0]);
     for (int i_ = 0; i_ < 6; ++i_) atomicAdd(&p.prof[22 + i_], S.pc[i_]);
   }
 #endif
@@ -1561,9 +1657,9 @@ __device__ void lv_solo_rounds(const LvParams& p, const LvPersist& q, LvRun& R, 
 template <int NQ>
 __global__ __launch_bounds__(LV_BLOCK) void lv_persist(LvParams p, LvPersist q) {
   // solo rounds use s_heads[0] (the configuration's heads), s_heads[1] (the
-  // moves' next heads) and s_heads[2..3] as the heads' whole records
+  // moves' next heads) and s_heads[2..3] as the move records (LvSoloExt)
   __shared__ __attribute__((aligned(16))) LvHeadsLds<NQ> s_heads[LV_BLOCK / 64];
-  static_assert(2 * sizeof(LvHeadsLds<NQ>) >= 64 * NQ * sizeof(OpRec), "solo head records fit in s_heads[2..3]");
+  static_assert(2 * sizeof(LvHeadsLds<NQ>) >= sizeof(LvSoloExt<NQ>), "solo move records fit in s_heads[2..3]");
   __shared__ uint32_t s_cs[64 * NQ];
   __shared__ LvRun s_run;
   __shared__ LvSolo<(NQ <= 5 ? NQ : 1)> s_solo;  // (solo rounds only for NQ <= 5)
@@ -1587,7 +1683,7 @@ __global__ __launch_bounds__(LV_BLOCK) void lv_persist(LvParams p, LvPersist q) 
     if (NQ <= 5 && q.solo && s_run.nf == 1) {
       if (blockIdx.x == 0) {
         if constexpr (NQ <= 5) lv_solo_rounds<NQ>(p, q, s_run, s_heads[0], &s_heads[1],
-                                                   reinterpret_cast<OpRec*>(&s_heads[2]), s_cs, s_solo, max(1u, q.max_rounds - it));
+                                                   reinterpret_cast<LvSoloExt<(NQ <= 5 ? NQ : 1)>*>(&s_heads[2]), s_cs, s_solo, max(1u, q.max_rounds - it));
         // the next grid round's counters start at zero: the slot after
         // r_before's, never r_before's own (a workgroup that left round
         // r_before's barrier late may still be reading it: ADVICE r2); the
@@ -1676,7 +1772,7 @@ __global__ __attribute__((unused)) void lv_run_init(LvRun* R, unsigned long long
   R->found_parent = TRACE_NONE; R->found_move = LV_NONE; R->found_p4 = 0;
   R->witness = witness; R->deep_trace = TRACE_NONE; R->deep_len = 0; R->last_tbase = TRACE_NONE;
   R->last_nf = 0; R->last_closed = 0; R->solo_rounds = 0;
-  R->t_last = wall_clock64(); R->narrow_ticks = 0; R->wide_ticks = 0;
+  R->t_last = wall_clock64(); R->narrow_ticks = 0; R->wide_ticks = 0; R->solo_ticks = 0;
 }
 
 // ---- distributed: owner of a configuration ---------------------------------

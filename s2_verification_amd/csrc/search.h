@@ -87,7 +87,8 @@ struct LevelStats {
   uint64_t persist_rounds = 0, persist_launches = 0;  // rounds run inside lv_persist
   uint64_t solo_rounds = 0;  // of those, one-configuration rounds run by one workgroup
   uint32_t persist_fallbacks = 0;  // searches restarted host-driven (persistent launch refused / timed out)
-  double narrow_ms = 0, wide_ms = 0;  // host wall time of rounds on frontiers < 4096 / >= 4096
+  double narrow_ms = 0, wide_ms = 0;  // device wall time of rounds on frontiers < 4096 / >= 4096
+  double solo_ms = 0;                 // of narrow: the solo rounds
 };
 
 // A batch of histories resident on one device. Every buffer is grown on

@@ -23,7 +23,8 @@ for name in sys.argv[1:]:
     print(json.dumps({"name": name, "verdict": r.verdict, "reason": r.reason, "cold_s": round(cold, 3),
                       "warm_s": round(warm, 4), "witness": r.witness is not None,
                       **{k: st[k] for k in ("kernel_ms", "level_ms", "level_rounds", "level_configs", "level_children",
-                                            "level_max_frontier")}}), flush=True)
+                                            "level_max_frontier", "level_narrow_ms", "level_wide_ms", "level_solo_ms",
+                                            "level_solo_rounds")}}), flush=True)
 
 # release the batches and the context while the HIP runtime is fully up
 del b, ck
