@@ -346,7 +346,8 @@ typedef struct s2lc_batch_stats {
   double level_narrow_ms;
   double level_wide_ms;
   double level_solo_ms;      /* of level_narrow_ms: the one-configuration (solo) rounds */
-  double _pad5;
+  uint32_t level_grows;      /* staging capacity raised after an overflowing round (starts at 2 GiB) */
+  uint32_t _pad5;
 } s2lc_batch_stats;
 int s2lc_batch_stats_get(const s2lc_batch* b, s2lc_batch_stats* out);
 /* With S2LC_F_ROUND_COUNTS: the unique-configuration count of each completed

@@ -111,7 +111,7 @@ class c_batch_stats(ctypes.Structure):
                 ("pack8_algo_bytes", ctypes.c_uint64), ("pack8_histories", ctypes.c_uint32), ("_pad3", ctypes.c_uint32),
                 ("level_persist_fallbacks", ctypes.c_uint32), ("_pad4", ctypes.c_uint32),
                 ("level_narrow_ms", ctypes.c_double), ("level_wide_ms", ctypes.c_double),
-                ("level_solo_ms", ctypes.c_double), ("_pad5", ctypes.c_double)]
+                ("level_solo_ms", ctypes.c_double), ("level_grows", ctypes.c_uint32), ("_pad5", ctypes.c_uint32)]
 
 
 class c_sim_params(ctypes.Structure):

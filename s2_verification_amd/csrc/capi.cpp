@@ -675,6 +675,7 @@ int s2lc_batch_stats_get(const s2lc_batch* b, s2lc_batch_stats* out) {
   out->level_narrow_ms = b->stats.level.narrow_ms;
   out->level_wide_ms = b->stats.level.wide_ms;
   out->level_solo_ms = b->stats.level.solo_ms;
+  out->level_grows = b->stats.level.grows;
   return 0;
 }
 

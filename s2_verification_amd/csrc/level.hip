@@ -162,32 +162,50 @@ int lv_grids(LevelBufs& L, uint32_t nq, std::string& err) {
 
 uint32_t level_nq(uint32_t K) { return std::max<uint32_t>(1, std::min<uint32_t>(8, (K + 63) / 64)); }
 
-int level_buffers(DevBatch& b, uint32_t nq, std::string& err) {
-  LevelBufs& L = b.lv;
-  if (L.nq >= nq && L.ctl) return 0;
-  size_t free_b = 0, total_b = 0;
-  LVCHK(hipMemGetInfo(&free_b, &total_b));
-  // a quarter of free HBM (at most 48 GiB): two staging arrays, their index
-  // lists and the table (2 slots per staged configuration)
-  const size_t budget = std::min<size_t>(free_b / 4, 48ull << 30);
-  const size_t cb = lv_cfg_bytes(8);  // sized for the widest layout: reused by every history
+// Staging capacity for `budget` bytes: two staging arrays and their index
+// lists plus two tables of 2 slots per staged configuration (cb: the widest
+// layout, so one allocation serves every history).
+static uint64_t lv_scap_for(size_t budget, size_t cb) {
   uint64_t scap = std::min<uint64_t>(1ull << 25, (uint64_t)budget / (2 * cb + 2 * 4 + 2 * 2 * 8));
   scap = std::max<uint64_t>(scap, 64 * LV_STRIPES);
-  // S2LC_LEVEL_SCAP (tests): a small staging capacity, to reach the
-  // frontier-overflow paths with small histories
-  if (const char* e = getenv("S2LC_LEVEL_SCAP")) {
+  if (const char* e = getenv("S2LC_LEVEL_SCAP")) {  // (tests) a small staging capacity: the overflow paths
     const uint64_t v = strtoull(e, nullptr, 10);
     if (v >= LV_STRIPES) scap = std::min<uint64_t>(scap, v);
   }
-  scap -= scap % LV_STRIPES;  // whole stripes
+  return scap - scap % LV_STRIPES;  // whole stripes
+}
+
+static int lv_tables(LevelBufs& L, uint64_t scap, std::string& err) {
   uint64_t ht = 1024;
   while (ht < 2 * scap) ht <<= 1;
+  for (int i = 0; i < 2; ++i)
+    if (lv_ensure((void**)&L.ht[i], L.ht_bytes[i], ht * 8, err)) return S2LC_EHIP;
+  for (int i = 0; i < 2; ++i) LVCHK(hipMemset(L.ht[i], 0xFF, ht * 8));
+  L.ht_mask = (uint32_t)(ht - 1);
+  return 0;
+}
+
+// The buffers start at 2 GiB (S2LC_LEVEL_BUDGET_MB overrides) and grow on a
+// staging overflow (level_grow) up to the full budget: the first kernel
+// after an allocation commits it, ~54 ms per GB on the MI355X box
+// (tools/startup/big_alloc.cpp: 2.7 s for 50 GB), which a history that never
+// needs the capacity should not pay.
+int level_buffers(DevBatch& b, uint32_t nq, std::string& err, bool full) {
+  LevelBufs& L = b.lv;
+  (void)nq;
+  if (L.ctl && (!full || L.scap >= L.scap_max)) return 0;
+  size_t free_b = 0, total_b = 0;
+  LVCHK(hipMemGetInfo(&free_b, &total_b));
+  const size_t cb = lv_cfg_bytes(8);  // sized for the widest layout: reused by every history
+  if (!L.scap_max) L.scap_max = (uint32_t)lv_scap_for(std::min<size_t>(free_b / 4, 48ull << 30), cb);
+  size_t first = 2ull << 30;
+  if (const char* e = getenv("S2LC_LEVEL_BUDGET_MB")) first = (size_t)strtoull(e, nullptr, 10) << 20;
+  const uint64_t scap = full ? L.scap_max : std::min<uint64_t>(L.scap_max, lv_scap_for(first, cb));
   for (int i = 0; i < 2; ++i) {
     if (lv_ensure((void**)&L.stg[i], L.stg_bytes[i], scap * cb, err)) return S2LC_EHIP;
     if (lv_ensure((void**)&L.idx[i], L.idx_bytes[i], scap * sizeof(uint32_t), err)) return S2LC_EHIP;
   }
-  for (int i = 0; i < 2; ++i)
-    if (lv_ensure((void**)&L.ht[i], L.ht_bytes[i], ht * 8, err)) return S2LC_EHIP;
+  if (lv_tables(L, scap, err)) return S2LC_EHIP;
   if (!L.ctl) LVCHK(hipMalloc(&L.ctl, 3 * sizeof(LvCtl)));
   if (!L.bar) LVCHK(hipMalloc(&L.bar, sizeof(LvBar)));
   if (!L.run) LVCHK(hipMalloc(&L.run, sizeof(LvRun)));
@@ -195,10 +213,37 @@ int level_buffers(DevBatch& b, uint32_t nq, std::string& err) {
   if (!L.h_ctl) LVCHK(hipHostMalloc(&L.h_ctl, sizeof(LvCtl), hipHostMallocDefault));
   for (hipEvent_t& e : L.ev)
     if (!e) LVCHK(hipEventCreate(&e));
-  for (int i = 0; i < 2; ++i) LVCHK(hipMemset(L.ht[i], 0xFF, ht * 8));
   L.nq = 8;
   L.scap = (uint32_t)scap;
-  L.ht_mask = (uint32_t)(ht - 1);
+  return 0;
+}
+
+// Raise the staging capacity (x8, up to the budget), keeping staging array
+// `keep` and its index list (the frontier of the round to re-run); the tables
+// are new and empty. Returns 1 when the capacity is already at the budget.
+int level_grow(DevBatch& b, int keep, hipStream_t st, std::string& err) {
+  LevelBufs& L = b.lv;
+  if (L.scap >= L.scap_max) return 1;
+  const size_t cb = lv_cfg_bytes(8);
+  uint64_t scap = std::min<uint64_t>(L.scap_max, (uint64_t)L.scap * 8);
+  scap -= scap % LV_STRIPES;
+  LVCHK(hipStreamSynchronize(st));
+  for (int i = 0; i < 2; ++i) {
+    uint8_t* ns = nullptr;
+    uint32_t* ni = nullptr;
+    LVCHK(hipMalloc(&ns, scap * cb));
+    LVCHK(hipMalloc(&ni, scap * sizeof(uint32_t)));
+    if (i == keep) {
+      LVCHK(hipMemcpy(ns, L.stg[i], (size_t)L.scap * cb, hipMemcpyDeviceToDevice));
+      LVCHK(hipMemcpy(ni, L.idx[i], (size_t)L.scap * sizeof(uint32_t), hipMemcpyDeviceToDevice));
+    }
+    (void)hipFree(L.stg[i]);
+    (void)hipFree(L.idx[i]);
+    L.stg[i] = ns; L.stg_bytes[i] = scap * cb;
+    L.idx[i] = ni; L.idx_bytes[i] = scap * sizeof(uint32_t);
+  }
+  if (lv_tables(L, scap, err)) return S2LC_EHIP;
+  L.scap = (uint32_t)scap;
   return 0;
 }
 
@@ -217,7 +262,7 @@ int level_search(DevBatch& b, uint32_t h, hipStream_t st, const RunOpts& ro, int
   const HistDesc& hd = b.h_hist[h];
   const uint32_t K = hd.K;
   const uint32_t nq = level_nq(K);
-  if (level_buffers(b, nq, err)) return S2LC_EHIP;
+  if (level_buffers(b, nq, err, false)) return S2LC_EHIP;
   LevelBufs& L = b.lv;
   if (lv_grids(L, nq, err)) return S2LC_EHIP;
   LvRun* hr = reinterpret_cast<LvRun*>(L.h_run);
@@ -225,7 +270,7 @@ int level_search(DevBatch& b, uint32_t h, hipStream_t st, const RunOpts& ro, int
   LVCHK(hipHostGetDevicePointer((void**)&d_pub, hr, 0));
   LvRun* const run = reinterpret_cast<LvRun*>(L.run);
   LvCtl* const ctl = reinterpret_cast<LvCtl*>(L.ctl);
-  const size_t ht_bytes = ((size_t)L.ht_mask + 1) * 8;
+  size_t ht_bytes = ((size_t)L.ht_mask + 1) * 8;  // (grows with the staging capacity)
 
   // trace entries continue after what earlier passes / histories used
   unsigned long long tb0 = 0;
@@ -361,10 +406,22 @@ int level_search(DevBatch& b, uint32_t h, hipStream_t st, const RunOpts& ro, int
       }
       if (hr->done == LVR_OVERFLOW) {
         // round r overflowed the staging array: its frontier (stg[(r+1)&1]) is
-        // intact; re-run it host-driven over halves of the frontier, into a
-        // clean table (an aborted persistent round left entries behind)
+        // intact; raise the capacity if the budget allows, then re-run the
+        // round host-driven, over halves of the frontier while it still does
+        // not fit, into a clean table (an aborted persistent round left
+        // entries behind)
         const uint32_t r = hr->round + 1;
         const uint32_t nf = hr->nf;
+        {
+          const int g = level_grow(b, (int)((r + 1) & 1), st, err);
+          if (g < 0) return g;
+          if (g == 0) {
+            ++ls.grows;
+            p.scap = L.scap; p.scs = L.scap / LV_STRIPES; p.ht_mask = L.ht_mask;
+            for (int i = 0; i < 2; ++i) { pq.stg[i] = L.stg[i]; pq.idx[i] = L.idx[i]; pq.ht[i] = L.ht[i]; }
+            ht_bytes = ((size_t)L.ht_mask + 1) * 8;
+          }
+        }
         LvRun cont = *hr;
         cont.done = LVR_RUNNING;
         LVCHK(hipMemcpyAsync(run, &cont, sizeof cont, hipMemcpyHostToDevice, st));
@@ -542,7 +599,7 @@ int dist_create(DistLevel& d, const History* h, uint32_t rank, uint32_t world, u
   d.nq = level_nq(d.K);
   d.cb = lv_cfg_bytes(d.nq);
   if (d.b.forced[0]) { err = "history is structurally illegal (unmatched events)"; return S2LC_EINVAL; }
-  if (level_buffers(d.b, d.nq, err)) return S2LC_EHIP;
+  if (level_buffers(d.b, d.nq, err, true)) return S2LC_EHIP;
   if (lv_grids(d.b.lv, d.nq, err)) return S2LC_EHIP;
   LVCHK(hipMalloc(&d.own_cnt, 8 * sizeof(uint32_t)));
   LVCHK(hipMalloc(&d.own_pos, (size_t)d.b.lv.scap * sizeof(uint32_t)));

@@ -63,6 +63,7 @@ struct SearchGeom {
 // Buffers of the device-wide level search (level.hip), reused across histories.
 struct LevelBufs {
   uint32_t nq = 0, scap = 0, ht_mask = 0;
+  uint32_t scap_max = 0;                    // what the budget allows (a quarter of free HBM, <= 48 GiB)
   uint8_t* stg[2] = {nullptr, nullptr};     // staging arrays (frontier of round r = staging of round r-1)
   uint32_t* idx[2] = {nullptr, nullptr};    // frontier index lists
   unsigned long long* ht[2] = {nullptr, nullptr};  // dedupe tables: round r inserts into ht[r & 1]
@@ -83,6 +84,7 @@ struct LevelStats {
   double ms = 0;
   uint64_t rounds = 0, configs = 0, children = 0;
   uint32_t max_frontier = 0, histories = 0, chunk_retries = 0;
+  uint32_t grows = 0;  // staging capacity raised after an overflowing round
   uint32_t syncs = 0;  // host synchronizations (one per batch of device-driven rounds)
   uint64_t persist_rounds = 0, persist_launches = 0;  // rounds run inside lv_persist
   uint64_t solo_rounds = 0;  // of those, one-configuration rounds run by one workgroup

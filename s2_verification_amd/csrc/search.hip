@@ -515,6 +515,16 @@ int batch_run(DevBatch& b, hipStream_t stream, const RunOpts& ro, RunStats& st, 
     t_enq = steady_ns();
     HIPCHK(stream_wait(stream, b.ev[6]));
     t_wait = steady_ns();
+#ifdef S2LC_PROF
+    {
+      unsigned long long gp[16];
+      HIPCHK(hipMemcpyFromSymbol(gp, HIP_SYMBOL(g_prof), sizeof gp));
+      const double rd = gp[13] ? (double)gp[13] : 1.0;
+      fprintf(stderr, "[s2lc prof] pack: rounds %llu children %llu | cycles/round expand %.0f closure %.0f dedupe+rest %.0f"
+              " | closure passes/round %.2f, of which with a window reload %.2f\n",
+              gp[13], gp[15], gp[10] / rd, gp[11] / rd, gp[12] / rd, gp[8] / rd, gp[9] / rd);
+    }
+#endif
     if (fast && b.h_agg[PACK_AGG_OVERFLOW] + b.h_agg[8 + PACK_AGG_OVERFLOW] + b.h_agg[16 + PACK_AGG_OVERFLOW] == 0) {
       for (int li = 0; li < 3; ++li) {
         if (!launched[li]) continue;
@@ -554,16 +564,6 @@ int batch_run(DevBatch& b, hipStream_t stream, const RunOpts& ro, RunStats& st, 
       if (li == 1) st.pack16_ms = ms;
     }
     t_ev = steady_ns();
-#ifdef S2LC_PROF
-    {
-      unsigned long long gp[16];
-      HIPCHK(hipMemcpyFromSymbol(gp, HIP_SYMBOL(g_prof), sizeof gp));
-      const double rd = gp[13] ? (double)gp[13] : 1.0;
-      fprintf(stderr, "[s2lc prof] pack: rounds %llu children %llu | cycles/round expand %.0f closure %.0f dedupe+rest %.0f"
-              " | closure passes/round %.2f, of which with a window reload %.2f\n",
-              gp[13], gp[15], gp[10] / rd, gp[11] / rd, gp[12] / rd, gp[8] / rd, gp[9] / rd);
-    }
-#endif
     // histories that outgrew the packed frontier go on to the workgroup passes
     // (in history order: h_hist / h_res are pinned host memory, slow to read
     // in LPT order — 180-240 us per C4 step — and fast sequentially)

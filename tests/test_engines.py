@@ -235,6 +235,27 @@ def test_hard_round_counts(name, off, mode, monkeypatch):
 
 
 @pytest.mark.parametrize("mode", ["default", "no_persist"])
+def test_level_buffers_grow_on_overflow(mode, monkeypatch):
+    """The level search starts with a small staging capacity (here 16 MiB of
+    buffers) and raises it when a round overflows: C5wide (frontier up to
+    273 k) then gives the committed verdict and every round's count."""
+    from s2_verification_amd import workloads as W
+    _set_mode(monkeypatch, mode)
+    monkeypatch.setenv("S2LC_LEVEL_BUDGET_MB", "16")
+    ref = golden("hard_round_counts.json")["C5wide"]
+    assert config_digest("C5wide") == ref["digest"]
+    want = ref["0"]
+    c = s2.Checker(round_counts=True)
+    b = c.batch([W.config_history("C5wide")])
+    r = b.check()[0]
+    st = b.stats()
+    assert r.verdict == want["verdict"] and r.rounds == want["rounds"], r
+    assert b.round_counts(0) == want["counts"]
+    assert st["level_grows"] >= 1, st
+    assert r.witness is not None
+
+
+@pytest.mark.parametrize("mode", ["default", "no_persist"])
 @pytest.mark.parametrize("name,off", [("H174", 1), ("H174", 8), ("C5bad", 1), ("C5bad", 8)])
 def test_hard_exploding_ablation_prefix(name, off, mode, monkeypatch):
     """P1 or the indefinite deferral switched off on the hard histories: the
