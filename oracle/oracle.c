@@ -292,6 +292,14 @@ static int check_wgl_impl(const or_event* ev, size_t n_ev, int compute_partial, 
         int found = 0;
         if (b) for (int k = 0; k < b->n && !found; k++)
           if (memcmp(b->e[k].bits, nl, sizeof(uint64_t) * (size_t)W) == 0 && sset_equal(&b->e[k].st, &ns)) found = 1;
+        if (!found && ncalls >= n + 1) {
+          /* more calls on the stack than calls in the history: only a return
+           * shared by two calls (duplicate ids) gets here; porcupine's calls
+           * slice would grow, this restatement stops (Unknown) */
+          free(nl); free(ns.v);
+          result = OR_UNKNOWN;
+          break;
+        }
         if (!found) {
           b = cache_bucket(&c, hk, 1);
           if (b->n == b->cap) { b->cap = b->cap ? b->cap * 2 : 2; b->e = (centry*)realloc(b->e, sizeof(centry) * (size_t)b->cap); }

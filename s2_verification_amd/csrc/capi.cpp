@@ -415,6 +415,35 @@ int collect_results(DevBatch& B, const RunStats& stats, bool witness_recorded, s
           moves = mv.data();
         }
         const uint32_t n_moves = corrupt && r.verdict == V_OK ? (uint32_t)mv.size() : r.witness_len;
+        if (H.literal) {
+          // the literal engine wrote the call events of porcupine's calls
+          // stack; ops are the call events in order (History::op_call)
+          if (r.verdict != V_OK) continue;
+          order.resize(n_moves);
+          bool ok = true;
+          for (uint32_t k = 0; k < n_moves && ok; ++k) {
+            const auto it = std::lower_bound(H.op_call.begin(), H.op_call.end(), moves[k]);
+            ok = it != H.op_call.end() && *it == moves[k];
+            if (ok) order[k] = (uint32_t)(it - H.op_call.begin());
+          }
+          if (!ok || !replay_literal(H, order.data(), order.size())) {
+            o.verdict = S2LC_UNKNOWN;
+            o.reason = S2LC_R_WITNESS_INVALID;
+            invalid = 1;
+            continue;
+          }
+          if (flat_ids) {
+            int64_t* w = flat_ids + flat_offs[i];
+            for (size_t k = 0; k < order.size(); ++k) w[k] = H.op_ids[order[k]];
+            o.witness_len = (uint32_t)order.size();
+            continue;
+          }
+          o.witness = (int64_t*)malloc(sizeof(int64_t) * (order.size() ? order.size() : 1));
+          if (!o.witness) { oom = 1; continue; }
+          for (size_t k = 0; k < order.size(); ++k) o.witness[k] = H.op_ids[order[k]];
+          o.witness_len = (uint32_t)order.size();
+          continue;
+        }
         if (r.verdict == V_OK) {
           const bool ok = rebuild_linearization(H, moves, n_moves, r.p4 != 0, order, ident, false) &&
                           replay_path(H, order.data(), ident.data(), order.size());
@@ -794,6 +823,10 @@ int s2lc_check_partials(s2lc_ctx* c, const s2lc_history* h, s2lc_partials* out) 
   memset(out, 0, sizeof *out);
   const History& H = h->h;
   if (H.status) { c->err = H.error; return H.status; }
+  if (H.literal) {  // (porcupine's own partials there come from its id-keyed DFS: not restated)
+    c->err = "partial linearizations of histories with duplicate op ids";
+    return S2LC_EUNSUPPORTED;
+  }
   s2lc_result r;
   int rc = s2lc_check(c, h, &r);
   if (rc) { s2lc_result_free(&r); return rc; }

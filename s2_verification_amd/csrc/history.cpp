@@ -95,13 +95,11 @@ int History::finalize() {
     if (events[i].kind == 0) { ncall[d]++; call[d] = (uint32_t)i; }
     else { nret[d]++; ret[d] = (uint32_t)i; }
   }
-  for (uint32_t d = 0; d < m; ++d) {
-    if (ncall[d] > 1 || nret[d] > 1) {
-      status = S2LC_EUNSUPPORTED;
-      error = "op_id " + std::to_string(ids[d]) + " has more than one Start or Finish";
-      return status;
-    }
-  }
+  literal = false;
+  lit_id.clear();
+  lit_match.clear();
+  for (uint32_t d = 0; d < m && !literal; ++d)
+    if (ncall[d] > 1 || nret[d] > 1) literal = true;
   // Validate what the Go model would dereference (main.go:279, 313, 327).
   for (size_t i = 0; i < E; ++i) {
     const Event& e = events[i];
@@ -113,6 +111,32 @@ int History::finalize() {
     } else if (!e.failure && !e.has_tail) {
       status = S2LC_EINVAL; error = "success output without tail"; return status;
     }
+  }
+  if (literal) {
+    // porcupine makeLinkedEntries: walk the events backwards; a return
+    // registers itself for its id, a call takes the registered return (the
+    // nearest later one with its id; two calls may take the same return)
+    lit_id.assign(dense.begin(), dense.end());
+    lit_match.assign(E, -1);
+    std::vector<int32_t> reg(m, -1);
+    for (size_t i = E; i-- > 0;) {
+      if (events[i].kind == 1) reg[dense[i]] = (int32_t)i;
+      else lit_match[i] = reg[dense[i]];
+    }
+    recs.clear(); rec_op.clear(); chain_start.clear(); K = 0;
+    n_ident = 0; hflags = 0; max_chain_len = 0;
+    op_ids.clear(); op_call.clear(); op_ret.clear();
+    for (size_t i = 0; i < E; ++i)
+      if (events[i].kind == 0) {
+        op_call.push_back((uint32_t)i);
+        op_ret.push_back(lit_match[i] >= 0 ? (uint32_t)lit_match[i] : EV_INF);
+        op_ids.push_back(events[i].op_id);
+      }
+    n_ops = (uint32_t)op_call.size();
+    op_rec.assign(n_ops, EV_INF);
+    if (tokens.size() > 0xFFFF) { status = S2LC_EUNSUPPORTED; error = "more than 65535 distinct fencing tokens"; }
+    if (pool.size() > 0xFFFFFFFFull) { status = S2LC_EUNSUPPORTED; error = "more than 2^32 record hashes"; }
+    return status;
   }
   for (uint32_t d = 0; d < m; ++d)
     if (ncall[d] != 1 || nret[d] != 1 || ret[d] < call[d]) structural = S2LC_R_UNMATCHED;

@@ -64,6 +64,14 @@ struct History {
   std::vector<uint32_t> op_rec;            // dense op id -> record position
   uint16_t hflags = 0;
   uint32_t max_chain_len = 0;
+  // Duplicate op ids (more than one Start or Finish per op_id): porcupine's
+  // checkSingle is run literally (literal.hip), on its own linked entry list.
+  // Ops are then the call events in order (op_call), op_ret their porcupine
+  // match (makeLinkedEntries: the nearest later return with the same id;
+  // EV_INF when none), op_ids their Event.Id; there are no chains.
+  bool literal = false;
+  std::vector<int32_t> lit_id;     // per event: porcupine's dense id (renumber)
+  std::vector<int32_t> lit_match;  // per event: a call's matched return event (-1: none / a return)
 
   // Validate, renumber, classify, decompose into chains. Idempotent.
   int finalize();

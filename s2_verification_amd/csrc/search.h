@@ -45,6 +45,25 @@ struct HistResult {
 };
 static_assert(sizeof(HistResult) == 64, "HistResult is 64 bytes");
 
+// The literal engine (literal.hip: porcupine's checkSingle, one thread per
+// duplicate-id history).
+struct LitDesc {
+  uint32_t h;         // batch history index
+  uint32_t n_ev;      // events
+  uint32_t ev_off;    // first LitEv
+  uint32_t W;         // bitset words (porcupine: len(entries) / 2 bits)
+  uint64_t mem_off;   // this history's work slice in the literal buffer
+  uint64_t mem_bytes;
+};
+struct LitEv {
+  OpRec rec;          // a call with a matched return: the op's record (batch pool offsets)
+  int32_t id;         // porcupine's dense id (renumber)
+  int32_t match;      // call: node of its matched return (event + 1), 0 = none; return: -1
+  uint32_t kind;      // 0 call, 1 return
+  uint32_t _pad;
+};
+static_assert(sizeof(LitEv) == 128, "LitEv layout (OpRec is 64-byte aligned)");
+
 struct SearchGeom {
   bool shared;         // arrays in LDS (true) or in a per-workgroup HBM slab
   uint32_t block;      // threads per workgroup (64 or 256)
@@ -143,6 +162,14 @@ struct DevBatch {
   // kernels: the run read their per-launch totals only); batch_host_results
   // copies it on first use
   bool h_res_stale = false;
+  // duplicate-id histories (History::literal): the literal engine's tables
+  std::vector<uint8_t> literal;      // per history
+  std::vector<LitDesc> lit_desc;
+  std::vector<LitEv> lit_ev;
+  uint8_t* lit_meta = nullptr;       // device: descs | events
+  uint8_t* lit_mem = nullptr;        // device: one work slice per literal history
+  size_t lit_bytes = 0, lit_mem_bytes = 0;
+  bool lit_dev_ready = false;
   unsigned long long* agg = nullptr;   // device: per packed launch, 8 totals (pack_kernel PackAgg)
   unsigned long long* h_agg = nullptr; // pinned copy
   uint64_t in_bytes_list[3] = {0, 0, 0};  // input SoA bytes of each packed list
@@ -182,6 +209,12 @@ int batch_upload(DevBatch& b, const std::vector<const History*>& hs, uint32_t re
 void batch_release(DevBatch& b);
 // Copy the witness moves of the last run into b.h_moves (pinned).
 int batch_fetch_moves(DevBatch& b, std::string& err);
+// the literal engine (literal.hip)
+void literal_prepare(const History& h, uint32_t i, uint64_t pool_off, std::vector<LitDesc>& descs,
+                     std::vector<LitEv>& evs);
+int literal_run(DevBatch& b, hipStream_t stream, const RunOpts& ro, const unsigned long long* deadline,
+                std::string& err);
+void literal_release(DevBatch& b);
 // h_res valid on the host (copies it if the last run left it on the device)
 int batch_host_results(DevBatch& b, std::string& err);
 // out[i] = fold_hashes_blk(seeds[i], pool[offs[i] ..+ cnts[i]]) on the device.
@@ -247,6 +280,8 @@ bool real_time_ok(const History& h, const uint32_t* order, size_t n);
 // check), porcupine's ToModel().Step semantics; false if the state set would
 // exceed 2^16 states.
 bool replay_order(const History& h, const uint32_t* order, size_t n);
+// A duplicate-id history's literal-engine order through the powerset model.
+bool replay_literal(const History& h, const uint32_t* order, size_t n);
 // Single-path replay: real-time check, then every op's claimed outcome must be
 // one of s2Model.Step's successors (main.go:264-335). A path of states is a
 // certificate that the powerset run never empties.

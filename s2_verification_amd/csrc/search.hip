@@ -160,6 +160,10 @@ int batch_upload(DevBatch& b, const std::vector<const History*>& hs, uint32_t re
   b.n_hist = (uint32_t)n;
   b.src = hs;
   b.forced.assign(n, 0);
+  b.literal.assign(n, 0);
+  b.lit_desc.clear();
+  b.lit_ev.clear();
+  b.lit_dev_ready = false;
   b.rc_valid = false;
   uint32_t kmax_needed = 1;
   size_t n_recs = 0, n_pool = 0, n_cs = 0;
@@ -174,6 +178,7 @@ int batch_upload(DevBatch& b, const std::vector<const History*>& hs, uint32_t re
     const History& h = *hs[i];
     if (h.status != 0) { err = "history " + std::to_string(i) + ": " + h.error; return h.status; }
     if (h.structural) b.forced[i] = 1;
+    if (h.literal) b.literal[i] = 1;
     if (h.K > LEVEL_KMAX) { err = "history has more than 512 concurrent chains"; return S2LC_EUNSUPPORTED; }
     if (h.max_chain_len >= 0xFFFF) { err = "chain longer than 65534 ops"; return S2LC_EUNSUPPORTED; }
     if (h.K <= 128) kmax_needed = std::max(kmax_needed, h.K);
@@ -252,6 +257,8 @@ int batch_upload(DevBatch& b, const std::vector<const History*>& hs, uint32_t re
     R.witness_off = b.h_moves_off[i];
   });
   for (size_t i = 0; i < n; ++i) b.algo_bytes_inputs += b.h_in_bytes[i];
+  for (size_t i = 0; i < n; ++i)
+    if (b.literal[i]) literal_prepare(*hs[i], (uint32_t)i, off_pool[i], b.lit_desc, b.lit_ev);
   // LPT order, longest first. A history's search runs one round per
   // non-identity op it linearizes (appends: n_ops - n_ident), a dependent
   // chain whatever the engine, so that count leads the key; n_ops x K breaks
@@ -261,7 +268,7 @@ int batch_upload(DevBatch& b, const std::vector<const History*>& hs, uint32_t re
   b.lpt.clear();
   std::vector<uint64_t> key(n, 0);
   for (uint32_t i = 0; i < n; ++i) {
-    if (b.forced[i]) continue;
+    if (b.forced[i] || b.literal[i]) continue;
     b.lpt.push_back(i);
     const History& h = *hs[i];
     key[i] = ((uint64_t)(h.n_ops - h.n_ident) << 40) | ((uint64_t)h.n_ops * h.K & ((1ull << 40) - 1));
@@ -311,6 +318,7 @@ int batch_upload(DevBatch& b, const std::vector<const History*>& hs, uint32_t re
 
 void batch_release(DevBatch& b) {
   level_release(b);
+  literal_release(b);
   if (b.agg) (void)hipFree(b.agg);
   if (b.h_agg) (void)hipHostFree(b.h_agg);
   b.agg = nullptr;
@@ -416,6 +424,13 @@ int batch_run(DevBatch& b, hipStream_t stream, const RunOpts& ro, RunStats& st, 
     prm.deadline = d;
   }
 
+  // duplicate-id histories: porcupine's own search (literal.hip), first on
+  // the stream, so every later read-back of the results includes them
+  if (!b.lit_desc.empty()) {
+    const int rc = literal_run(b, stream, ro, prm.deadline, err);
+    if (rc) return rc;
+  }
+
   // the histories of each engine, LPT order
   std::vector<uint32_t> todo;   // workgroup passes
   std::vector<uint32_t> level;  // device-wide level search
@@ -507,7 +522,8 @@ int batch_run(DevBatch& b, hipStream_t stream, const RunOpts& ro, RunStats& st, 
     // the run down the full path (results read back, overflow scan).
     uint32_t n_forced = 0;
     for (uint32_t i = 0; i < b.n_hist; ++i) n_forced += b.forced[i] ? 1u : 0u;
-    const bool fast = todo.empty() && level.empty() && !ro.round_counts && n_packed + n_forced == b.n_hist;
+    const bool fast = todo.empty() && level.empty() && !ro.round_counts && b.lit_desc.empty() &&
+                      n_packed + n_forced == b.n_hist;
     if (fast)
       HIPCHK(hipMemcpyAsync(b.h_agg, b.agg, 24 * sizeof(unsigned long long), hipMemcpyDeviceToHost, stream));
     else

@@ -31,8 +31,9 @@ std::string tok_str(const History& h, uint32_t id) { return id ? h.tokens[id - 1
 // DescribeOperation (main.go:341-352) with formatAppendCall / formatReadCall /
 // formatCheckTailCall (main.go:362-426).
 std::string describe_op(const History& h, uint32_t d) {
+  static const Event no_return{};  // (a call without a return: duplicate-id histories)
   const Event& in = h.events[h.op_call[d]];
-  const Event& out = h.events[h.op_ret[d]];
+  const Event& out = h.op_ret[d] < h.events.size() ? h.events[h.op_ret[d]] : no_return;
   if (in.input_type == 0) {
     std::string failure = "none";
     if (out.definite) failure = "definite";
@@ -165,7 +166,8 @@ static int render(const s2lc_history* hh, const s2lc_result* r, const s2lc_parti
       fprintf(f, "<text x=\"0\" y=\"%zu\">c%lld</text>\n", i * rh + 15, (long long)clients[i]);
     for (uint32_t d = 0; d < h.n_ops; ++d) {
       const int y = row[h.events[h.op_call[d]].client_id] * rh + 3;
-      const double x0 = 60.0 + xs * h.op_call[d], x1 = 60.0 + xs * h.op_ret[d] + xs * 0.8;
+      const double x0 = 60.0 + xs * h.op_call[d],
+                   x1 = 60.0 + xs * std::min<size_t>(h.op_ret[d], n_ev ? n_ev - 1 : 0) + xs * 0.8;
       const char* cls = pos[d] >= 0 ? "lin" : (r->verdict == S2LC_OK ? "ok" : "out");
       std::string tip = "op " + std::to_string(h.op_ids[d]) + ": " + describe_op(h, d);
       if (pos[d] >= 0) tip += "\nlinearized #" + std::to_string(pos[d]) + ", state after: " + after[(size_t)pos[d]];

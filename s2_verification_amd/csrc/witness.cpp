@@ -262,4 +262,34 @@ bool replay_order(const History& h, const uint32_t* order, size_t n) {
   return true;
 }
 
+// Duplicate-id histories (History::literal): the literal engine's order is
+// porcupine's own calls stack, a sequence of (call, matched return) ops that
+// its DFS stepped through ToModel().Step; certify it by replaying those steps
+// through the CPU model, the powerset state never empty. (Real-time order is
+// porcupine's list discipline there: two calls may share one return.)
+bool replay_literal(const History& h, const uint32_t* order, size_t n) {
+  if (!h.literal || n != h.n_ops) return false;
+  std::vector<uint8_t> seen(h.n_ops, 0);
+  std::vector<State> set{State{0, 0, 0}}, next;
+  for (size_t i = 0; i < n; ++i) {
+    const uint32_t d = order[i];
+    if (d >= h.n_ops || seen[d] || h.op_ret[d] == EV_INF) return false;
+    seen[d] = 1;
+    const OpRec r = h.rec_of(d);
+    next.clear();
+    for (const State& s : set) {
+      State kids[2];
+      const int nk = s2_step(r, s, h.pool.data(), kids);
+      for (int k = 0; k < nk; ++k) {
+        bool dup = false;
+        for (const State& x : next) if (state_eq(x, kids[k])) { dup = true; break; }
+        if (!dup) next.push_back(kids[k]);
+      }
+    }
+    if (next.empty() || next.size() > (1u << 20)) return false;
+    set.swap(next);
+  }
+  return true;
+}
+
 }  // namespace s2lc

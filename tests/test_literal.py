@@ -1,0 +1,143 @@
+"""Duplicate op ids on the GPU: porcupine's checkSingle run literally
+(csrc/literal.hip, one thread per history) against the oracle's restatement
+of the same search (oracle/oracle.c check_wgl: renumber, makeLinkedEntries,
+the id-keyed bitset and the (bitset, powerset state) cache). With repeated
+ids porcupine's verdict depends on its DFS order, so the pin
+is the search itself: the verdict, the cache insertions and the Step calls
+must all be equal. Parity is unpinned by the reference (no Go, porcupine
+absent): the oracle is the restatement checked on the reference's own cases.
+Every Ok carries porcupine's linearization, certified through the CPU model."""
+import random
+
+import pytest
+
+import oracle as orc
+import s2_verification_amd as s2
+from helpers import random_history, to_s2_events
+
+pytestmark = pytest.mark.gpu
+
+
+def dup_history(rng, n_ops, n_clients=3, p_dup=0.35, overlap=False):
+    """A random history whose op ids repeat: op i takes the id of an earlier
+    op with probability p_dup. Without `overlap` an id is reused only after
+    its last op returned, so every call keeps a return of its own; with it,
+    ops of one id may overlap, and makeLinkedEntries then links two calls to
+    one return."""
+    ev = random_history(rng, n_ops, n_clients=n_clients)
+    call_at = {e["op_id"]: k for k, e in enumerate(ev) if e["kind"] == "call"}
+    ret_at = {e["op_id"]: k for k, e in enumerate(ev) if e["kind"] == "return"}
+    ids = list(range(n_ops))
+    last = {}  # id -> its latest op
+    order = sorted(range(n_ops), key=lambda i: call_at[i])
+    for i in order:
+        if last and rng.random() < p_dup:
+            j = rng.choice(sorted(last))
+            if overlap or ret_at[last[j]] < call_at[i]:
+                ids[i] = j
+        last[ids[i]] = i
+    return [dict(e, op_id=ids[e["op_id"]]) for e in ev]
+
+
+def check(hs_events):
+    hs = [s2.History.from_events(to_s2_events(e)) for e in hs_events]
+    res = s2.Checker().check_batch(hs)
+    return hs, res
+
+
+def oracle(ev):
+    return orc.check_wgl(ev, compute_partial=False, timeout=60.0)
+
+
+def test_sequential_reuse_of_an_id():
+    ev = [{"kind": "call", "op_id": 1, "input_type": 0, "num_records": 1, "record_hashes": [5]},
+          {"kind": "return", "op_id": 1, "failure": False, "definite_failure": False, "tail": 1},
+          {"kind": "call", "op_id": 1, "input_type": 2},
+          {"kind": "return", "op_id": 1, "failure": False, "definite_failure": False, "tail": 1}]
+    hs, res = check([ev])
+    assert hs[0].info()["n_ops"] == 2 and hs[0].info()["n_chains"] == 0
+    # porcupine prunes the second op (its bitset and state equal the first's
+    # cache entry): Illegal, as the literal search must say too
+    assert oracle(ev)[0] == "Illegal" and res[0].verdict == s2.Illegal
+
+
+def test_two_calls_share_one_return():
+    """makeLinkedEntries links both calls to the nearest later return of
+    their id; porcupine's list surgery then runs on a shared node."""
+    ev = [{"kind": "call", "op_id": 7, "input_type": 2},
+          {"kind": "call", "op_id": 7, "input_type": 2},
+          {"kind": "return", "op_id": 7, "failure": False, "definite_failure": False, "tail": 0},
+          {"kind": "return", "op_id": 7, "failure": False, "definite_failure": False, "tail": 0}]
+    v, _ = oracle(ev)
+    hs, res = check([ev])
+    if v == "Panic":
+        assert res[0].verdict == s2.Unknown
+    else:
+        assert res[0].verdict == v
+
+
+def test_random_duplicate_id_histories_match_the_literal_oracle():
+    rng = random.Random(20261017)
+    cases = [dup_history(rng, rng.randint(2, 14), n_clients=rng.randint(2, 4)) for _ in range(400)]
+    hs, res = check(cases)
+    seen = {"Ok": 0, "Illegal": 0}
+    for i, (ev, r) in enumerate(zip(cases, res)):
+        v, st = oracle(ev)
+        if v == "Panic":  # (porcupine would crash: a nil entry or a bitset index past its length)
+            assert r.verdict == s2.Unknown, (i, r)
+            continue
+        assert r.verdict == v, (i, r.verdict, v)
+        assert r.configs_explored == st["cache_inserts"], (i, r.configs_explored, st)
+        seen[v] += 1
+        if v == "Ok":
+            assert r.witness is not None and len(r.witness) == hs[i].info()["n_ops"], (i, r)
+    assert seen["Ok"] > 50 and seen["Illegal"] > 50, seen
+
+
+def test_shared_returns_terminate():
+    """Overlapping ops with one id: two calls linked to one return. Porcupine's
+    list surgery on the shared node can send its search round a cycle (with
+    no timeout it would never return); the GPU search is bounded
+    (S2LC_LITERAL_ITERS) and must end, with the oracle's verdict whenever the
+    oracle itself ends within 2 s, else Unknown."""
+    import os
+    rng = random.Random(20261017)
+    cases = [dup_history(rng, rng.randint(2, 14), n_clients=rng.randint(2, 4), overlap=True) for _ in range(120)]
+    os.environ["S2LC_LITERAL_ITERS"] = "200000"
+    try:
+        hs, res = check(cases)
+    finally:
+        del os.environ["S2LC_LITERAL_ITERS"]
+    agree = 0
+    for i, (ev, r) in enumerate(zip(cases, res)):
+        v, _ = orc.check_wgl(ev, compute_partial=False, timeout=2.0)
+        if v in ("Ok", "Illegal") and r.verdict != s2.Unknown:
+            assert r.verdict == v, (i, r.verdict, v)
+            agree += 1
+        elif v in ("Unknown", "Panic"):
+            assert r.verdict == s2.Unknown, (i, r.verdict, v)
+    assert agree >= 10, agree
+
+
+def test_mixed_batch_routes_each_history_to_its_engine():
+    """Duplicate-id histories beside ordinary ones (packed kernel, level
+    search) in one batch: every verdict equals the oracle's."""
+    from s2_verification_amd import workloads as W
+    rng = random.Random(7)
+    evs = []
+    for k in range(60):
+        evs.append(dup_history(rng, rng.randint(3, 12)) if k % 2 else random_history(rng, rng.randint(3, 12)))
+    hs = [s2.History.from_events(to_s2_events(e)) for e in evs]
+    hs.append(W.config_history("C1"))
+    res = s2.Checker().check_batch(hs)
+    for i, (h, r) in enumerate(zip(hs, res)):
+        v, _ = oracle(orc.from_s2lc_numpy(h.events_numpy()))
+        if v == "Panic":
+            assert r.verdict == s2.Unknown
+        else:
+            assert r.verdict == v, (i, r.verdict, v)
+    b = s2.Checker().batch(hs)
+    b.run()
+    flat = b.results_flat(with_witness=True)  # certified witnesses, flat form
+    want = [{s2.Ok: s2.S2LC_OK, s2.Illegal: s2.S2LC_ILLEGAL, s2.Unknown: s2.S2LC_UNKNOWN}[x.verdict] for x in res]
+    assert flat["verdict"].tolist() == want
