@@ -89,7 +89,7 @@ struct Head {
 // the loader or the simulator makes): stored without the event array.
 bool compactable(const History& h) {
   h.ensure_events();
-  if (h.status || h.structural || h.events.size() != 2ull * h.n_ops || h.op_rec.size() != h.n_ops) return false;
+  if (h.status || h.structural || h.literal || h.events.size() != 2ull * h.n_ops || h.op_rec.size() != h.n_ops) return false;
   for (uint32_t d = 0; d < h.n_ops; ++d) {
     Event c, r;
     event_pair(h, d, h.events[h.op_call[d]].client_id, h.events[h.op_ret[d]].client_id, c, r);
@@ -206,6 +206,16 @@ bool read_section(const uint8_t* p, const uint8_t* end, History& h) {
   h.hflags = (uint16_t)hd.hflags;
   h.max_chain_len = hd.max_chain_len;
   const bool searchable = hd.status == 0 && hd.structural == 0;
+  if (searchable && hd.mode == 1 && hd.n_cs == 0 && hd.n_recs == 0 && hd.K == 0) {
+    // a duplicate-id history (History::literal): no chains; its porcupine
+    // linking is rebuilt from the events by finalize, which must agree
+    for (const Event& e : h.events)
+      if (e.hash_off + e.hash_cnt > hd.n_pool || e.set_tok > hd.n_tokens || e.batch_tok > hd.n_tokens) return false;
+    const uint32_t n_ops = hd.n_ops;
+    const std::vector<int64_t> ids = h.op_ids;
+    if (h.finalize() != 0 || !h.literal || h.n_ops != n_ops || h.op_ids != ids) return false;
+    return true;
+  }
   if (!searchable) {
     // the check never reads records here (the verdict is fixed or the history
     // refused); only what the event API reads must be in range

@@ -107,3 +107,21 @@ def test_malformed_images_are_refused():
                 h.events()
         except s2.S2LCError as e:
             assert e.status == -2
+
+
+def test_duplicate_id_histories_round_trip():
+    """Duplicate-id histories (the literal engine's) are stored with their
+    events and re-linked on load (History::finalize): same ops, same ids."""
+    import random
+    import sys
+    sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+    from test_literal import dup_history
+    from helpers import to_s2_events
+    rng = random.Random(3)
+    hs = [s2.History.from_events(to_s2_events(dup_history(rng, 8, overlap=bool(k % 2)))) for k in range(6)]
+    back = s2.load_cache(s2.save_cache(hs))
+    for a, b in zip(hs, back):
+        assert a.info() == b.info()
+        ea, eb = a.events_numpy(), b.events_numpy()
+        for f in ("kind", "op_id", "input_type", "num_records", "n_record_hashes", "failure", "tail", "stream_hash"):
+            assert (ea[f] == eb[f]).all(), f
