@@ -78,20 +78,25 @@ def test_two_calls_share_one_return():
 
 def test_random_duplicate_id_histories_match_the_literal_oracle():
     rng = random.Random(20261017)
-    cases = [dup_history(rng, rng.randint(2, 14), n_clients=rng.randint(2, 4)) for _ in range(400)]
+    cases = [dup_history(rng, rng.randint(2, 14), n_clients=rng.randint(2, 4), p_dup=0.7) for _ in range(400)]
     hs, res = check(cases)
     seen = {"Ok": 0, "Illegal": 0}
+    n_dup = 0
     for i, (ev, r) in enumerate(zip(cases, res)):
         v, st = oracle(ev)
         if v == "Panic":  # (porcupine would crash: a nil entry or a bitset index past its length)
             assert r.verdict == s2.Unknown, (i, r)
             continue
         assert r.verdict == v, (i, r.verdict, v)
-        assert r.configs_explored == st["cache_inserts"], (i, r.configs_explored, st)
+        calls = [e["op_id"] for e in ev if e["kind"] == "call"]
+        if len(set(calls)) < len(calls):  # the literal engine's: the same search, step for step
+            n_dup += 1
+            assert r.configs_explored == st["cache_inserts"], (i, r.configs_explored, st)
         seen[v] += 1
         if v == "Ok":
             assert r.witness is not None and len(r.witness) == hs[i].info()["n_ops"], (i, r)
     assert seen["Ok"] > 50 and seen["Illegal"] > 50, seen
+    assert n_dup >= 150, n_dup  # (189 with this seed: 160 Illegal, 29 Ok)
 
 
 def test_shared_returns_terminate():
