@@ -316,7 +316,9 @@ int literal_run(DevBatch& b, hipStream_t stream, const RunOpts& ro, const unsign
       b.lit_desc[k].mem_off = (uint64_t)k * slice;
       b.lit_desc[k].mem_bytes = slice;
     }
-    const size_t need_d = n * sizeof(LitDesc), need_e = std::max<size_t>(1, b.lit_ev.size()) * sizeof(LitEv);
+    // (the events start 256-byte aligned: LitEv holds a 64-byte aligned OpRec)
+    const size_t need_d = (n * sizeof(LitDesc) + 255) & ~(size_t)255,
+                 need_e = std::max<size_t>(1, b.lit_ev.size()) * sizeof(LitEv);
     if (b.lit_bytes < need_d + need_e || !b.lit_meta) {
       if (b.lit_meta) (void)hipFree(b.lit_meta);
       b.lit_meta = nullptr;
@@ -329,12 +331,12 @@ int literal_run(DevBatch& b, hipStream_t stream, const RunOpts& ro, const unsign
       LITCHK(hipMalloc(&b.lit_mem, slice * n));
       b.lit_mem_bytes = slice * n;
     }
-    LITCHK(hipMemcpy(b.lit_meta, b.lit_desc.data(), need_d, hipMemcpyHostToDevice));
+    LITCHK(hipMemcpy(b.lit_meta, b.lit_desc.data(), n * sizeof(LitDesc), hipMemcpyHostToDevice));
     if (!b.lit_ev.empty()) LITCHK(hipMemcpy(b.lit_meta + need_d, b.lit_ev.data(), b.lit_ev.size() * sizeof(LitEv), hipMemcpyHostToDevice));
     b.lit_dev_ready = true;
   }
   const LitDesc* d = reinterpret_cast<const LitDesc*>(b.lit_meta);
-  const LitEv* e = reinterpret_cast<const LitEv*>(b.lit_meta + n * sizeof(LitDesc));
+  const LitEv* e = reinterpret_cast<const LitEv*>(b.lit_meta + ((n * sizeof(LitDesc) + 255) & ~(size_t)255));
   // loop iterations per history (S2LC_LITERAL_ITERS; a single GPU thread
   // runs ~1 M per second)
   unsigned long long iters = 1ull << 22;
