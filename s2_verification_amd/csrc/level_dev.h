@@ -57,10 +57,11 @@ struct __attribute__((aligned(128))) LCfg {
   uint32_t move;    // chain | MOVE_IDENT; LV_NONE initial configuration; LV_HOLE unused slot
   uint32_t trace;   // own trace id once in a frontier
   uint32_t slot;    // table slot (cleared when this configuration is expanded)
-  uint32_t _pad[20];
+  uint64_t chx;     // XOR of its chain terms (lv_chain_term): its children's fingerprints start here
+  uint32_t _pad[18];
   uint16_t cnt[64 * NQ];
 };
-static_assert(offsetof(LCfg<1>, trace) == 40, "LCfg::trace offset");
+static_assert(offsetof(LCfg<1>, trace) == 40 && offsetof(LCfg<1>, chx) == 48, "LCfg header offsets");
 static_assert(offsetof(LCfg<1>, cnt) == 128 && sizeof(LCfg<5>) == 128 * 6, "LCfg line layout");
 
 // Per-round device counters (double buffered by round parity). Staging is
@@ -411,7 +412,7 @@ __device__ __forceinline__ int lv_closure(LvHot (&H)[NQ], uint32_t (&d)[NQ], con
 // reserves LV_RESERVE slots of its stripe at a time (rk / rleft, wave-uniform).
 template <int NQ>
 __device__ __forceinline__ void lv_stage(const LvParams& p, uint32_t st, uint32_t& rk, uint32_t& rleft, const State& s,
-                                         uint64_t fp, uint32_t minret, uint32_t ptrace, uint32_t move,
+                                         uint64_t fp, uint64_t chx, uint32_t minret, uint32_t ptrace, uint32_t move,
                                          const uint32_t (&cnt)[NQ], const uint32_t (&d)[NQ]) {
   const int lane = (int)(threadIdx.x & 63);
   if (rleft == 0) {
@@ -430,7 +431,7 @@ __device__ __forceinline__ void lv_stage(const LvParams& p, uint32_t st, uint32_
   if (lane == 0) {
     o->tail = s.tail; o->hash = s.hash; o->fp = fp; o->tok = s.tok;
     o->minret = minret; o->ptrace = ptrace; o->move = move;
-    o->trace = TRACE_NONE; o->slot = LV_NONE;
+    o->trace = TRACE_NONE; o->slot = LV_NONE; o->chx = chx;
   }
 #pragma unroll
   for (int q = 0; q < NQ; ++q) o->cnt[lane + 64 * q] = (uint16_t)(cnt[q] + d[q]);
@@ -548,9 +549,9 @@ __device__ __forceinline__ void lv_store_cnt_wt(uint16_t* dst, const uint32_t (&
 // CAS, and on a tag hit a wave-parallel compare against the resident entry).
 template <int NQ>
 __device__ __forceinline__ void lv_stage_insert(const LvParams& p, const LvRoundIn& in, uint32_t st, uint32_t& rk,
-                                                uint32_t& rleft, const State& s, uint64_t fp, uint32_t minret,
-                                                uint32_t ptrace, uint32_t move, const uint32_t (&cnt)[NQ],
-                                                const uint32_t (&d)[NQ]) {
+                                                uint32_t& rleft, const State& s, uint64_t fp, uint64_t chx,
+                                                uint32_t minret, uint32_t ptrace, uint32_t move,
+                                                const uint32_t (&cnt)[NQ], const uint32_t (&d)[NQ]) {
   const int lane = (int)(threadIdx.x & 63);
   if (rleft == 0) {
     uint32_t b = 0;
@@ -608,6 +609,7 @@ __device__ __forceinline__ void lv_stage_insert(const LvParams& p, const LvRound
                              : lane == 3 ? ((unsigned long long)minret << 32 | s.tok)
                              : lane == 4 ? ((unsigned long long)move << 32 | ptrace)
                              : lane == 5 ? ((unsigned long long)slot << 32 | tr)
+                             : lane == 6 ? chx
                                          : 0ull;
   if (lane < 16) st_wt64(reinterpret_cast<unsigned long long*>(o) + lane, w);
   lv_store_cnt_wt<NQ>(o->cnt, cnt, d);
@@ -743,7 +745,7 @@ __device__ __forceinline__ void wave_min2_hot32(const LvHot (&H)[NQ], uint32_t& 
 // Write one surviving solo child into staging slot k of round r (header line,
 // counters, next-frontier index, trace entry): the form lv_stage_insert leaves.
 template <int NQ>
-__device__ __forceinline__ void lv_solo_put(const LvParams& p, uint32_t k, const State& s, uint64_t fp,
+__device__ __forceinline__ void lv_solo_put(const LvParams& p, uint32_t k, const State& s, uint64_t fp, uint64_t chx,
                                             uint32_t minret, uint32_t ptrace, uint32_t move, uint32_t tbase,
                                             uint32_t wit, const uint32_t (&cnt)[NQ], const uint32_t (&d)[NQ]) {
   const int lane = (int)(threadIdx.x & 63);
@@ -755,6 +757,7 @@ __device__ __forceinline__ void lv_solo_put(const LvParams& p, uint32_t k, const
                              : lane == 3 ? ((unsigned long long)minret << 32 | s.tok)
                              : lane == 4 ? ((unsigned long long)move << 32 | ptrace)
                              : lane == 5 ? ((unsigned long long)LV_NONE << 32 | tr)
+                             : lane == 6 ? chx
                                          : 0ull;
   if (lane < 16) st_wt64(reinterpret_cast<unsigned long long*>(o) + lane, w);
   lv_store_cnt_wt<NQ>(o->cnt, cnt, d);
@@ -840,12 +843,12 @@ __device__ __forceinline__ bool lv_expand(const LvParams& p, const LvRoundIn& in
           H[q] = lv_hot_null();
           PL.fl[q][lane] = OPF_SENTINEL; PL.call[q][lane] = EV_INF; PL.ret[q][lane] = EV_INF; PL.suf[q][lane] = REQ_NONE;
         }
-        if (j < K) chx ^= lv_chain_term(j, cnt[q]);
+        if (j < K && !pc) chx ^= lv_chain_term(j, cnt[q]);  // (round 0; a staged parent carries it)
       }
       // candidate moves: minimal durable / indefinite appends at the chain heads
       if (has_parent && !(H[q].fl & (OPF_SENTINEL | OPF_CLS_E)) && H[q].call < pmin) cand |= 1u << q;
     }
-    const uint64_t parent_chx = SOLO ? sol->chx : wave_xor_u64(chx);
+    const uint64_t parent_chx = SOLO ? sol->chx : pc ? pc->chx : wave_xor_u64(chx);
     LV_LAP(1);
     // candidate moves in (slot, lane) order; this slice takes moves [c0, c1)
     uint32_t n_cand = 0, my_idx[NQ];
@@ -1101,7 +1104,7 @@ __device__ __forceinline__ bool lv_expand(const LvParams& p, const LvRoundIn& in
                 sol->kchx = cdx; sol->kmr = mr; sol->kmv = mv;
               }
             } else if (k < p.scs) {
-              lv_solo_put<NQ>(p, k, cs_, fp, mr, ptrace, mv, in.tbase, in.wit, cnt, d);
+              lv_solo_put<NQ>(p, k, cs_, fp, cdx, mr, ptrace, mv, in.tbase, in.wit, cnt, d);
             } else if (lane == 0) {
               sol->c[in.par].ovf = 1u;
             }
@@ -1109,9 +1112,9 @@ __device__ __forceinline__ bool lv_expand(const LvParams& p, const LvRoundIn& in
             if (lane == 0) atomicAdd(&sol->pc[3], clock64() - ts0_);
 #endif
           } else if (FUSED) {
-            lv_stage_insert<NQ>(p, in, stripe, rk, rleft, cs_, fp, mr, ptrace, mv, cnt, d);
+            lv_stage_insert<NQ>(p, in, stripe, rk, rleft, cs_, fp, cdx, mr, ptrace, mv, cnt, d);
           } else {
-            lv_stage<NQ>(p, stripe, rk, rleft, cs_, fp, mr, ptrace, mv, cnt, d);
+            lv_stage<NQ>(p, stripe, rk, rleft, cs_, fp, cdx, mr, ptrace, mv, cnt, d);
           }
         }
         // back to the parent's heads on the chains this child advanced
@@ -1500,6 +1503,7 @@ __device__ void lv_solo_write(const LvSolo<NQ>& S, bool child, uint8_t* stg, uin
                                : l == 3 ? ((unsigned long long)mr << 32 | tok)
                                : l == 4 ? ((unsigned long long)(child ? S.kmv : LV_NONE) << 32 | (child ? S.ptrace : TRACE_NONE))
                                : l == 5 ? ((unsigned long long)LV_NONE << 32 | trace_id)
+                               : l == 6 ? (child ? S.kchx : S.chx)
                                         : 0ull;
     st_wt64(reinterpret_cast<unsigned long long*>(o) + l, w);
   }
