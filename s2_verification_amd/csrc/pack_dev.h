@@ -279,6 +279,10 @@ __global__ __launch_bounds__(PACK_BLOCK, S2LC_PACK_MINW) void pack_kernel(Params
   // wave run in lockstep (every round costs the wave the most any of its
   // groups spends), so fewer histories per wave shorten every round, at the
   // price of fewer histories in flight (the host picks gpw from the batch)
+  if (p.zero_ctr && blockIdx.x == 0 && threadIdx.x < 32) {  // the next run's counters (this run uses the other set)
+    p.zero_ctr[threadIdx.x] = 0;
+    p.zero_agg[threadIdx.x] = 0;
+  }
   if (p.gpw && (uint32_t)(lane / L) >= p.gpw) return;
   uint32_t tbase = 0, tleft = 0;  // group's trace chunk (uniform)
   // this group's totals (lane gl == 0), added to p.agg once at the end

@@ -142,7 +142,9 @@ struct DevBatch {
   std::vector<uint32_t> lpt;        // searchable histories, longest (n_ops x K) first
   std::vector<uint64_t> h_in_bytes; // per history: input SoA bytes (48 per op + 8 per record hash)
   LevelBufs lv;
-  uint32_t* counter = nullptr;      // work counters (scheduling) + the run's deadline (u64 at [16])
+  uint32_t* counter = nullptr;      // 2 x 32: work counters (scheduling) + the run's deadline (u64 at [16]) +
+                                    // trace head ([24]), one set per run parity
+  uint32_t run_par = 0;             // the next run's counter set
   TraceEnt* trace = nullptr;
   unsigned long long* trace_head = nullptr;
   uint64_t trace_cap = 0;

@@ -371,9 +371,25 @@ int batch_run(DevBatch& b, hipStream_t stream, const RunOpts& ro, RunStats& st, 
   (void)hipDeviceGetAttribute(&n_cu, hipDeviceAttributeMultiprocessorCount, dev);
   b.rc_valid = false;
 
-  // [0..15] work counters, [16..17] deadline, [24..25] trace head (one memset clears them)
-  if (!b.counter) HIPCHK(hipMalloc(&b.counter, 32 * sizeof(uint32_t)));
-  b.trace_head = reinterpret_cast<unsigned long long*>(b.counter + 24);
+  // Counters, by run parity: [0..15] work counters, [16..17] deadline,
+  // [24..25] trace head; the packed totals likewise. A run zeroes the other
+  // parity's set for the next run: in the reset dispatch, or (a batch every
+  // history of which the packed kernels settle) in the first packed launch,
+  // so that such a run needs no dispatch before its search.
+  if (!b.counter) {
+    HIPCHK(hipMalloc(&b.counter, 64 * sizeof(uint32_t)));
+    HIPCHK(hipMemset(b.counter, 0, 64 * sizeof(uint32_t)));
+  }
+  if (!b.agg) {
+    HIPCHK(hipMalloc(&b.agg, 64 * sizeof(unsigned long long)));
+    HIPCHK(hipMemset(b.agg, 0, 64 * sizeof(unsigned long long)));
+    HIPCHK(hipHostMalloc(&b.h_agg, 32 * sizeof(unsigned long long), hipHostMallocDefault));
+  }
+  const uint32_t par = b.run_par;
+  b.run_par ^= 1u;
+  uint32_t* const ctr = b.counter + 32 * par;
+  unsigned long long* const agg = b.agg + 32 * par;
+  b.trace_head = reinterpret_cast<unsigned long long*>(ctr + 24);
   for (hipEvent_t& e : b.ev)
     if (!e) HIPCHK(hipEventCreate(&e));
   // trace pool: generous, allocated once per batch and reused across runs
@@ -404,21 +420,27 @@ int batch_run(DevBatch& b, hipStream_t stream, const RunOpts& ro, RunStats& st, 
   prm.n_recs = b.n_recs; prm.n_pool = b.n_pool; prm.n_res = b.n_hist;
   prm.rcounts = ro.round_counts ? b.rcounts : nullptr;
 
-  // one dispatch resets the results and zeroes the work counters
-  if (!b.agg) {
-    HIPCHK(hipMalloc(&b.agg, 32 * sizeof(unsigned long long)));
-    HIPCHK(hipHostMalloc(&b.h_agg, 32 * sizeof(unsigned long long), hipHostMallocDefault));
-  }
   b.h_res_stale = false;
-  hipLaunchKernelGGL(reset_results_kernel, dim3(std::max<uint32_t>(1, (b.n_hist + 255) / 256)), dim3(256), 0, stream,
-                     b.res, b.n_hist, b.counter, b.agg);
-  HIPCHK(hipGetLastError());
+  // Every history settled by the packed kernels (they write all of their
+  // results) or fixed on the host: no reset dispatch; the first packed launch
+  // zeroes the next run's counters. Otherwise one dispatch resets the
+  // results and zeroes both counter sets.
+  uint32_t n_forced = 0;
+  for (uint32_t i = 0; i < b.n_hist; ++i) n_forced += b.forced[i] ? 1u : 0u;
+  const uint32_t n_packed_all = b.n_pack8 + b.n_pack16 + b.n_pack32;
+  const bool no_reset = engine == S2LC_ENGINE_AUTO && b.lit_desc.empty() && !ro.round_counts && !deadline_ns &&
+                        n_packed_all > 0 && n_packed_all + n_forced == b.n_hist && !getenv("S2LC_RESET_ALWAYS");
+  if (!no_reset) {
+    hipLaunchKernelGGL(reset_results_kernel, dim3(std::max<uint32_t>(1, (b.n_hist + 255) / 256)), dim3(256), 0,
+                       stream, b.res, b.n_hist, b.counter, b.agg);
+    HIPCHK(hipGetLastError());
+  }
   if (deadline_ns) {
     int rate_khz = 100000;  // device wall clock (s_memrealtime); 100 MHz on gfx950
     (void)hipDeviceGetAttribute(&rate_khz, hipDeviceAttributeWallClockRate, dev);
     const int64_t left_ns = std::max<int64_t>(0, deadline_ns - steady_ns());
     const unsigned long long ticks = (unsigned long long)((double)left_ns * 1e-6 * rate_khz);
-    unsigned long long* d = reinterpret_cast<unsigned long long*>(b.counter + 16);
+    unsigned long long* d = reinterpret_cast<unsigned long long*>(ctr + 16);
     hipLaunchKernelGGL(deadline_kernel, dim3(1), dim3(1), 0, stream, d, std::max<unsigned long long>(ticks, 1));
     HIPCHK(hipGetLastError());
     prm.deadline = d;
@@ -476,8 +498,11 @@ int batch_run(DevBatch& b, hipStream_t stream, const RunOpts& ro, RunStats& st, 
       Params pp = prm;
       pp.order = b.order + first[li];
       pp.n_hist = n_l;
-      pp.counter = b.counter + 12 + li;
-      pp.agg = b.agg + 8 * li;
+      pp.counter = ctr + 12 + li;
+      pp.agg = agg + 8 * li;
+      const bool first_launch = !(launched[0] || launched[1] || launched[2]);
+      pp.zero_ctr = no_reset && first_launch ? b.counter + 32 * (par ^ 1u) : nullptr;
+      pp.zero_agg = no_reset && first_launch ? b.agg + 32 * (par ^ 1u) : nullptr;
       const uint32_t L = 8u << li;
       const size_t smem = li == 0 ? pack_smem_bytes<8>() : li == 1 ? pack_smem_bytes<16>() : pack_smem_bytes<32>();
       int bpc = b.pack_bpc[li];  // resident blocks per CU (queried once per batch)
@@ -486,6 +511,7 @@ int batch_run(DevBatch& b, hipStream_t stream, const RunOpts& ro, RunStats& st, 
         else if (li == 1) HIPCHK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&bpc, pack_kernel<16>, PACK_BLOCK, smem));
         else HIPCHK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&bpc, pack_kernel<32>, PACK_BLOCK, smem));
         bpc = std::max(1, bpc);
+        if (const char* e = getenv("S2LC_PACK_BPC")) bpc = std::max(1, atoi(e));  // (diagnostics: grid blocks per CU)
         b.pack_bpc[li] = bpc;
       }
       // lane groups per wave that take histories: the fewest (1, 2, 4, ...)
@@ -520,12 +546,10 @@ int batch_run(DevBatch& b, hipStream_t stream, const RunOpts& ro, RunStats& st, 
     // totals; the per-history results stay on the device until asked for
     // (batch_host_results). A history that outgrew its packed frontier sends
     // the run down the full path (results read back, overflow scan).
-    uint32_t n_forced = 0;
-    for (uint32_t i = 0; i < b.n_hist; ++i) n_forced += b.forced[i] ? 1u : 0u;
     const bool fast = todo.empty() && level.empty() && !ro.round_counts && b.lit_desc.empty() &&
                       n_packed + n_forced == b.n_hist;
     if (fast)
-      HIPCHK(hipMemcpyAsync(b.h_agg, b.agg, 24 * sizeof(unsigned long long), hipMemcpyDeviceToHost, stream));
+      HIPCHK(hipMemcpyAsync(b.h_agg, agg, 24 * sizeof(unsigned long long), hipMemcpyDeviceToHost, stream));
     else
       HIPCHK(hipMemcpyAsync(b.h_res, b.res, b.n_hist * sizeof(HistResult), hipMemcpyDeviceToHost, stream));
     t_enq = steady_ns();
@@ -564,8 +588,9 @@ int batch_run(DevBatch& b, hipStream_t stream, const RunOpts& ro, RunStats& st, 
       const int64_t t_end = steady_ns();
       st.total_ms = (double)(t_end - t0) * 1e-6;
       if (step_timing)
-        fprintf(stderr, "[s2lc step] enqueue %.1f us, wait %.1f us (kernel %.1f us), after %.1f us (totals only)\n",
-                1e-3 * (t_enq - t0), 1e-3 * (t_wait - t_enq), 1e3 * st.pack_ms, 1e-3 * (t_end - t_wait));
+        fprintf(stderr, "[s2lc step] enqueue %.1f us, wait %.1f us (kernel %.1f us), after %.1f us (totals only); "
+                "pack16 blocks/CU %d\n",
+                1e-3 * (t_enq - t0), 1e-3 * (t_wait - t_enq), 1e3 * st.pack_ms, 1e-3 * (t_end - t_wait), b.pack_bpc[1]);
       return 0;
     }
     if (fast)  // a packed frontier overflowed: the full path needs every result
@@ -623,7 +648,7 @@ int batch_run(DevBatch& b, hipStream_t stream, const RunOpts& ro, RunStats& st, 
     HIPCHK(hipMemcpyAsync(b.list, todo.data(), todo.size() * sizeof(uint32_t), hipMemcpyHostToDevice, stream));
     pp.order = b.list;
     pp.n_hist = n_pass;
-    pp.counter = b.counter + 4 * pass;
+    pp.counter = ctr + 4 * pass;
     pp.slab = b.slab;
     pp.slab_bytes = g.slab_bytes;
     pp.fcap = g.fcap; pp.chunk = g.chunk; pp.stage_cap = g.stage_cap; pp.ht_mask = g.ht_slots - 1;

@@ -105,6 +105,8 @@ struct Params {
   const unsigned long long* deadline;  // wall_clock64() value after which histories give Unknown (nullable)
   uint32_t gpw;                    // pack kernels: lane groups per wave that take histories (0 = all)
   unsigned long long* agg;         // pack kernels: this launch's totals (PACK_AGG_*; nullable)
+  uint32_t* zero_ctr;              // (nullable) the next run's counter set (32 words) and
+  unsigned long long* zero_agg;    // totals (32), zeroed by block 0: no reset dispatch before it
 };
 
 // The run's deadline in device wall-clock ticks (written once per run, read by
@@ -116,8 +118,8 @@ __global__ __attribute__((unused)) void deadline_kernel(unsigned long long* d, u
 __global__ __attribute__((unused)) void reset_results_kernel(HistResult* res, uint32_t n, uint32_t* counter,
                                                              unsigned long long* agg) {
   const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
-  if (counter && i < 32) counter[i] = 0;  // work counters, deadline, trace head
-  if (agg && i < 32) agg[i] = 0;          // packed launches' totals
+  if (counter && i < 64) counter[i] = 0;  // both sets: work counters, deadline, trace head
+  if (agg && i < 64) agg[i] = 0;          // both sets: packed launches' totals
   if (i >= n) return;
   HistResult& r = res[i];
   r.verdict = V_UNKNOWN;
