@@ -181,6 +181,7 @@ static int lv_tables(LevelBufs& L, uint64_t scap, std::string& err) {
   for (int i = 0; i < 2; ++i)
     if (lv_ensure((void**)&L.ht[i], L.ht_bytes[i], ht * 8, err)) return S2LC_EHIP;
   for (int i = 0; i < 2; ++i) LVCHK(hipMemset(L.ht[i], 0xFF, ht * 8));
+  LVCHK(hipStreamSynchronize(nullptr));  // (the null stream does not order the search's non-blocking one)
   L.ht_mask = (uint32_t)(ht - 1);
   return 0;
 }
@@ -323,6 +324,7 @@ int level_search(DevBatch& b, uint32_t h, hipStream_t st, const RunOpts& ro, int
   unsigned long long* d_prof = nullptr;
   LVCHK(hipMalloc(&d_prof, 32 * sizeof(unsigned long long)));
   LVCHK(hipMemset(d_prof, 0, 32 * sizeof(unsigned long long)));
+  LVCHK(hipStreamSynchronize(nullptr));
   p.prof = d_prof;
 #endif
   LVCHK(hipEventRecord(L.ev[0], st));

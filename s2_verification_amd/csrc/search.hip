@@ -378,11 +378,12 @@ int batch_run(DevBatch& b, hipStream_t stream, const RunOpts& ro, RunStats& st, 
   // so that such a run needs no dispatch before its search.
   if (!b.counter) {
     HIPCHK(hipMalloc(&b.counter, 64 * sizeof(uint32_t)));
-    HIPCHK(hipMemset(b.counter, 0, 64 * sizeof(uint32_t)));
+    HIPCHK(hipMemsetAsync(b.counter, 0, 64 * sizeof(uint32_t), stream));  // (on the stream: the
+    // null stream does not order a non-blocking one, and a run that needs no reset dispatch reads these first)
   }
   if (!b.agg) {
     HIPCHK(hipMalloc(&b.agg, 64 * sizeof(unsigned long long)));
-    HIPCHK(hipMemset(b.agg, 0, 64 * sizeof(unsigned long long)));
+    HIPCHK(hipMemsetAsync(b.agg, 0, 64 * sizeof(unsigned long long), stream));
     HIPCHK(hipHostMalloc(&b.h_agg, 32 * sizeof(unsigned long long), hipHostMallocDefault));
   }
   const uint32_t par = b.run_par;
