@@ -655,10 +655,11 @@ int load_jsonl(const uint8_t* buf, size_t len, History& h, std::string& err) {
   {
     // size the event / hash arrays once (a record per line in the collector's
     // output): growing them record by record re-maps large blocks, which
-    // serialises parallel decoders on the process's address-space lock
-    size_t lines = 0;
-    for (const uint8_t* q = buf; (q = (const uint8_t*)memchr(q, '\n', (size_t)(buf + len - q))) != nullptr; ++q) ++lines;
-    h.events.reserve(h.events.size() + lines + 1);
+    // serialises parallel decoders on the process's address-space lock. The
+    // bound is the shortest record's length (a Finish without a value, ~60
+    // bytes): counting the lines instead cost a quarter of the decode
+    // (memchr per ~107-byte record), and untouched capacity is never faulted in.
+    h.events.reserve(h.events.size() + len / 56 + 16);
     h.pool.reserve(h.pool.size() + len / 24);
   }
   while (true) {
