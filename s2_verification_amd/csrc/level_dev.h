@@ -464,24 +464,27 @@ __device__ __forceinline__ void lv_release(const LvParams& p, uint32_t st, uint3
 // cnt[q] for a wave-uniform runtime slot q (a select chain, no scratch)
 template <int NQ>
 __device__ __forceinline__ uint32_t sel_cnt(const uint32_t (&cnt)[NQ], uint32_t q) {
-  uint32_t v = cnt[0];
+  // (masks, not a select chain: the compiler turned that back into an
+  // indexed private array, i.e. a scratch store per update and a scratch
+  // load per move on the round's critical path)
+  uint32_t v = 0;
 #pragma unroll
-  for (int i = 1; i < NQ; ++i) v = q == (uint32_t)i ? cnt[i] : v;
+  for (int i = 0; i < NQ; ++i) v |= cnt[i] & (0u - (uint32_t)(q == (uint32_t)i));
   return v;
 }
 
 template <int N>
 __device__ __forceinline__ uint32_t sel_u32(const uint32_t (&a)[N], uint32_t q) {
-  uint32_t v = a[0];
+  uint32_t v = 0;
 #pragma unroll
-  for (int i = 1; i < N; ++i) v = q == (uint32_t)i ? a[i] : v;
+  for (int i = 0; i < N; ++i) v |= a[i] & (0u - (uint32_t)(q == (uint32_t)i));
   return v;
 }
 template <int N>
 __device__ __forceinline__ uint64_t sel_u64(const uint64_t (&a)[N], uint32_t q) {
-  uint64_t v = a[0];
+  uint64_t v = 0;
 #pragma unroll
-  for (int i = 1; i < N; ++i) v = q == (uint32_t)i ? a[i] : v;
+  for (int i = 0; i < N; ++i) v |= a[i] & (0ull - (uint64_t)(q == (uint32_t)i));
   return v;
 }
 
@@ -1087,7 +1090,8 @@ __device__ __forceinline__ bool lv_expand(const LvParams& p, const LvRoundIn& in
             if (d[q]) dx ^= lv_chain_term(jj, cnt[q]) ^ lv_chain_term(jj, cnt[q] + d[q]);
           }
           const uint64_t cdx = parent_chx ^ wave_xor_u64(dx);
-          const uint64_t fp = mix64(cdx ^ lv_state_term(cs_.tail, cs_.hash, cs_.tok));
+          // (a solo round's first survivor is kept in LDS without it)
+          auto fp_of = [&]() { return mix64(cdx ^ lv_state_term(cs_.tail, cs_.hash, cs_.tok)); };
           if (SOLO) {
             // distinct children: staging slot = arrival order; the first one is
             // kept in LDS in case it turns out to be the round's only survivor
@@ -1104,7 +1108,7 @@ __device__ __forceinline__ bool lv_expand(const LvParams& p, const LvRoundIn& in
                 sol->kchx = cdx; sol->kmr = mr; sol->kmv = mv;
               }
             } else if (k < p.scs) {
-              lv_solo_put<NQ>(p, k, cs_, fp, cdx, mr, ptrace, mv, in.tbase, in.wit, cnt, d);
+              lv_solo_put<NQ>(p, k, cs_, fp_of(), cdx, mr, ptrace, mv, in.tbase, in.wit, cnt, d);
             } else if (lane == 0) {
               sol->c[in.par].ovf = 1u;
             }
@@ -1112,9 +1116,9 @@ __device__ __forceinline__ bool lv_expand(const LvParams& p, const LvRoundIn& in
             if (lane == 0) atomicAdd(&sol->pc[3], clock64() - ts0_);
 #endif
           } else if (FUSED) {
-            lv_stage_insert<NQ>(p, in, stripe, rk, rleft, cs_, fp, cdx, mr, ptrace, mv, cnt, d);
+            lv_stage_insert<NQ>(p, in, stripe, rk, rleft, cs_, fp_of(), cdx, mr, ptrace, mv, cnt, d);
           } else {
-            lv_stage<NQ>(p, stripe, rk, rleft, cs_, fp, cdx, mr, ptrace, mv, cnt, d);
+            lv_stage<NQ>(p, stripe, rk, rleft, cs_, fp_of(), cdx, mr, ptrace, mv, cnt, d);
           }
         }
         // back to the parent's heads on the chains this child advanced
@@ -1659,7 +1663,7 @@ __device__ void lv_solo_rounds(const LvParams& p, const LvPersist& q, LvRun& R, 
 }
 
 template <int NQ>
-__global__ __launch_bounds__(LV_BLOCK) void lv_persist(LvParams p, LvPersist q) {
+__global__ __launch_bounds__(LV_BLOCK, 2) void lv_persist(LvParams p, LvPersist q) {
   // solo rounds use s_heads[0] (the configuration's heads), s_heads[1] (the
   // moves' next heads) and s_heads[2..3] as the move records (LvSoloExt)
   __shared__ __attribute__((aligned(16))) LvHeadsLds<NQ> s_heads[LV_BLOCK / 64];
