@@ -22,6 +22,21 @@ def lv_total(stats, counter):
                for k, cs in stats.items() if k.startswith("lv_"))
 
 
+def per_kernel(fetch, write, atom):
+    """Each lv_ kernel's counters from all three passes, per search (MiB for
+    the sizes; the gfx950 FETCH_SIZE correction applied)."""
+    out = {}
+    for k in sorted(set(fetch) | set(write) | set(atom)):
+        if not k.startswith("lv_"):
+            continue
+        f, w, a = fetch.get(k, {}), write.get(k, {}), atom.get(k, {})
+        out[k] = {"dispatches": f.get("dispatches", w.get("dispatches", a.get("dispatches", 0))),
+                  "fetch_MiB_per_search": round(2 * f.get("FETCH_SIZE", 0.0) * f.get("dispatches", 0) / 1024 / SEARCHES, 1),
+                  "write_MiB_per_search": round(w.get("WRITE_SIZE", 0.0) * w.get("dispatches", 0) / 1024 / SEARCHES, 1),
+                  "atomics_per_search": round(a.get("TCC_EA0_ATOMIC_total", 0.0) / SEARCHES, 1)}
+    return out
+
+
 def main():
     root = sys.argv[1]
     fetch = load(os.path.join(root, "c5_fetch"))
@@ -37,8 +52,7 @@ def main():
         "hbm_bytes_per_search": round((2 * fb + wb) * 1024 / SEARCHES, 1),
         "tcc_ea_atomics_per_search": round(lv_total(atom, "TCC_EA0_ATOMIC") / SEARCHES, 1),
         "tcc_atomics_per_search": round(lv_total(atom, "TCC_ATOMIC") / SEARCHES, 1),
-        "per_kernel": {k: {c: v for c, v in cs.items()} for k, cs in {**fetch, **write, **atom}.items()
-                       if k.startswith("lv_")},
+        "per_kernel": per_kernel(fetch, write, atom),
         "source": "rocprofv3 --pmc passes (profiles/collect_pmc.sh: c5_fetch FETCH_SIZE TCC_ATOMIC, "
                   "c5_write WRITE_SIZE TCC_ATOMIC, c5_atomic TCC_ATOMIC TCC_EA0_ATOMIC)",
     }

@@ -1,0 +1,70 @@
+"""CPU: the gfx950 code objects inside libs2lincheck.so, read back from their
+metadata notes (no GPU). The search kernels must keep their working state in
+registers: a private (scratch) segment on a hot kernel means the compiler
+spilled an array to memory, as the level search's move selection did until
+round 3 (5.7 GB of scratch writes per C5 search)."""
+import os
+import re
+import subprocess
+import tempfile
+
+import pytest
+
+import s2_verification_amd as s2
+
+LLVM = "/opt/rocm/lib/llvm/bin"
+MAGIC = b"__CLANG_OFFLOAD_BUNDLE__"
+TARGET = "hipv4-amdgcn-amd-amdhsa--gfx950"
+
+
+def kernel_metadata():
+    """{kernel name: {'scratch': bytes per lane, 'vgpr': count}} over every
+    offload bundle in the library's .hip_fatbin section."""
+    tools = [os.path.join(LLVM, t) for t in ("llvm-objcopy", "clang-offload-bundler", "llvm-readelf")]
+    if not all(os.path.exists(t) for t in tools):
+        pytest.skip("ROCm LLVM tools not found")
+    objcopy, bundler, readelf = tools
+    out = {}
+    with tempfile.TemporaryDirectory() as d:
+        fat = os.path.join(d, "fatbin")
+        subprocess.run([objcopy, "--dump-section=.hip_fatbin=" + fat, s2.LIB_PATH, os.path.join(d, "x.so")],
+                       check=True, capture_output=True)
+        data = open(fat, "rb").read()
+        starts = [m.start() for m in re.finditer(re.escape(MAGIC), data)]
+        assert starts, "no offload bundle in .hip_fatbin"
+        for k, a in enumerate(starts):
+            part = os.path.join(d, f"b{k}")
+            with open(part, "wb") as f:
+                f.write(data[a:starts[k + 1] if k + 1 < len(starts) else len(data)])
+            co = os.path.join(d, f"b{k}.co")
+            subprocess.run([bundler, "--unbundle", "--type=o", "--input=" + part, "--targets=" + TARGET,
+                            "--output=" + co], check=True, capture_output=True)
+            notes = subprocess.run([readelf, "--notes", co], check=True, capture_output=True, text=True).stdout
+            name = None
+            for line in notes.splitlines():
+                m = re.match(r"\s*\.name:\s+(\S+)", line)
+                if m:
+                    name = m.group(1)
+                    out.setdefault(name, {})
+                m = re.match(r"\s*\.private_segment_fixed_size:\s+(\d+)", line)
+                if m and name:
+                    out[name]["scratch"] = int(m.group(1))
+                m = re.match(r"\s*\.vgpr_count:\s+(\d+)", line)
+                if m and name:
+                    out[name]["vgpr"] = int(m.group(1))
+    return out
+
+
+def test_search_kernels_use_no_scratch():
+    md = kernel_metadata()
+    hot = {n: v for n, v in md.items()
+           if re.search(r"(pack_kernel|search_kernel|lv_round|lv_insert|lv_persist|literal_kernel)", n)}
+    assert len(hot) >= 30, sorted(hot)
+    for n, v in hot.items():
+        # lv_persist<5> is bounded to 2 waves/SIMD (256 VGPRs); the compiler
+        # spills 2 VGPRs (12 bytes) outside its round loop. lv_insert declares
+        # a 20-byte frame its body never touches (no scratch instruction:
+        # the round close's counters, addressed flat)
+        limit = 16 if "lv_persistILi5E" in n else 20 if "lv_insert" in n else 0
+        assert v.get("scratch", 0) <= limit, (n, v)
+        assert v.get("vgpr", 0) <= 256, (n, v)
