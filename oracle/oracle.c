@@ -180,19 +180,28 @@ static uint64_t bits_hash(const uint64_t* b, int w) { /* bitset.hash: popcnt ^ x
   return h;
 }
 
-static void lift(node* e) {
+/* lift / unlift as porcupine writes them: the call's next node is
+ * dereferenced unconditionally (entry.next.prev = ...), the return's only when
+ * non-nil. With two calls sharing one return, a call can end up last in the
+ * list; porcupine then panics on the nil dereference, which is returned here
+ * as -1 (the caller maps it to OR_PANIC) instead of dereferencing NULL. */
+static int lift(node* e) {
+  if (!e->next) return -1;
   e->prev->next = e->next;
   e->next->prev = e->prev;
   node* m = e->match;
   m->prev->next = m->next;
   if (m->next) m->next->prev = m->prev;
+  return 0;
 }
-static void unlift(node* e) {
+static int unlift(node* e) {
   node* m = e->match;
   m->prev->next = m;
   if (m->next) m->next->prev = m;
   e->prev->next = e;
+  if (!e->next) return -1;
   e->next->prev = e;
+  return 0;
 }
 
 typedef struct callsent { node* entry; sset st; } callsent;
@@ -309,7 +318,7 @@ static int check_wgl_impl(const or_event* ev, size_t n_ev, int compute_partial, 
           calls[ncalls].entry = entry; calls[ncalls].st = state; ncalls++;
           state = ns;
           lin[entry->id / 64] |= 1ULL << (entry->id % 64);
-          lift(entry);
+          if (lift(entry) < 0) { result = OR_PANIC; break; }
           entry = head->next;
           if (max_entries && local.cache_inserts > max_entries) { result = OR_UNKNOWN; break; }
         } else {
@@ -342,7 +351,7 @@ static int check_wgl_impl(const or_event* ev, size_t n_ev, int compute_partial, 
       entry = top.entry;
       state = top.st;
       lin[entry->id / 64] &= ~(1ULL << (entry->id % 64));
-      unlift(entry);
+      if (unlift(entry) < 0) { result = OR_PANIC; break; }
       entry = entry->next;
     }
   }

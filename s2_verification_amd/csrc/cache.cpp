@@ -71,6 +71,10 @@ void event_pair(const History& h, uint32_t d, int64_t c_client, int64_t r_client
   r.stream_hash = o.out_hash;
 }
 
+// [off, off + cnt) inside a pool of n entries, without the u64 sum (a
+// crafted image could make off + cnt wrap past n)
+bool pool_range_ok(uint64_t off, uint64_t cnt, uint64_t n) { return cnt <= n && off <= n - cnt; }
+
 bool event_eq(const Event& a, const Event& b) {  // field by field (padding bytes are not data)
   return a.kind == b.kind && a.op_id == b.op_id && a.client_id == b.client_id && a.input_type == b.input_type &&
          a.has_num_records == b.has_num_records && a.has_msn == b.has_msn && a.num_records == b.num_records &&
@@ -210,7 +214,7 @@ bool read_section(const uint8_t* p, const uint8_t* end, History& h) {
     // a duplicate-id history (History::literal): no chains; its porcupine
     // linking is rebuilt from the events by finalize, which must agree
     for (const Event& e : h.events)
-      if (e.hash_off + e.hash_cnt > hd.n_pool || e.set_tok > hd.n_tokens || e.batch_tok > hd.n_tokens) return false;
+      if (!pool_range_ok(e.hash_off, e.hash_cnt, hd.n_pool) || e.set_tok > hd.n_tokens || e.batch_tok > hd.n_tokens) return false;
     const uint32_t n_ops = hd.n_ops;
     const std::vector<int64_t> ids = h.op_ids;
     if (h.finalize() != 0 || !h.literal || h.n_ops != n_ops || h.op_ids != ids) return false;
@@ -221,7 +225,7 @@ bool read_section(const uint8_t* p, const uint8_t* end, History& h) {
     // refused); only what the event API reads must be in range
     if (hd.mode != 1 || hd.n_cs || hd.n_recs) return false;
     for (const Event& e : h.events)
-      if (e.hash_off + e.hash_cnt > hd.n_pool || e.set_tok > hd.n_tokens || e.batch_tok > hd.n_tokens) return false;
+      if (!pool_range_ok(e.hash_off, e.hash_cnt, hd.n_pool) || e.set_tok > hd.n_tokens || e.batch_tok > hd.n_tokens) return false;
     return true;
   }
   // the index arrays must stay inside the tables they index (the checker
@@ -242,7 +246,7 @@ bool read_section(const uint8_t* p, const uint8_t* end, History& h) {
   for (const OpRec& o : h.recs) n_e += (!(o.flags & OPF_SENTINEL) && (o.flags & OPF_CLS_E)) ? 1u : 0u;
   if (n_e != hd.n_ident) return false;
   for (const OpRec& o : h.recs)
-    if ((uint64_t)o.hash_off + o.hash_cnt > hd.n_pool || o.set_tok > hd.n_tokens || o.batch_tok > hd.n_tokens ||
+    if (!pool_range_ok(o.hash_off, o.hash_cnt, hd.n_pool) || o.set_tok > hd.n_tokens || o.batch_tok > hd.n_tokens ||
         (!(o.flags & OPF_SENTINEL) && (o.call_ev >= hd.n_events || o.ret_ev >= hd.n_events)))
       return false;
   std::vector<uint32_t> orec(hd.n_ops, UINT32_MAX);
@@ -285,7 +289,18 @@ bool read_section(const uint8_t* p, const uint8_t* end, History& h) {
     h.lazy_once = std::make_unique<std::once_flag>();
   } else {
     for (const Event& e : h.events)
-      if (e.hash_off + e.hash_cnt > hd.n_pool || e.set_tok > hd.n_tokens || e.batch_tok > hd.n_tokens) return false;
+      if (!pool_range_ok(e.hash_off, e.hash_cnt, hd.n_pool) || e.set_tok > hd.n_tokens || e.batch_tok > hd.n_tokens) return false;
+    // the searched records must be the events' own (rec_of): witness
+    // certification replays the record table, so a section whose records and
+    // events disagree would certify a history other than the one the event
+    // API shows. Every field but sufmin (the chain's P1 bound).
+    for (uint32_t d = 0; d < hd.n_ops; ++d) {
+      const OpRec a = h.rec_of(d), &b = h.recs[h.op_rec[d]];
+      if (a.num_records != b.num_records || a.msn != b.msn || a.out_tail != b.out_tail || a.out_hash != b.out_hash ||
+          a.call_ev != b.call_ev || a.ret_ev != b.ret_ev || a.hash_off != b.hash_off || a.hash_cnt != b.hash_cnt ||
+          a.batch_tok != b.batch_tok || a.set_tok != b.set_tok || a.flags != b.flags)
+        return false;
+    }
   }
   return true;
 }

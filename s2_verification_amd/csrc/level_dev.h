@@ -298,16 +298,16 @@ struct LvHeadsLds {
   uint32_t call[NQ][64], ret[NQ][64], fl[NQ][64];
 };
 
-// Load the head at rec into LDS slot q and return its hot fields.
+// A parent's head (record bytes 16..47 and its flags, already loaded) into
+// LDS slot q; returns its hot fields.
 template <int NQ>
-__device__ __forceinline__ LvHot lv_load_parent_head(const OpRec* r, LvHeadsLds<NQ>& L, int q, int lane) {
-  const uint4 a = ld16(r, 16);
-  const uint4 b = ld16(r, 32);
+__device__ __forceinline__ LvHot lv_put_parent_head(const uint4& a, const uint4& b, uint32_t fl, LvHeadsLds<NQ>& L,
+                                                    int q, int lane) {
   LvHot h;
   h.suf = (uint64_t)b.x | ((uint64_t)b.y << 32);
   h.call = b.z;
   h.ret = b.w;
-  h.fl = r->flags;
+  h.fl = fl;
   L.otail[q][lane] = (uint64_t)a.x | ((uint64_t)a.y << 32);
   L.ohash[q][lane] = (uint64_t)a.z | ((uint64_t)a.w << 32);
   L.suf[q][lane] = h.suf;
@@ -387,6 +387,37 @@ __device__ __forceinline__ int lv_closure(LvHot (&H)[NQ], uint32_t (&d)[NQ], con
     if (!changed && minret == minret_prev) {
       minret_out = minret;
       return minret == EV_INF ? CL_COMPLETE : ((p4 && bound == REQ_NONE) ? CL_P4 : CL_ALIVE);
+    }
+    if (!NX && NQ <= 5) {
+      // grid rounds (NQ <= 5): every slot's next head loaded at once, unconditionally
+      // (a slot that does not advance reloads its current head, cached), so
+      // the pass waits one memory latency, not one or two per advancing slot
+      uint4 ca[NQ], cb[NQ];
+      uint32_t cf[NQ];
+#pragma unroll
+      for (int q = 0; q < NQ; ++q) {
+        const OpRec* r = recs + s_cs[64 * q + lane] + cnt[q] + d[q] + ((adv >> q) & 1u);
+        ca[q] = ld16(r, 16);
+        cb[q] = ld16(r, 32);
+        cf[q] = r->flags;
+      }
+#pragma unroll
+      for (int q = 0; q < NQ; ++q) {
+        if ((adv >> q) & 1u) {
+          d[q] += 1;
+          H[q].suf = (uint64_t)cb[q].x | ((uint64_t)cb[q].y << 32);
+          H[q].call = cb[q].z;
+          H[q].ret = cb[q].w;
+          H[q].fl = cf[q] | HB_KNOWN |
+                    lv_legal_bits(cf[q], (uint64_t)ca[q].x | ((uint64_t)ca[q].y << 32),
+                                  (uint64_t)ca[q].z | ((uint64_t)ca[q].w << 32), s);
+        }
+      }
+#ifdef S2LC_PROF
+      if (prof) atomicAdd(prof + 1, (unsigned long long)__popc(adv));  // head loads from memory (per lane)
+#endif
+      minret_prev = minret;
+      continue;
     }
 #pragma unroll
     for (int q = 0; q < NQ; ++q) {
@@ -831,6 +862,32 @@ __device__ __forceinline__ bool lv_expand(const LvParams& p, const LvRoundIn& in
     LV_LAP(0);
     uint64_t chx = 0;  // this lane's part of the parent's chain fingerprint
     uint32_t cand = 0;
+    // Grid rounds: every slot's count, then every slot's head record, each
+    // group issued before any is used: one memory latency per group. (Loads
+    // under a per-slot condition were compiled into a wait per slot, two
+    // serialized latencies per slot: ~12.6 k cycles per item for NQ = 5.)
+    // Unconditional loads stay in bounds: a configuration holds 64 * NQ
+    // counts, and a slot past K reads record 0 (s_cs is 0 there).
+    // (NQ <= 5: wider layouts would spill the grouped registers; they load
+    // per slot)
+    constexpr bool HG = !SOLO && NQ <= 5;
+    uint4 ha[HG ? NQ : 1], hb[HG ? NQ : 1];
+    uint32_t hf[HG ? NQ : 1];
+    if (HG) {
+#pragma unroll
+      for (int q = 0; q < NQ; ++q) {
+        const uint32_t j = (uint32_t)lane + 64u * q;
+        const uint32_t c = pc ? (uint32_t)pc->cnt[j] : 0u;
+        cnt[q] = j < K ? c : 0u;
+      }
+#pragma unroll
+      for (int q = 0; q < NQ; ++q) {
+        const OpRec* r = p.recs + s_cs[64 * q + lane] + cnt[q];
+        ha[HG ? q : 0] = ld16(r, 16);
+        hb[HG ? q : 0] = ld16(r, 32);
+        hf[HG ? q : 0] = r->flags;
+      }
+    }
 #pragma unroll
     for (int q = 0; q < NQ; ++q) {
       const uint32_t j = (uint32_t)lane + 64u * q;
@@ -839,9 +896,14 @@ __device__ __forceinline__ bool lv_expand(const LvParams& p, const LvRoundIn& in
         cnt[q] = sol->cnt[j];
         H[q] = lv_parent_hot<NQ>(PL, q, lane);
       } else {
-        cnt[q] = (j < K && pc) ? (uint32_t)pc->cnt[j] : 0u;
+        if (!HG) cnt[q] = (j < K && pc) ? (uint32_t)pc->cnt[j] : 0u;
         if (j < K) {
-          H[q] = lv_load_parent_head<NQ>(p.recs + s_cs[64 * q + lane] + cnt[q], PL, q, lane);
+          if (HG) {
+            H[q] = lv_put_parent_head<NQ>(ha[HG ? q : 0], hb[HG ? q : 0], hf[HG ? q : 0], PL, q, lane);
+          } else {
+            const OpRec* r = p.recs + s_cs[64 * q + lane] + cnt[q];
+            H[q] = lv_put_parent_head<NQ>(ld16(r, 16), ld16(r, 32), r->flags, PL, q, lane);
+          }
         } else {
           H[q] = lv_hot_null();
           PL.fl[q][lane] = OPF_SENTINEL; PL.call[q][lane] = EV_INF; PL.ret[q][lane] = EV_INF; PL.suf[q][lane] = REQ_NONE;
@@ -891,6 +953,25 @@ __device__ __forceinline__ bool lv_expand(const LvParams& p, const LvRoundIn& in
       if (t32) wave_min2_hot32<NQ>(H, b_min32, b_2nd32);
       else wave_min2_hot<NQ>(H, b_min, b_2nd);
     }
+#ifndef S2LC_PRE_GROUP
+#define S2LC_PRE_GROUP 0
+#endif
+    // (S2LC_PRE_GROUP) grid rounds: the rest of every candidate's record and
+    // its next record's P1 bound loaded for all slots before the precheck
+    // uses any (one latency instead of one per slot with a candidate)
+    constexpr bool PG = !SOLO && NQ <= 5 && S2LC_PRE_GROUP;
+    uint4 pm0[PG ? NP : 1], pm3[PG ? NP : 1];
+    uint64_t pns[PG ? NP : 1];
+    if (PG) {
+#pragma unroll
+      for (int q = 0; q < NP; ++q) {
+        const OpRec* hp = p.recs + s_cs[64 * q + lane] + cnt[q];
+        pm0[q] = ld16(hp, 0);
+        pm3[q] = ld16(hp, 48);
+        // (a non-candidate head may be its chain's sentinel: no next record)
+        pns[q] = p1 ? ld_suf(hp + ((cand >> q) & 1u)) : REQ_NONE;
+      }
+    }
 
 #pragma unroll
     for (int q = 0; q < NP; ++q) {
@@ -900,7 +981,7 @@ __device__ __forceinline__ bool lv_expand(const LvParams& p, const LvRoundIn& in
       if (PRE && ((cand >> q) & 1u) && my_idx[q] >= c0 && my_idx[q] < c1) {
         const OpRec* hp = p.recs + s_cs[64 * q + lane] + cnt[q];
         // the chain's next record's P1 bound (solo rounds: in LDS)
-        const uint64_t nx_suf = SOLO ? NX->suf[q][lane] : (p1 ? ld_suf(hp + 1) : REQ_NONE);
+        const uint64_t nx_suf = SOLO ? NX->suf[q][lane] : PG ? pns[PG ? q : 0] : (p1 ? ld_suf(hp + 1) : REQ_NONE);
         // the head: solo rounds keep the heads' whole records in LDS; grid
         // rounds just loaded its hot part (cached)
         OpRec r;
@@ -912,6 +993,15 @@ __device__ __forceinline__ bool lv_expand(const LvParams& p, const LvRoundIn& in
           r.hash_off = m_.hash_off; r.hash_cnt = m_.hash_cnt;
           r.batch_tok = (uint16_t)m_.toks; r.set_tok = (uint16_t)(m_.toks >> 16);
           r.flags = PL.fl[q][lane];
+        } else if (PG) {  // bytes 0..15 and 48..63 just loaded; 16..47 in PL / H
+          const uint4 a0 = pm0[PG ? q : 0], a3 = pm3[PG ? q : 0];
+          r.num_records = (uint64_t)a0.x | ((uint64_t)a0.y << 32);
+          r.msn = (uint64_t)a0.z | ((uint64_t)a0.w << 32);
+          r.out_tail = PL.otail[q][lane]; r.out_hash = PL.ohash[q][lane]; r.sufmin = H[q].suf;
+          r.call_ev = H[q].call; r.ret_ev = H[q].ret;
+          r.hash_off = a3.x; r.hash_cnt = a3.y;
+          r.batch_tok = (uint16_t)a3.z; r.set_tok = (uint16_t)(a3.z >> 16);
+          r.flags = a3.w;
         } else {
           r = load_rec(hp);
         }

@@ -217,10 +217,13 @@ __global__ void literal_kernel(const LitDesc* __restrict__ descs, uint32_t n, co
           max_calls = max(max_calls, ncalls);
           s_off = ns_off; s_n = ns_n;
           w.lin[id / 64] |= 1ull << (id % 64);
-          // lift(entry)
+          // lift(entry): porcupine writes entry.next.prev unconditionally, so
+          // a call left last in the list (two calls sharing one return) is
+          // its nil dereference
           const int32_t m = E.match;
+          if (w.next[entry] < 0) { outcome = LIT_PANIC; break; }
           w.next[w.prev[entry]] = w.next[entry];
-          if (w.next[entry] >= 0) w.prev[w.next[entry]] = w.prev[entry];
+          w.prev[w.next[entry]] = w.prev[entry];
           w.next[w.prev[m]] = w.next[m];
           if (w.next[m] >= 0) w.prev[w.next[m]] = w.prev[m];
           entry = w.next[0];
@@ -241,7 +244,8 @@ __global__ void literal_kernel(const LitDesc* __restrict__ descs, uint32_t n, co
       w.next[w.prev[m]] = m;
       if (w.next[m] >= 0) w.prev[w.next[m]] = m;
       w.next[w.prev[entry]] = entry;
-      if (w.next[entry] >= 0) w.prev[w.next[entry]] = entry;
+      if (w.next[entry] < 0) { outcome = LIT_PANIC; break; }  // (entry.next.prev: unconditional)
+      w.prev[w.next[entry]] = entry;
       entry = w.next[entry];
     }
   }
@@ -260,9 +264,12 @@ __global__ void literal_kernel(const LitDesc* __restrict__ descs, uint32_t n, co
   R.deep_len = 0;
   if (outcome == LIT_OK && moves) {
     // the linearization: the call events in the order the search took them
+    // (clamped to the history's n_ops + 1 slot; a longer stack can only come
+    // from a shared-return list and fails certification)
     uint32_t* out = moves + R.witness_off;
-    for (uint32_t k = 0; k < ncalls; ++k) out[k] = (uint32_t)(w.calls[k].entry - 1);
-    R.witness_len = ncalls;
+    const uint32_t nw = min(ncalls, D.moves_cap);
+    for (uint32_t k = 0; k < nw; ++k) out[k] = (uint32_t)(w.calls[k].entry - 1);
+    R.witness_len = nw;
     R.has_witness = 1;
   } else {
     R.witness_len = 0;
@@ -282,6 +289,7 @@ void literal_prepare(const History& h, uint32_t i, uint64_t pool_off, std::vecto
   d.n_ev = n_ev;
   d.ev_off = (uint32_t)evs.size();
   d.W = std::max<uint32_t>(1, (n_ev / 2 + 63) / 64);
+  d.moves_cap = h.n_ops + 1;
   descs.push_back(d);
   std::vector<uint32_t> op_of_call(n_ev, EV_INF);
   for (uint32_t k = 0; k < h.n_ops; ++k) op_of_call[h.op_call[k]] = k;
@@ -307,13 +315,20 @@ int literal_run(DevBatch& b, hipStream_t stream, const RunOpts& ro, const unsign
   const uint32_t n = (uint32_t)b.lit_desc.size();
   if (!n) return 0;
   if (!b.lit_dev_ready) {
-    // one slice of device memory per history: 1/8 of free HBM over the
-    // histories, at most 2 GiB each
+    // One slice of device memory per history, from a fixed share of free HBM
+    // (1/8, at least 64 MiB): that share over the histories, between 16 MiB
+    // and 2 GiB each. When the histories need more slices than the share
+    // holds (about 2,000 histories on an empty MI355X), they run in chunks
+    // that reuse one buffer, so the literal engine never takes more than its
+    // share from the other engines and never fails a batch for memory.
     size_t free_b = 0, total_b = 0;
     LITCHK(hipMemGetInfo(&free_b, &total_b));
-    const uint64_t slice = std::max<uint64_t>(16ull << 20, std::min<uint64_t>(2ull << 30, (free_b / 8) / n)) & ~255ull;
+    uint64_t share = std::max<uint64_t>(64ull << 20, free_b / 8);
+    if (const char* e_ = getenv("S2LC_LITERAL_SHARE")) share = std::max<uint64_t>(16ull << 20, strtoull(e_, nullptr, 10));  // (tests)
+    const uint64_t slice = std::max<uint64_t>(16ull << 20, std::min<uint64_t>(2ull << 30, share / n)) & ~255ull;
+    b.lit_chunk = (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>(n, share / slice));
     for (uint32_t k = 0; k < n; ++k) {
-      b.lit_desc[k].mem_off = (uint64_t)k * slice;
+      b.lit_desc[k].mem_off = (uint64_t)(k % b.lit_chunk) * slice;
       b.lit_desc[k].mem_bytes = slice;
     }
     // (the events start 256-byte aligned: LitEv holds a 64-byte aligned OpRec)
@@ -325,11 +340,12 @@ int literal_run(DevBatch& b, hipStream_t stream, const RunOpts& ro, const unsign
       LITCHK(hipMalloc(&b.lit_meta, need_d + need_e));
       b.lit_bytes = need_d + need_e;
     }
-    if (b.lit_mem_bytes < slice * n || !b.lit_mem) {
+    const uint64_t need_m = slice * b.lit_chunk;
+    if (b.lit_mem_bytes < need_m || !b.lit_mem) {
       if (b.lit_mem) (void)hipFree(b.lit_mem);
       b.lit_mem = nullptr;
-      LITCHK(hipMalloc(&b.lit_mem, slice * n));
-      b.lit_mem_bytes = slice * n;
+      LITCHK(hipMalloc(&b.lit_mem, need_m));
+      b.lit_mem_bytes = need_m;
     }
     LITCHK(hipMemcpy(b.lit_meta, b.lit_desc.data(), n * sizeof(LitDesc), hipMemcpyHostToDevice));
     if (!b.lit_ev.empty()) LITCHK(hipMemcpy(b.lit_meta + need_d, b.lit_ev.data(), b.lit_ev.size() * sizeof(LitEv), hipMemcpyHostToDevice));
@@ -341,10 +357,15 @@ int literal_run(DevBatch& b, hipStream_t stream, const RunOpts& ro, const unsign
   // runs ~1 M per second)
   unsigned long long iters = 1ull << 22;
   if (const char* ev_ = getenv("S2LC_LITERAL_ITERS")) iters = std::max<unsigned long long>(1, strtoull(ev_, nullptr, 10));
-  hipLaunchKernelGGL(literal_kernel, dim3((n + 63) / 64), dim3(64), 0, stream, d, n, e, (const uint64_t*)b.pool,
-                     b.lit_mem, b.res, ro.witness ? b.moves : nullptr, (unsigned long long)ro.max_configs, iters,
-                     deadline);
-  LITCHK(hipGetLastError());
+  // chunks of lit_chunk histories, one launch each, in stream order (each
+  // chunk's slices are the previous chunk's)
+  for (uint32_t c0 = 0; c0 < n; c0 += b.lit_chunk) {
+    const uint32_t m = std::min(b.lit_chunk, n - c0);
+    hipLaunchKernelGGL(literal_kernel, dim3((m + 63) / 64), dim3(64), 0, stream, d + c0, m, e, (const uint64_t*)b.pool,
+                       b.lit_mem, b.res, ro.witness ? b.moves : nullptr, (unsigned long long)ro.max_configs, iters,
+                       deadline);
+    LITCHK(hipGetLastError());
+  }
   return 0;
 }
 

@@ -54,6 +54,8 @@ struct LitDesc {
   uint32_t W;         // bitset words (porcupine: len(entries) / 2 bits)
   uint64_t mem_off;   // this history's work slice in the literal buffer
   uint64_t mem_bytes;
+  uint32_t moves_cap;  // witness slots (n_ops + 1)
+  uint32_t _pad;
 };
 struct LitEv {
   OpRec rec;          // a call with a matched return: the op's record (batch pool offsets)
@@ -172,6 +174,8 @@ struct DevBatch {
   uint8_t* lit_mem = nullptr;        // device: one work slice per literal history
   size_t lit_bytes = 0, lit_mem_bytes = 0;
   bool lit_dev_ready = false;
+  bool force_reset = false;  // the next run must zero its counters with the reset dispatch
+  uint32_t lit_chunk = 1;  // literal histories per launch (their slices share one buffer)
   unsigned long long* agg = nullptr;   // device: per packed launch, 8 totals (pack_kernel PackAgg)
   unsigned long long* h_agg = nullptr; // pinned copy
   uint64_t in_bytes_list[3] = {0, 0, 0};  // input SoA bytes of each packed list

@@ -429,12 +429,19 @@ int batch_run(DevBatch& b, hipStream_t stream, const RunOpts& ro, RunStats& st, 
   uint32_t n_forced = 0;
   for (uint32_t i = 0; i < b.n_hist; ++i) n_forced += b.forced[i] ? 1u : 0u;
   const uint32_t n_packed_all = b.n_pack8 + b.n_pack16 + b.n_pack32;
+  // (force_reset: a run that flipped the parity but returned before it had
+  // enqueued the zeroing of the other set leaves that set unzeroed)
   const bool no_reset = engine == S2LC_ENGINE_AUTO && b.lit_desc.empty() && !ro.round_counts && !deadline_ns &&
+                        !b.force_reset &&
                         n_packed_all > 0 && n_packed_all + n_forced == b.n_hist && !getenv("S2LC_RESET_ALWAYS");
   if (!no_reset) {
+    b.force_reset = true;
     hipLaunchKernelGGL(reset_results_kernel, dim3(std::max<uint32_t>(1, (b.n_hist + 255) / 256)), dim3(256), 0,
                        stream, b.res, b.n_hist, b.counter, b.agg);
     HIPCHK(hipGetLastError());
+    b.force_reset = false;
+  } else {
+    b.force_reset = true;  // until the first packed launch (it zeroes the next run's set) is enqueued
   }
   if (deadline_ns) {
     int rate_khz = 100000;  // device wall clock (s_memrealtime); 100 MHz on gfx950
@@ -538,6 +545,7 @@ int batch_run(DevBatch& b, hipStream_t stream, const RunOpts& ro, RunStats& st, 
       else if (li == 1) hipExtLaunchKernelGGL(pack_kernel<16>, dim3(grid), dim3(PACK_BLOCK), smem, stream, e0, e1, 0, pp);
       else hipExtLaunchKernelGGL(pack_kernel<32>, dim3(grid), dim3(PACK_BLOCK), smem, stream, e0, e1, 0, pp);
       HIPCHK(hipGetLastError());
+      if (pp.zero_ctr) b.force_reset = false;
       launched[li] = true;
       st.launches++;
     }

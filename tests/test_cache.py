@@ -125,3 +125,24 @@ def test_duplicate_id_histories_round_trip():
         ea, eb = a.events_numpy(), b.events_numpy()
         for f in ("kind", "op_id", "input_type", "num_records", "n_record_hashes", "failure", "tail", "stream_hash"):
             assert (ea[f] == eb[f]).all(), f
+
+
+def test_wrapping_hash_range_is_refused():
+    """An event whose record-hash range wraps the u64 sum (hash_off = 2^64 - 1,
+    hash_cnt = 2: off + cnt = 1) must be refused, not handed out as a pointer
+    past the pool (cache.cpp bounds checks)."""
+    h = s2.events_from_reader(
+        b'{"event":{"Start":{"Append":{"num_records":1,"record_hashes":[7],"set_fencing_token":null,'
+        b'"fencing_token":null,"match_seq_num":null}}},"client_id":1,"op_id":1}\n')
+    assert h.info()["structural"] != 0  # a call without a return: stored with its events (mode 1)
+    img = s2.save_cache([h])
+    assert s2.load_cache(img)[0].events() == h.events()
+    hdr = (24 + 8 * 2 + 7) & ~7
+    off0 = struct.unpack_from("<Q", img, 24)[0]
+    ev0 = hdr + off0 + 72  # the section header is 72 bytes; Event: hash_off at +56, hash_cnt at +64
+    assert struct.unpack_from("<QQ", img, ev0 + 56) == (0, 1)
+    t = bytearray(img)
+    struct.pack_into("<QQ", t, ev0 + 56, (1 << 64) - 1, 2)
+    with pytest.raises(s2.S2LCError) as e:
+        s2.load_cache(bytes(t))
+    assert e.value.status == -2

@@ -76,6 +76,39 @@ def test_two_calls_share_one_return():
         assert res[0].verdict == v
 
 
+def _call_left_last():
+    """c(b) c(a) c(a) r(a) r(b), indefinite-failure appends: both a-calls link
+    to the one r(a); after two lifts the second a-call is last in the list and
+    porcupine's lift dereferences its nil next node."""
+    A = lambda i: {"kind": "call", "op_id": i, "input_type": 0, "num_records": 1, "record_hashes": [5 + i]}
+    R = lambda i: {"kind": "return", "op_id": i, "failure": True, "definite_failure": False}
+    return [A(2), A(1), A(1), R(1), R(2)]
+
+
+def test_call_left_last_in_the_list_is_porcupines_panic():
+    ev = _call_left_last()
+    assert oracle(ev)[0] == "Panic"
+    hs, res = check([ev])
+    assert res[0].verdict == s2.Unknown, res[0]
+    assert res[0].witness is None
+
+
+def test_literal_histories_in_chunks_sharing_one_buffer(monkeypatch):
+    """More duplicate-id histories than the literal engine's share of HBM holds
+    slices for (S2LC_LITERAL_SHARE = 32 MiB: two 16 MiB slices): they run in
+    chunks over one buffer, and every verdict still equals the oracle's."""
+    monkeypatch.setenv("S2LC_LITERAL_SHARE", str(32 << 20))
+    rng = random.Random(11)
+    cases = [dup_history(rng, rng.randint(3, 10), p_dup=0.7) for _ in range(9)]
+    hs, res = check(cases)
+    for i, (ev, r) in enumerate(zip(cases, res)):
+        v, _ = oracle(ev)
+        if v == "Panic":
+            assert r.verdict == s2.Unknown, (i, r)
+        else:
+            assert r.verdict == v, (i, r.verdict, v)
+
+
 def test_random_duplicate_id_histories_match_the_literal_oracle():
     rng = random.Random(20261017)
     cases = [dup_history(rng, rng.randint(2, 14), n_clients=rng.randint(2, 4), p_dup=0.7) for _ in range(400)]

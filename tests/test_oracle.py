@@ -75,6 +75,16 @@ def test_model_panics_are_reported():
     assert orc.check_wgl([call, ret])[0] == "Panic"
 
 
+def test_call_left_last_in_the_list_panics_instead_of_crashing():
+    """Two calls linked to one return can leave a call last in checkSingle's
+    list; porcupine's lift then dereferences the call's nil next node. The
+    restatement reports that panic (it used to dereference NULL itself)."""
+    A = lambda i: {"kind": "call", "op_id": i, "input_type": 0, "num_records": 1, "record_hashes": [5 + i]}
+    R = lambda i: {"kind": "return", "op_id": i, "failure": True, "definite_failure": False}
+    v, st = orc.check_wgl([A(2), A(1), A(1), R(1), R(2)], compute_partial=True, timeout=5.0)
+    assert v == "Panic" and st["cache_inserts"] == 3
+
+
 def test_reduced_search_matches_wgl():
     """The CPU reduced search (cross-check oracle for C5) agrees with the WGL
     restatement on random histories and on simulator histories."""
