@@ -379,6 +379,15 @@ int s2lc_replay(const s2lc_history* h, const uint32_t* order, size_t n);
 int s2lc_witness_from_moves(const s2lc_history* h, const uint32_t* moves, size_t n_moves, int p4,
                             int64_t* out_ids, size_t cap);
 
+/* s2Model.DescribeOperation (main.go:341-352, formatAppendCall /
+ * formatReadCall / formatCheckTailCall main.go:362-426) of op op_index (dense,
+ * as s2lc_step_cpu): written NUL-terminated into buf[cap] (truncated to fit);
+ * returns the full length without the NUL, or a negative error. */
+int s2lc_describe_operation(const s2lc_history* h, uint32_t op_index, char* buf, size_t cap);
+/* s2Model.DescribeState (main.go:353-360) of s, whose token is an interned id
+ * of h (0 = nil); same buffer convention. */
+int s2lc_describe_state(const s2lc_history* h, const s2lc_state* s, char* buf, size_t cap);
+
 /* porcupine.Visualize(model, info, file) (main.go:608-631): write an HTML page
  * for a checked history — each client's ops on the event axis, labelled with
  * DescribeOperation (main.go:341-426), and the witness (Ok) or the deepest

@@ -196,6 +196,8 @@ SIGNATURES = [
                                             ctypes.c_size_t, ctypes.c_int, ctypes.POINTER(_P),
                                             ctypes.POINTER(ctypes.c_size_t), ctypes.c_char_p, ctypes.c_size_t]),
     ("s2lc_visualize", ctypes.c_int, [_P, ctypes.POINTER(c_result), ctypes.c_char_p]),
+    ("s2lc_describe_operation", ctypes.c_int, [_P, ctypes.c_uint32, ctypes.c_char_p, ctypes.c_size_t]),
+    ("s2lc_describe_state", ctypes.c_int, [_P, ctypes.POINTER(c_state), ctypes.c_char_p, ctypes.c_size_t]),
     ("s2lc_check_partials", ctypes.c_int, [_P, _P, ctypes.POINTER(c_partials)]),
     ("s2lc_visualize_info", ctypes.c_int, [_P, ctypes.POINTER(c_result), ctypes.POINTER(c_partials), ctypes.c_char_p]),
     ("s2lc_partials_free", None, [ctypes.POINTER(c_partials)]),
@@ -404,6 +406,25 @@ class History:
         if n < 0:
             raise S2LCError(n, "step")
         return [(outs[k].tail, outs[k].stream_hash, outs[k].token) for k in range(n)]
+
+    def describe_operation(self, op_index: int) -> str:
+        """s2Model.DescribeOperation (main.go:341-352) of dense op `op_index`."""
+        n = lib().s2lc_describe_operation(self._h, op_index, None, 0)
+        if n < 0:
+            raise S2LCError(n, "describe_operation")
+        buf = ctypes.create_string_buffer(n + 1)
+        lib().s2lc_describe_operation(self._h, op_index, buf, n + 1)
+        return buf.value.decode()
+
+    def describe_state(self, state: Tuple[int, int, int]) -> str:
+        """s2Model.DescribeState (main.go:353-360) of (tail, hash, token_id)."""
+        s = c_state(state[0], state[1], state[2], 0)
+        n = lib().s2lc_describe_state(self._h, ctypes.byref(s), None, 0)
+        if n < 0:
+            raise S2LCError(n, "describe_state")
+        buf = ctypes.create_string_buffer(n + 1)
+        lib().s2lc_describe_state(self._h, ctypes.byref(s), buf, n + 1)
+        return buf.value.decode()
 
     def replay(self, order: Sequence[int]) -> bool:
         arr = (ctypes.c_uint32 * len(order))(*order)

@@ -81,6 +81,30 @@ using namespace s2lc;
 
 static int render(const s2lc_history* hh, const s2lc_result* r, const s2lc_partials* info, const char* path);
 
+static int put_str(const std::string& s, char* buf, size_t cap) {
+  if (buf && cap) {
+    const size_t n = std::min(s.size(), cap - 1);
+    memcpy(buf, s.data(), n);
+    buf[n] = 0;
+  }
+  return (int)std::min<size_t>(s.size(), 0x7FFFFFFF);
+}
+
+extern "C" int s2lc_describe_operation(const s2lc_history* hh, uint32_t op, char* buf, size_t cap) {
+  if (!hh) return S2LC_EINVAL;
+  const History& h = hh->h;
+  h.ensure_events();
+  if (op >= h.n_ops || h.op_call[op] >= h.events.size()) return S2LC_EINVAL;
+  return put_str(describe_op(h, op), buf, cap);
+}
+
+extern "C" int s2lc_describe_state(const s2lc_history* hh, const s2lc_state* s, char* buf, size_t cap) {
+  if (!hh || !s) return S2LC_EINVAL;
+  const History& h = hh->h;
+  if (s->token > h.tokens.size()) return S2LC_EINVAL;
+  return put_str(describe_state(h, State{s->tail, s->stream_hash, s->token}), buf, cap);
+}
+
 extern "C" int s2lc_visualize(const s2lc_history* hh, const s2lc_result* r, const char* path) {
   return render(hh, r, nullptr, path);
 }
