@@ -77,7 +77,8 @@ struct LvCtl {
   uint32_t found_parent, found_move, found_p4, closed;  // closed: children closed (the rest failed the P1 precheck)
   unsigned long long children;  // children generated this round
   unsigned long long prof_end;  // S2LC_PROF: latest expansion end of the round (wall clock)
-  uint32_t _pad[4];
+  uint32_t stop;      // lv_persist: the run's deadline passed (set by workgroup 0 before the round's barrier)
+  uint32_t _pad[3];
   uint32_t lo[LV_STRIPES];        // lv_insert: first slot of each stripe not inserted yet (chunked rounds)
   uint32_t cnt[LV_STRIPES * 16];  // stripe s reserves slots at cnt[16 s] (holes included)
 };
@@ -92,7 +93,8 @@ __device__ __forceinline__ unsigned long long ld_agent64(const unsigned long lon
 
 // State of one level search, kept on the device across rounds and published
 // to host-mapped memory by the last lv_insert block of every round.
-enum : uint32_t { LVR_RUNNING = 0, LVR_FOUND = 1, LVR_EMPTY = 2, LVR_BUDGET = 3, LVR_OVERFLOW = 4, LVR_ABORT = 5 };
+enum : uint32_t { LVR_RUNNING = 0, LVR_FOUND = 1, LVR_EMPTY = 2, LVR_BUDGET = 3, LVR_OVERFLOW = 4, LVR_ABORT = 5,
+                  LVR_TIMEOUT = 6 };  // (timeout: the run's device deadline passed inside lv_persist)
 struct LvRun {
   uint32_t done;           // LVR_*
   uint32_t round;          // expansion rounds completed (round 0 = the initial closure)
@@ -109,7 +111,7 @@ struct LvRun {
   uint32_t last_nf;        // frontier expanded by the last round
   unsigned long long last_closed;  // children it closed (slices per configuration)
   uint32_t solo_rounds;    // rounds run as solo rounds (LvSolo)
-  uint32_t _pad;
+  uint32_t solo_skip;      // a round a solo phase handed to the grid (too many live moves)
   // wall-clock ticks of the rounds by their frontier (the configurations they
   // expand): narrower than LV_WIDE_NF (the rounds the distributed search
   // replicates) or not (the ones it partitions); t_last = the last close
@@ -350,8 +352,7 @@ template <int NQ>
 __device__ __forceinline__ int lv_closure(LvHot (&H)[NQ], uint32_t (&d)[NQ], const uint32_t (&cnt)[NQ],
                                           const uint32_t* s_cs, const LvHeadsLds<NQ>& PL, int lane, const State& s,
                                           uint32_t hflags, uint32_t minret_seed, const OpRec* __restrict__ recs,
-                                          uint32_t& minret_out, const LvHeadsLds<NQ>* NX = nullptr,
-                                          unsigned long long* prof = nullptr) {
+                                          uint32_t& minret_out) {
   const bool nowrap = hflags & H_NOWRAP;
   const bool p2 = hflags & H_P2OK;
   const bool p4 = hflags & H_P4;
@@ -377,18 +378,13 @@ __device__ __forceinline__ int lv_closure(LvHot (&H)[NQ], uint32_t (&d)[NQ], con
     }
     const uint32_t minret = wave_min_u32(mr);
     const uint64_t bound = t32 ? suf64_of32(wave_min_u32(bd32)) : wave_min_u64(bd);
-#ifdef S2LC_PROF
-    if (prof && lane == 0) atomicAdd(prof, 1ull);  // passes
-#else
-    (void)prof;
-#endif
     if (__ballot(dead) || (nowrap && s.tail > bound)) return CL_DEAD;
     const bool changed = __ballot(adv != 0) != 0;
     if (!changed && minret == minret_prev) {
       minret_out = minret;
       return minret == EV_INF ? CL_COMPLETE : ((p4 && bound == REQ_NONE) ? CL_P4 : CL_ALIVE);
     }
-    if (!NX && NQ <= 5) {
+    if (NQ <= 5) {
       // grid rounds (NQ <= 5): every slot's next head loaded at once, unconditionally
       // (a slot that does not advance reloads its current head, cached), so
       // the pass waits one memory latency, not one or two per advancing slot
@@ -413,9 +409,6 @@ __device__ __forceinline__ int lv_closure(LvHot (&H)[NQ], uint32_t (&d)[NQ], con
                                   (uint64_t)ca[q].z | ((uint64_t)ca[q].w << 32), s);
         }
       }
-#ifdef S2LC_PROF
-      if (prof) atomicAdd(prof + 1, (unsigned long long)__popc(adv));  // head loads from memory (per lane)
-#endif
       minret_prev = minret;
       continue;
     }
@@ -423,16 +416,7 @@ __device__ __forceinline__ int lv_closure(LvHot (&H)[NQ], uint32_t (&d)[NQ], con
     for (int q = 0; q < NQ; ++q) {
       if ((adv >> q) & 1u) {
         d[q] += 1;
-        if (NX && d[q] == 1) {  // solo rounds: the record after the parent's head is in LDS
-          H[q].suf = NX->suf[q][lane]; H[q].call = NX->call[q][lane]; H[q].ret = NX->ret[q][lane];
-          const uint32_t fl = NX->fl[q][lane];
-          H[q].fl = fl | HB_KNOWN | lv_legal_bits(fl, NX->otail[q][lane], NX->ohash[q][lane], s);
-        } else {
-          H[q] = lv_load_child_head(recs + s_cs[64 * q + lane] + cnt[q] + d[q], s);
-#ifdef S2LC_PROF
-          if (prof) atomicAdd(prof + 1, 1ull);  // head loads from memory (per lane)
-#endif
-        }
+        H[q] = lv_load_child_head(recs + s_cs[64 * q + lane] + cnt[q] + d[q], s);
       }
     }
     minret_prev = minret;
@@ -655,66 +639,10 @@ __device__ __forceinline__ void lv_stage_insert(const LvParams& p, const LvRound
   if (lane == 0) atomicExch(&p.ht[slot], mine);
 }
 
-// ---- solo rounds: a frontier of ONE configuration ---------------------------
-// Most rounds of a hard history keep exactly one configuration (H174: 10,129
-// of its 10,285 rounds). The children of one configuration are pairwise
-// distinct (each linearizes a different durable / indefinite op, or the same
-// indefinite op with two different states), so such a round needs no dedupe
-// table and no grid: workgroup 0 of lv_persist runs it alone, its four waves
-// splitting the moves, with the configuration's heads kept in LDS from round
-// to round (only the chains the surviving child advanced are reloaded). Every
-// surviving child is written to the staging array exactly as a grid round
-// leaves its frontier (staging slot, next-frontier index, trace entry; no
-// table slot), so grid rounds and the host take over after any solo round.
 // Workgroup barrier over LDS only: waits for this wave's LDS operations, not
 // for its global loads and write-through stores (a __syncthreads release
 // would drain those too). Solo rounds share only LDS between their waves.
 __device__ __forceinline__ void lv_sync_lds() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); }
-
-constexpr int LV_SOLO_HP = 4;  // record hashes of each head kept in LvSolo
-constexpr int LV_SOLO_HP2 = 4; // the next ones, in LvSoloExt (8 in LDS: 91 % of C5's appends)
-
-// Solo rounds' per-head data kept beside PL / NX in the space the grid rounds
-// use for waves 2 and 3 (s_heads[2..3]): the move's fields PL does not hold
-// (32 bytes per chain, not the whole 64-byte record) and record hashes
-// LV_SOLO_HP .. LV_SOLO_HP + LV_SOLO_HP2 - 1 of each head, so that a move
-// whose append carries up to 8 record hashes folds them from LDS (round 2:
-// 4 in LDS, the rest loaded on the round's critical path for 60 % of C5's
-// appends).
-struct LvMoveRec {
-  uint64_t num_records, msn;
-  uint32_t hash_off, hash_cnt;
-  uint32_t toks;  // batch_tok | set_tok << 16 (OpRec bytes 56..59)
-  uint32_t _pad;
-};
-template <int NQ>
-struct LvSoloExt {
-  LvMoveRec mr[64 * NQ];
-  uint64_t hp2[LV_SOLO_HP2][64 * NQ];
-};
-template <int NQ>
-struct LvSolo {
-  uint64_t hp[LV_SOLO_HP][64 * NQ];  // the heads' first record hashes
-  uint32_t nx_hoff[64 * NQ], nx_hcnt[64 * NQ];  // record-hash range of each head's next record
-  uint16_t cnt[64 * NQ];   // the configuration's chain counts
-  uint16_t keep[64 * NQ];  // advance per chain of the child with staging index 0
-  uint64_t tail, hash, chx;        // the configuration: state, XOR of its chain terms
-  uint64_t ktail, khash, kchx;     // the kept child
-  uint32_t tok, pmin, ptrace, ktok, kmr, kmv, cs_end;
-  uint32_t tbase, wit;
-  // the round's outcome, by round parity: round n counts into c[n & 1] while
-  // its close zeroes c[(n + 1) & 1] (no barrier between reading and resetting)
-  struct Ctr {
-    uint32_t alive, found, fpar, fmov, fp4, ovf;
-    unsigned long long kids;
-  } c[2];
-  uint64_t wx[LV_BLOCK / 64];
-#ifdef S2LC_PROF
-  unsigned long long pt[8];  // wave 0 phase cycles: [0] start [1] setup [2] pre [3] moves [4] close [5] next; [7] last stamp
-  unsigned long long pc[6];  // closure cycles (ALIVE, other), ALIVE closures, stage cycles (all waves), closure passes, closure head loads
-  unsigned long long pw[2];  // [0] sum over rounds of the slowest wave's expansion cycles, [1] this round's max
-#endif
-};
 
 // (smallest, second smallest) of the heads' P1 bounds over the wave's chains
 // (a value held by two chains is both), in every lane.
@@ -776,31 +704,6 @@ __device__ __forceinline__ void wave_min2_hot32(const LvHot (&H)[NQ], uint32_t& 
   }
 }
 
-// Write one surviving solo child into staging slot k of round r (header line,
-// counters, next-frontier index, trace entry): the form lv_stage_insert leaves.
-template <int NQ>
-__device__ __forceinline__ void lv_solo_put(const LvParams& p, uint32_t k, const State& s, uint64_t fp, uint64_t chx,
-                                            uint32_t minret, uint32_t ptrace, uint32_t move, uint32_t tbase,
-                                            uint32_t wit, const uint32_t (&cnt)[NQ], const uint32_t (&d)[NQ]) {
-  const int lane = (int)(threadIdx.x & 63);
-  LCfg<NQ>* o = lv_cfg<NQ>(p.stg, k);
-  const uint32_t tr = wit ? p.tgid + tbase + k : TRACE_NONE;
-  const unsigned long long w = lane == 0 ? s.tail
-                             : lane == 1 ? s.hash
-                             : lane == 2 ? fp
-                             : lane == 3 ? ((unsigned long long)minret << 32 | s.tok)
-                             : lane == 4 ? ((unsigned long long)move << 32 | ptrace)
-                             : lane == 5 ? ((unsigned long long)LV_NONE << 32 | tr)
-                             : lane == 6 ? chx
-                                         : 0ull;
-  if (lane < 16) st_wt64(reinterpret_cast<unsigned long long*>(o) + lane, w);
-  lv_store_cnt_wt<NQ>(o->cnt, cnt, d);
-  if (lane == 0) {
-    st_wt32(&p.nxt_idx[k], k);
-    if (wit) p.trace[tbase + k] = TraceEnt{ptrace, move};
-  }
-}
-
 // P1 bound (sufmin) of a record
 __device__ __forceinline__ uint64_t ld_suf(const OpRec* r) {
   return *reinterpret_cast<const uint64_t*>(reinterpret_cast<const uint8_t*>(r) + 32);
@@ -808,24 +711,22 @@ __device__ __forceinline__ uint64_t ld_suf(const OpRec* r) {
 
 // ---- expansion: one wave per (frontier configuration, slice of its candidates)
 // MODE 0: stage into the striped staging array (lv_insert deduplicates);
-// MODE 1: the persistent kernel's stage-and-insert;
-// MODE 2: a solo round (one configuration, in LDS; the four waves of
-//         workgroup 0 take one slice of its moves each).
+// MODE 1: the persistent kernel's stage-and-insert.
+// (A frontier of one configuration runs as solo rounds: solo_dev.h.)
 template <int NQ, int MODE>
 __device__ __forceinline__ bool lv_expand(const LvParams& p, const LvRoundIn& in, LvHeadsLds<NQ>& PL,
-                                          const uint32_t* s_cs, LvSolo<NQ>* sol = nullptr,
-                                          LvHeadsLds<NQ>* NX = nullptr, const LvSoloExt<NQ>* FR = nullptr) {
-  constexpr bool FUSED = MODE == 1, SOLO = MODE == 2;
+                                          const uint32_t* s_cs) {
+  constexpr bool FUSED = MODE == 1;
   const int lane = (int)(threadIdx.x & 63);
   const uint32_t K = p.K;
   const bool idefer = p.hflags & H_IDEFER;
   const uint32_t f0 = in.f0, nf = in.nf, S = in.S;
-  const uint32_t nwaves = SOLO ? LV_BLOCK / 64 : gridDim.x * (LV_BLOCK / 64);
+  const uint32_t nwaves = gridDim.x * (LV_BLOCK / 64);
   const uint32_t items = nf * S;
   uint32_t rk = 0, rleft = 0;  // reserved staging slots (wave-uniform)
-  const uint32_t wave_id = SOLO ? (threadIdx.x >> 6) : blockIdx.x * (LV_BLOCK / 64) + (threadIdx.x >> 6);
+  const uint32_t wave_id = blockIdx.x * (LV_BLOCK / 64) + (threadIdx.x >> 6);
   const uint32_t stripe = wave_id & (LV_STRIPES - 1);
-  if (!SOLO && wave_id < items) {  // the first reservation, in flight with the first item's loads
+  if (wave_id < items) {  // the first reservation, in flight with the first item's loads
     uint32_t b0 = 0;
     if (lane == 0) b0 = atomicAdd(&p.ctl->cnt[16 * stripe], LV_RESERVE);
     rk = rl(b0, 0);
@@ -841,16 +742,12 @@ __device__ __forceinline__ bool lv_expand(const LvParams& p, const LvRoundIn& in
     LV_ADD(5, 1);
     const uint32_t f = f0 + it / S;
     const uint32_t slice = it % S;
-    // parent configuration (round 0: the all-zero initial one; solo: in LDS)
-    const LCfg<NQ>* pc = (p.init || SOLO) ? nullptr : lv_cfg<NQ>(p.cur, p.cur_idx[f]);
-    const bool has_parent = SOLO || pc;
+    // parent configuration (round 0: the all-zero initial one)
+    const LCfg<NQ>* pc = p.init ? nullptr : lv_cfg<NQ>(p.cur, p.cur_idx[f]);
+    const bool has_parent = pc != nullptr;
     State ps{0, 0, 0};
     uint32_t pmin = 0, ptrace = TRACE_NONE;
-    if (SOLO) {
-      ps = State{sol->tail, sol->hash, sol->tok};
-      pmin = sol->pmin;
-      ptrace = sol->ptrace;
-    } else if (pc) {
+    if (pc) {
       ps = State{pc->tail, pc->hash, pc->tok};
       pmin = pc->minret;
       ptrace = pc->trace;
@@ -870,7 +767,7 @@ __device__ __forceinline__ bool lv_expand(const LvParams& p, const LvRoundIn& in
     // counts, and a slot past K reads record 0 (s_cs is 0 there).
     // (NQ <= 5: wider layouts would spill the grouped registers; they load
     // per slot)
-    constexpr bool HG = !SOLO && NQ <= 5;
+    constexpr bool HG = NQ <= 5;
     uint4 ha[HG ? NQ : 1], hb[HG ? NQ : 1];
     uint32_t hf[HG ? NQ : 1];
     if (HG) {
@@ -892,28 +789,23 @@ __device__ __forceinline__ bool lv_expand(const LvParams& p, const LvRoundIn& in
     for (int q = 0; q < NQ; ++q) {
       const uint32_t j = (uint32_t)lane + 64u * q;
       d[q] = 0;
-      if (SOLO) {
-        cnt[q] = sol->cnt[j];
-        H[q] = lv_parent_hot<NQ>(PL, q, lane);
-      } else {
-        if (!HG) cnt[q] = (j < K && pc) ? (uint32_t)pc->cnt[j] : 0u;
-        if (j < K) {
-          if (HG) {
-            H[q] = lv_put_parent_head<NQ>(ha[HG ? q : 0], hb[HG ? q : 0], hf[HG ? q : 0], PL, q, lane);
-          } else {
-            const OpRec* r = p.recs + s_cs[64 * q + lane] + cnt[q];
-            H[q] = lv_put_parent_head<NQ>(ld16(r, 16), ld16(r, 32), r->flags, PL, q, lane);
-          }
+      if (!HG) cnt[q] = (j < K && pc) ? (uint32_t)pc->cnt[j] : 0u;
+      if (j < K) {
+        if (HG) {
+          H[q] = lv_put_parent_head<NQ>(ha[HG ? q : 0], hb[HG ? q : 0], hf[HG ? q : 0], PL, q, lane);
         } else {
-          H[q] = lv_hot_null();
-          PL.fl[q][lane] = OPF_SENTINEL; PL.call[q][lane] = EV_INF; PL.ret[q][lane] = EV_INF; PL.suf[q][lane] = REQ_NONE;
+          const OpRec* r = p.recs + s_cs[64 * q + lane] + cnt[q];
+          H[q] = lv_put_parent_head<NQ>(ld16(r, 16), ld16(r, 32), r->flags, PL, q, lane);
         }
-        if (j < K && !pc) chx ^= lv_chain_term(j, cnt[q]);  // (round 0; a staged parent carries it)
+      } else {
+        H[q] = lv_hot_null();
+        PL.fl[q][lane] = OPF_SENTINEL; PL.call[q][lane] = EV_INF; PL.ret[q][lane] = EV_INF; PL.suf[q][lane] = REQ_NONE;
       }
+      if (j < K && !pc) chx ^= lv_chain_term(j, cnt[q]);  // (round 0; a staged parent carries it)
       // candidate moves: minimal durable / indefinite appends at the chain heads
       if (has_parent && !(H[q].fl & (OPF_SENTINEL | OPF_CLS_E)) && H[q].call < pmin) cand |= 1u << q;
     }
-    const uint64_t parent_chx = SOLO ? sol->chx : pc ? pc->chx : wave_xor_u64(chx);
+    const uint64_t parent_chx = pc ? pc->chx : wave_xor_u64(chx);
     LV_LAP(1);
     // candidate moves in (slot, lane) order; this slice takes moves [c0, c1)
     uint32_t n_cand = 0, my_idx[NQ];
@@ -933,9 +825,6 @@ __device__ __forceinline__ bool lv_expand(const LvParams& p, const LvRoundIn& in
     // outcome and hash fold, for those moves in parallel, so a move in the
     // loop below costs only its next head's load. Registers: 5 per slot
     // (NQ <= 6).
-#ifdef S2LC_PROF
-    if (SOLO && threadIdx.x == 0) { const unsigned long long t_ = clock64(); sol->pt[1] += t_ - sol->pt[7]; sol->pt[7] = t_; }
-#endif
     constexpr bool PRE = NQ <= 6;
     constexpr int NP = PRE ? NQ : 1;
     uint64_t mv_tail[NP], mv_hash[NP];
@@ -959,7 +848,7 @@ __device__ __forceinline__ bool lv_expand(const LvParams& p, const LvRoundIn& in
     // (S2LC_PRE_GROUP) grid rounds: the rest of every candidate's record and
     // its next record's P1 bound loaded for all slots before the precheck
     // uses any (one latency instead of one per slot with a candidate)
-    constexpr bool PG = !SOLO && NQ <= 5 && S2LC_PRE_GROUP;
+    constexpr bool PG = NQ <= 5 && S2LC_PRE_GROUP;
     uint4 pm0[PG ? NP : 1], pm3[PG ? NP : 1];
     uint64_t pns[PG ? NP : 1];
     if (PG) {
@@ -980,20 +869,11 @@ __device__ __forceinline__ bool lv_expand(const LvParams& p, const LvRoundIn& in
       mv_pk[q] = ps.tok << 16;
       if (PRE && ((cand >> q) & 1u) && my_idx[q] >= c0 && my_idx[q] < c1) {
         const OpRec* hp = p.recs + s_cs[64 * q + lane] + cnt[q];
-        // the chain's next record's P1 bound (solo rounds: in LDS)
-        const uint64_t nx_suf = SOLO ? NX->suf[q][lane] : PG ? pns[PG ? q : 0] : (p1 ? ld_suf(hp + 1) : REQ_NONE);
-        // the head: solo rounds keep the heads' whole records in LDS; grid
-        // rounds just loaded its hot part (cached)
+        // the chain's next record's P1 bound
+        const uint64_t nx_suf = PG ? pns[PG ? q : 0] : (p1 ? ld_suf(hp + 1) : REQ_NONE);
+        // the head: its hot part was just loaded (cached)
         OpRec r;
-        if (SOLO) {  // PL's fields + the move fields of LvSoloExt
-          const LvMoveRec& m_ = FR->mr[64 * q + lane];
-          r.num_records = m_.num_records; r.msn = m_.msn;
-          r.out_tail = PL.otail[q][lane]; r.out_hash = PL.ohash[q][lane]; r.sufmin = PL.suf[q][lane];
-          r.call_ev = PL.call[q][lane]; r.ret_ev = PL.ret[q][lane];
-          r.hash_off = m_.hash_off; r.hash_cnt = m_.hash_cnt;
-          r.batch_tok = (uint16_t)m_.toks; r.set_tok = (uint16_t)(m_.toks >> 16);
-          r.flags = PL.fl[q][lane];
-        } else if (PG) {  // bytes 0..15 and 48..63 just loaded; 16..47 in PL / H
+        if (PG) {  // bytes 0..15 and 48..63 just loaded; 16..47 in PL / H
           const uint4 a0 = pm0[PG ? q : 0], a3 = pm3[PG ? q : 0];
           r.num_records = (uint64_t)a0.x | ((uint64_t)a0.y << 32);
           r.msn = (uint64_t)a0.z | ((uint64_t)a0.w << 32);
@@ -1016,24 +896,7 @@ __device__ __forceinline__ bool lv_expand(const LvParams& p, const LvRoundIn& in
         // the fold: for a live opt child, or for an indefinite append's
         // identity test (opt == s needs equal tails)
         const bool fold = (to && !p1dead) || ((r.flags & OPF_CLS_I) && g && opt.tail == ps.tail);
-        if (fold) {
-          if (SOLO) {  // the first LV_SOLO_HP record hashes are in LDS
-            uint64_t h = ps.hash;
-            const uint32_t j = (uint32_t)lane + 64u * q;
-#pragma unroll
-            for (int k = 0; k < LV_SOLO_HP; ++k)
-              if ((uint32_t)k < r.hash_cnt) h = chain_hash(h, sol->hp[k][j]);
-#pragma unroll
-            for (int k = 0; k < LV_SOLO_HP2; ++k)
-              if ((uint32_t)(LV_SOLO_HP + k) < r.hash_cnt) h = chain_hash(h, FR->hp2[k][j]);
-            if (r.hash_cnt > (uint32_t)(LV_SOLO_HP + LV_SOLO_HP2))
-              h = fold_hashes_blk(h, p.pool + r.hash_off + LV_SOLO_HP + LV_SOLO_HP2,
-                                  r.hash_cnt - LV_SOLO_HP - LV_SOLO_HP2);
-            opt.hash = h;
-          } else {
-            opt.hash = fold_hashes_blk(ps.hash, p.pool + r.hash_off, r.hash_cnt);
-          }
-        }
+        if (fold) opt.hash = fold_hashes_blk(ps.hash, p.pool + r.hash_off, r.hash_cnt);
         const bool ti = (r.flags & OPF_CLS_I) && (!idefer || r.ret_ev == pmin) && !(g && state_eq(opt, ps));
         mv_tail[q] = opt.tail;
         mv_hash[q] = opt.hash;
@@ -1053,9 +916,6 @@ __device__ __forceinline__ bool lv_expand(const LvParams& p, const LvRoundIn& in
         LV_ADD(9, nd);
       }
     }
-#ifdef S2LC_PROF
-    if (SOLO && threadIdx.x == 0) { asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); const unsigned long long t_ = clock64(); sol->pt[2] += t_ - sol->pt[7]; sol->pt[7] = t_; }
-#endif
     uint32_t ord = 0, q_cur = 0;
     uint64_t m = has_parent ? __ballot(live & 1u) : 1ull;
     for (;;) {
@@ -1078,14 +938,7 @@ __device__ __forceinline__ bool lv_expand(const LvParams& p, const LvRoundIn& in
       uint32_t fl2;
       State so;
       if (PRE) {
-        if (SOLO) {
-          if (lane == src) {  // loaded into LDS with the slice's moves
-            const uint64_t ot = NX->otail[q_cur][lane], oh = NX->ohash[q_cur][lane], sf = NX->suf[q_cur][lane];
-            nx_obs = make_uint4((uint32_t)ot, (uint32_t)(ot >> 32), (uint32_t)oh, (uint32_t)(oh >> 32));
-            nx_mid = make_uint4((uint32_t)sf, (uint32_t)(sf >> 32), NX->call[q_cur][lane], NX->ret[q_cur][lane]);
-            nx_fl = NX->fl[q_cur][lane];
-          }
-        } else if (has_parent && lane == src) {
+        if (has_parent && lane == src) {
           // the chain's next head (the child's first new head)
           const OpRec* nx = p.recs + s_cs[64 * q_cur + lane] + sel_cnt<NQ>(cnt, q_cur) + 1;
           nx_obs = ld16(nx, 16);
@@ -1122,7 +975,6 @@ __device__ __forceinline__ bool lv_expand(const LvParams& p, const LvRoundIn& in
         if (!((fl2 >> w) & 1u)) continue;
         const State cs_ = w == 0 ? so : ps;
         const uint32_t mv = !has_parent ? LV_NONE : (w == 0 ? j : (j | MOVE_IDENT));
-        if (SOLO) LV_ADD(8, 1);
         if (has_parent) {
           kids++;
 #pragma unroll
@@ -1140,34 +992,11 @@ __device__ __forceinline__ bool lv_expand(const LvParams& p, const LvRoundIn& in
         uint32_t mr = 0;
         LV_LAP(4);
         LV_ADD(6, 1);
-#ifdef S2LC_PROF
-        const unsigned long long tc0_ = clock64();
-#endif
         ++closed;
-#ifdef S2LC_PROF
-        const int cr = lv_closure<NQ>(H, d, cnt, s_cs, PL, lane, cs_, p.hflags, pmin, p.recs, mr, SOLO ? NX : nullptr,
-                                      SOLO ? &sol->pc[4] : nullptr);
-#else
-        const int cr = lv_closure<NQ>(H, d, cnt, s_cs, PL, lane, cs_, p.hflags, pmin, p.recs, mr, SOLO ? NX : nullptr);
-#endif
-#ifdef S2LC_PROF
-        if (SOLO && lane == 0) {  // closure cycles: [8] ALIVE, [9] others; [10] ALIVE count; [11] stage cycles
-          asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-          const unsigned long long dt_ = clock64() - tc0_;
-          atomicAdd(&sol->pc[cr == CL_ALIVE ? 0 : 1], dt_);
-          if (cr == CL_ALIVE) atomicAdd(&sol->pc[2], 1ull);
-        }
-        const unsigned long long ts0_ = clock64();
-#endif
+        const int cr = lv_closure<NQ>(H, d, cnt, s_cs, PL, lane, cs_, p.hflags, pmin, p.recs, mr);
         LV_LAP(3);
         if (cr == CL_COMPLETE || cr == CL_P4) {
-          if (SOLO) {
-            if (lane == 0 && atomicCAS(&sol->c[in.par].found, 0u, 1u) == 0u) {
-              sol->c[in.par].fpar = ptrace;
-              sol->c[in.par].fmov = mv;
-              sol->c[in.par].fp4 = cr == CL_P4 ? 1u : 0u;
-            }
-          } else if (lane == 0 && atomicCAS(&p.ctl->found, 0u, 1u) == 0u) {
+          if (lane == 0 && atomicCAS(&p.ctl->found, 0u, 1u) == 0u) {
             atomicExch(&p.ctl->found_parent, ptrace);
             atomicExch(&p.ctl->found_move, mv);
             atomicExch(&p.ctl->found_p4, cr == CL_P4 ? 1u : 0u);
@@ -1180,32 +1009,8 @@ __device__ __forceinline__ bool lv_expand(const LvParams& p, const LvRoundIn& in
             if (d[q]) dx ^= lv_chain_term(jj, cnt[q]) ^ lv_chain_term(jj, cnt[q] + d[q]);
           }
           const uint64_t cdx = parent_chx ^ wave_xor_u64(dx);
-          // (a solo round's first survivor is kept in LDS without it)
           auto fp_of = [&]() { return mix64(cdx ^ lv_state_term(cs_.tail, cs_.hash, cs_.tok)); };
-          if (SOLO) {
-            // distinct children: staging slot = arrival order; the first one is
-            // kept in LDS in case it turns out to be the round's only survivor
-            uint32_t k = 0;
-            if (lane == 0) k = atomicAdd(&sol->c[in.par].alive, 1u);
-            k = rl(k, 0);
-            // the first survivor stays in LDS only: it is written to the
-            // staging array after the round if it is not the only one
-            if (k == 0) {
-#pragma unroll
-              for (int q = 0; q < NQ; ++q) sol->keep[lane + 64 * q] = (uint16_t)d[q];
-              if (lane == 0) {
-                sol->ktail = cs_.tail; sol->khash = cs_.hash; sol->ktok = cs_.tok;
-                sol->kchx = cdx; sol->kmr = mr; sol->kmv = mv;
-              }
-            } else if (k < p.scs) {
-              lv_solo_put<NQ>(p, k, cs_, fp_of(), cdx, mr, ptrace, mv, in.tbase, in.wit, cnt, d);
-            } else if (lane == 0) {
-              sol->c[in.par].ovf = 1u;
-            }
-#ifdef S2LC_PROF
-            if (lane == 0) atomicAdd(&sol->pc[3], clock64() - ts0_);
-#endif
-          } else if (FUSED) {
+          if (FUSED) {
             lv_stage_insert<NQ>(p, in, stripe, rk, rleft, cs_, fp_of(), cdx, mr, ptrace, mv, cnt, d);
           } else {
             lv_stage<NQ>(p, stripe, rk, rleft, cs_, fp_of(), cdx, mr, ptrace, mv, cnt, d);
@@ -1222,18 +1027,12 @@ __device__ __forceinline__ bool lv_expand(const LvParams& p, const LvRoundIn& in
     }
   }
 #ifdef S2LC_PROF
-  if (lane == 0 && p.prof && lv_acc[5]) {  // only waves that had work (idle waves would swamp the counters)
-    if (SOLO) {  // [14] closures run, [15] opt children dropped by the P1 precheck
-      atomicAdd(&p.prof[14], lv_acc[8]);
-      atomicAdd(&p.prof[15], lv_acc[9]);
-    } else {
-      for (int i_ = 0; i_ < 9; ++i_) atomicAdd(&p.prof[i_ < 7 ? i_ : i_ + 5], lv_acc[i_]);
-    }
-  }
+  if (lane == 0 && p.prof && lv_acc[5])  // only waves that had work (idle waves would swamp the counters)
+    for (int i_ = 0; i_ < 9; ++i_) atomicAdd(&p.prof[i_ < 7 ? i_ : i_ + 5], lv_acc[i_]);
 #endif
   if (MODE == 0 && rleft) lv_release<NQ>(p, stripe, rk, rleft);
-  if (lane == 0 && kids) atomicAdd(SOLO ? &sol->c[in.par].kids : &p.ctl->children, kids);
-  if (!SOLO && lane == 0 && closed) atomicAdd(&p.ctl->closed, closed);
+  if (lane == 0 && kids) atomicAdd(&p.ctl->children, kids);
+  if (lane == 0 && closed) atomicAdd(&p.ctl->closed, closed);
   return wave_id < items;
 }
 
@@ -1487,6 +1286,8 @@ struct LvPersist {
   uint32_t max_rounds;        // rounds per launch
   uint32_t nf_max;            // leave when the frontier is wider
   uint32_t solo;              // one-configuration frontiers run as solo rounds (workgroup 0)
+  uint32_t solo_maxlive;      // a solo round with more live moves goes to the grid (0: default)
+  const unsigned long long* deadline;  // the run's deadline (device wall clock; nullable, 0 = none)
   unsigned long long spin_ticks;  // barrier wait limit (wall-clock ticks)
 };
 
@@ -1524,233 +1325,7 @@ __device__ __forceinline__ bool lv_grid_sync(LvBar* B, uint32_t e, unsigned long
   return s_ok != 0;
 }
 
-// A solo configuration's head on chain j at record h (chain end: `end`, its
-// sentinel's index + 1): its whole record into FR[j] (the move's record, read
-// by the expansion), its closure fields into PL, the record after it into NX
-// (a child's first new head on this chain) with its record-hash range, and
-// the head's first LV_SOLO_HP record hashes into S.hp. `known`: the head's
-// hash range is already known (it was the previous head's next record), so
-// the hash loads go out with the record loads instead of after them.
-template <int NQ>
-__device__ __forceinline__ void lv_solo_head(const LvParams& p, const OpRec* h, const OpRec* end, uint32_t j,
-                                             bool known, LvHeadsLds<NQ>& PL, LvHeadsLds<NQ>& NX, LvSoloExt<NQ>* FR,
-                                             LvSolo<NQ>& S) {
-  constexpr int HP = LV_SOLO_HP + LV_SOLO_HP2;
-  const uint4* a = reinterpret_cast<const uint4*>(h);
-  const uint4* b = reinterpret_cast<const uint4*>(h + 1 < end ? h + 1 : h);  // (the sentinel has no next record)
-  const uint4 x0 = a[0], x1 = a[1], x2 = a[2], x3 = a[3];
-  const uint4 y1 = b[1], y2 = b[2], y3 = b[3];
-  uint64_t hv[HP];
-  if (known) {
-    const uint32_t ho = S.nx_hoff[j], hc = S.nx_hcnt[j];
-#pragma unroll
-    for (int k = 0; k < HP; ++k) hv[k] = (uint32_t)k < hc ? p.pool[ho + k] : 0ull;
-  } else {
-#pragma unroll
-    for (int k = 0; k < HP; ++k) hv[k] = (uint32_t)k < x3.y ? p.pool[x3.x + k] : 0ull;
-  }
-  LvMoveRec& m = FR->mr[j];
-  m.num_records = (uint64_t)x0.x | ((uint64_t)x0.y << 32);
-  m.msn = (uint64_t)x0.z | ((uint64_t)x0.w << 32);
-  m.hash_off = x3.x;
-  m.hash_cnt = x3.y;
-  m.toks = x3.z;
-  const int q = (int)(j >> 6), l = (int)(j & 63);
-  PL.otail[q][l] = (uint64_t)x1.x | ((uint64_t)x1.y << 32);
-  PL.ohash[q][l] = (uint64_t)x1.z | ((uint64_t)x1.w << 32);
-  PL.suf[q][l] = (uint64_t)x2.x | ((uint64_t)x2.y << 32);
-  PL.call[q][l] = x2.z;
-  PL.ret[q][l] = x2.w;
-  PL.fl[q][l] = x3.w;
-  NX.otail[q][l] = (uint64_t)y1.x | ((uint64_t)y1.y << 32);
-  NX.ohash[q][l] = (uint64_t)y1.z | ((uint64_t)y1.w << 32);
-  NX.suf[q][l] = (uint64_t)y2.x | ((uint64_t)y2.y << 32);
-  NX.call[q][l] = y2.z;
-  NX.ret[q][l] = y2.w;
-  NX.fl[q][l] = y3.w;
-  S.nx_hoff[j] = y3.x;
-  S.nx_hcnt[j] = y3.y;
-#pragma unroll
-  for (int k = 0; k < LV_SOLO_HP; ++k) S.hp[k][j] = hv[k];
-#pragma unroll
-  for (int k = 0; k < LV_SOLO_HP2; ++k) FR->hp2[k][j] = hv[LV_SOLO_HP + k];
-}
-
-// The whole workgroup writes a solo configuration held in LDS (counts
-// S.cnt[j] + (child ? S.keep[j] : 0), the configuration's or the kept child's
-// header) into staging slot 0 of `stg` / index list `idx`: the form a grid
-// round leaves its frontier in.
-template <int NQ>
-__device__ void lv_solo_write(const LvSolo<NQ>& S, bool child, uint8_t* stg, uint32_t* idx, uint32_t tgid,
-                              uint32_t trace_id, uint32_t K) {
-  LCfg<NQ>* o = lv_cfg<NQ>(stg, 0);
-  for (uint32_t j = threadIdx.x; j < 64u * NQ; j += LV_BLOCK)
-    st_wt16(&o->cnt[j], (uint16_t)(j < K ? S.cnt[j] + (child ? S.keep[j] : 0u) : 0u));
-  if (threadIdx.x < 16) {
-    const uint32_t l = threadIdx.x;
-    const uint64_t tail = child ? S.ktail : S.tail, hash = child ? S.khash : S.hash;
-    const uint32_t tok = child ? S.ktok : S.tok, mr = child ? S.kmr : S.pmin;
-    const uint64_t fp = mix64((child ? S.kchx : S.chx) ^ lv_state_term(tail, hash, tok));
-    const unsigned long long w = l == 0 ? tail
-                               : l == 1 ? hash
-                               : l == 2 ? fp
-                               : l == 3 ? ((unsigned long long)mr << 32 | tok)
-                               : l == 4 ? ((unsigned long long)(child ? S.kmv : LV_NONE) << 32 | (child ? S.ptrace : TRACE_NONE))
-                               : l == 5 ? ((unsigned long long)LV_NONE << 32 | trace_id)
-                               : l == 6 ? (child ? S.kchx : S.chx)
-                                        : 0ull;
-    st_wt64(reinterpret_cast<unsigned long long*>(o) + l, w);
-  }
-  if (threadIdx.x == 0) st_wt32(&idx[0], 0u);
-  (void)tgid;
-}
-
-// Solo rounds (LvSolo), run by workgroup 0 of lv_persist while the others
-// wait at the grid barrier: enter from the frontier's one configuration, go on
-// while every round keeps exactly one, and stop when a round keeps none or
-// several, completes, overflows, or after max_rounds. R is the workgroup's run
-// state; every round is closed on it exactly as a grid round is.
-template <int NQ>
-__device__ void lv_solo_rounds(const LvParams& p, const LvPersist& q, LvRun& R, LvHeadsLds<NQ>& PL,
-                               LvHeadsLds<NQ>* NX, LvSoloExt<NQ>* FR, const uint32_t* s_cs, LvSolo<NQ>& S,
-                               uint32_t max_rounds) {
-  const uint32_t K = p.K;
-  // end of chain j's records (its sentinel's index + 1)
-  auto chain_end = [&](uint32_t j) { return p.recs + (j + 1 < K ? s_cs[j + 1] : S.cs_end); };
-  if (threadIdx.x == 0) S.cs_end = p.cs[K];
-  lv_sync_lds();
-  {  // the configuration: counts, heads (all four waves share them), state, chain terms
-    const uint32_t r = R.round + 1;
-    const LCfg<NQ>* pc = lv_cfg<NQ>(q.stg[(r + 1) & 1], q.idx[(r + 1) & 1][0]);
-    uint64_t chx = 0;
-    for (uint32_t j = threadIdx.x; j < 64u * NQ; j += LV_BLOCK) {
-      const int qq = (int)(j >> 6), l = (int)(j & 63);
-      const uint32_t c = j < K ? (uint32_t)pc->cnt[j] : 0u;
-      S.cnt[j] = (uint16_t)c;
-      S.keep[j] = 0;
-      if (j < K) {
-        lv_solo_head<NQ>(p, p.recs + s_cs[j] + c, chain_end(j), j, false, PL, *NX, FR, S);
-        chx ^= lv_chain_term(j, c);
-      } else {
-        PL.fl[qq][l] = OPF_SENTINEL; PL.call[qq][l] = EV_INF; PL.ret[qq][l] = EV_INF; PL.suf[qq][l] = REQ_NONE;
-        NX->fl[qq][l] = OPF_SENTINEL; NX->call[qq][l] = EV_INF; NX->ret[qq][l] = EV_INF; NX->suf[qq][l] = REQ_NONE;
-      }
-    }
-    chx = wave_xor_u64(chx);
-    if ((threadIdx.x & 63) == 0) S.wx[threadIdx.x >> 6] = chx;
-    if (threadIdx.x == 0) {
-      S.tail = pc->tail; S.hash = pc->hash; S.tok = pc->tok;
-      S.pmin = pc->minret; S.ptrace = pc->trace;
-      if (pc->slot <= p.ht_mask) st_wt64(&q.ht[(r + 1) & 1][pc->slot], HT_EMPTY);
-    }
-    lv_sync_lds();
-    if (threadIdx.x == 0) {
-      uint64_t x = 0;
-      for (int w = 0; w < LV_BLOCK / 64; ++w) x ^= S.wx[w];
-      S.chx = x;
-    }
-  }
-#ifdef S2LC_PROF
-  const unsigned long long t_solo = wall_clock64();
-  uint32_t n_solo = 0;
-#endif
-#ifdef S2LC_PROF
-  if (threadIdx.x == 0) { for (int i_ = 0; i_ < 8; ++i_) S.pt[i_] = 0; for (int i_ = 0; i_ < 6; ++i_) S.pc[i_] = 0; S.pw[0] = S.pw[1] = 0; S.pt[7] = clock64(); }
-#define LV_SOLO_T(i) do { if (threadIdx.x == 0) { const unsigned long long t_ = clock64(); S.pt[i] += t_ - S.pt[7]; S.pt[7] = t_; } } while (0)
-#else
-#define LV_SOLO_T(i) do { } while (0)
-#endif
-  if (threadIdx.x == 0) {
-    for (int i = 0; i < 2; ++i) S.c[i] = typename LvSolo<NQ>::Ctr{0, 0, 0, 0, 0, 0, 0ull};
-    S.tbase = (uint32_t)R.tnext; S.wit = R.witness;
-  }
-  lv_sync_lds();
-  // Two workgroup barriers per round: after the expansion (its outcome is
-  // final), and after the close. When the round's only survivor carries on,
-  // its advanced heads are reloaded right after the first barrier, in the
-  // shadow of thread 0's close of the run state.
-  for (uint32_t n = 0; n < max_rounds; ++n) {
-    const uint32_t r = R.round + 1;
-    const uint32_t par = n & 1u;
-#ifdef S2LC_PROF
-    ++n_solo;
-#endif
-    LvParams rp = p;
-    rp.round = r;
-    rp.stg = q.stg[r & 1];
-    rp.nxt_idx = q.idx[r & 1];
-    LvRoundIn in;
-    in.f0 = 0; in.nf = 1; in.par = par; in.S = LV_BLOCK / 64; in.tbase = S.tbase; in.wit = S.wit;
-    LV_SOLO_T(0);
-#ifdef S2LC_PROF
-    const unsigned long long tw0_ = clock64();
-#endif
-    (void)lv_expand<NQ, 2>(rp, in, PL, s_cs, &S, NX, FR);
-#ifdef S2LC_PROF
-    if ((threadIdx.x & 63) == 0) atomicMax(&S.pw[1], clock64() - tw0_);
-#endif
-    LV_SOLO_T(3);
-    lv_sync_lds();
-    LV_SOLO_T(6);
-    const uint32_t alive = S.c[par].alive, found = S.c[par].found, ovf = S.c[par].ovf;
-    const bool carry = !found && !ovf && alive == 1;  // the only survivor is the next configuration
-    if (carry) {
-      for (uint32_t j = threadIdx.x; j < 64u * NQ; j += LV_BLOCK) {
-        const uint32_t dj = S.keep[j];
-        if (dj) {
-          const uint32_t c = S.cnt[j] + dj;
-          S.cnt[j] = (uint16_t)c;
-          lv_solo_head<NQ>(p, p.recs + s_cs[j] + c, chain_end(j), j, dj == 1, PL, *NX, FR, S);
-        }
-      }
-    }
-    if (threadIdx.x == 0) {
-      LvCounts k;
-      k.nn = alive; k.ovf = ovf; k.fnd = found;
-      k.fpar = S.c[par].fpar; k.fmov = S.c[par].fmov; k.fp4 = S.c[par].fp4; k.ch = S.c[par].kids; k.closed = 0;
-      const unsigned long long t_prev = R.t_last;
-      lv_close_state(R, k, r, p.rcounts, p.scap, p.trace_cap);
-      R.solo_rounds++;
-      R.solo_ticks += R.t_last - t_prev;
-      // the first survivor's trace entry (it was not staged)
-      if (!found && !ovf && alive && in.wit) p.trace[in.tbase] = TraceEnt{S.ptrace, S.kmv};
-      if (carry) {
-        S.tail = S.ktail; S.hash = S.khash; S.tok = S.ktok; S.chx = S.kchx; S.pmin = S.kmr;
-        S.ptrace = in.wit ? p.tgid + in.tbase : TRACE_NONE;
-      }
-      S.tbase = (uint32_t)R.tnext; S.wit = R.witness;
-      S.c[par ^ 1u] = typename LvSolo<NQ>::Ctr{0, 0, 0, 0, 0, 0, 0ull};
-#ifdef S2LC_PROF
-      S.pw[0] += S.pw[1];
-      S.pw[1] = 0;
-#endif
-    }
-    LV_SOLO_T(4);
-    lv_sync_lds();
-    LV_SOLO_T(5);
-    if (ovf && !found) {
-      // the host re-runs round r from its frontier: this configuration, in
-      // the staging array the round read its frontier from
-      lv_solo_write<NQ>(S, false, q.stg[(r + 1) & 1], q.idx[(r + 1) & 1], p.tgid, S.ptrace, K);
-    } else if (!found && alive >= 2) {
-      lv_solo_write<NQ>(S, true, q.stg[r & 1], q.idx[r & 1], p.tgid, in.wit ? p.tgid + in.tbase : TRACE_NONE, K);
-    }
-    if (R.done != LVR_RUNNING || R.nf != 1) break;
-    if (n + 1 == max_rounds)  // leaving with one configuration: the next round's frontier
-      lv_solo_write<NQ>(S, false, q.stg[r & 1], q.idx[r & 1], p.tgid, S.ptrace, K);
-  }
-#ifdef S2LC_PROF
-  if (threadIdx.x == 0 && p.prof) {  // [7] solo rounds, [8] their wall-clock ticks, [16..21] phase cycles
-    atomicAdd(&p.prof[7], (unsigned long long)n_solo);
-    atomicAdd(&p.prof[8], wall_clock64() - t_solo);
-    for (int i_ = 0; i_ < 6; ++i_) atomicAdd(&p.prof[16 + i_], S.pt[i_]);
-    atomicAdd(&p.prof[31], S.pt[6]);
-    atomicAdd(&p.prof[28], S.pw[0]);
-    for (int i_ = 0; i_ < 6; ++i_) atomicAdd(&p.prof[22 + i_], S.pc[i_]);
-  }
-#endif
-#undef LV_SOLO_T
-}
+#include "solo_dev.h"
 
 template <int NQ>
 __global__ __launch_bounds__(LV_BLOCK, 2) void lv_persist(LvParams p, LvPersist q) {
@@ -1758,6 +1333,7 @@ __global__ __launch_bounds__(LV_BLOCK, 2) void lv_persist(LvParams p, LvPersist 
   // moves' next heads) and s_heads[2..3] as the move records (LvSoloExt)
   __shared__ __attribute__((aligned(16))) LvHeadsLds<NQ> s_heads[LV_BLOCK / 64];
   static_assert(2 * sizeof(LvHeadsLds<NQ>) >= sizeof(LvSoloExt<NQ>), "solo move records fit in s_heads[2..3]");
+  static_assert(sizeof(LvHeadsLds<NQ>) >= sizeof(LvSoloHeads<NQ>), "solo heads fit in s_heads[0], s_heads[1]");
   __shared__ uint32_t s_cs[64 * NQ];
   __shared__ LvRun s_run;
   __shared__ LvSolo<(NQ <= 5 ? NQ : 1)> s_solo;  // (solo rounds only for NQ <= 5)
@@ -1766,6 +1342,7 @@ __global__ __launch_bounds__(LV_BLOCK, 2) void lv_persist(LvParams p, LvPersist 
   __syncthreads();
   if (s_run.done != LVR_RUNNING) return;
   const uint32_t nwaves = gridDim.x * (LV_BLOCK / 64);
+  const unsigned long long dl = q.deadline ? *q.deadline : 0ull;  // (deadline_kernel wrote it earlier on the stream)
   bool ok = true;
 #ifdef S2LC_PROF
   unsigned long long t_round = wall_clock64();
@@ -1778,10 +1355,15 @@ __global__ __launch_bounds__(LV_BLOCK, 2) void lv_persist(LvParams p, LvPersist 
     const uint32_t r_before = s_run.round;
     // solo rounds for NQ <= 5 (K <= 320): wider layouts would lose the second
     // resident workgroup per CU the grid barrier relies on (VGPRs)
-    if (NQ <= 5 && q.solo && s_run.nf == 1) {
+    // (H_TAIL32 histories only: their tails are 32-bit in solo rounds)
+    if (NQ <= 5 && q.solo && (p.hflags & H_TAIL32) && s_run.nf == 1 && s_run.solo_skip != s_run.round + 1) {
       if (blockIdx.x == 0) {
-        if constexpr (NQ <= 5) lv_solo_rounds<NQ>(p, q, s_run, s_heads[0], &s_heads[1],
-                                                   reinterpret_cast<LvSoloExt<(NQ <= 5 ? NQ : 1)>*>(&s_heads[2]), s_cs, s_solo, max(1u, q.max_rounds - it));
+        if constexpr (NQ <= 5) {
+          lv_solo_rounds<NQ>(p, q, s_run, *reinterpret_cast<LvSoloHeads<NQ>*>(&s_heads[0]),
+                             *reinterpret_cast<LvSoloHeads<NQ>*>(&s_heads[1]),
+                             *reinterpret_cast<LvSoloExt<NQ>*>(&s_heads[2]), s_cs, s_solo, max(1u, q.max_rounds - it),
+                             dl);
+        }
         // the next grid round's counters start at zero: the slot after
         // r_before's, never r_before's own (a workgroup that left round
         // r_before's barrier late may still be reading it: ADVICE r2); the
@@ -1826,6 +1408,9 @@ __global__ __launch_bounds__(LV_BLOCK, 2) void lv_persist(LvParams p, LvPersist 
     in.tbase = (uint32_t)s_run.tnext;
     in.wit = s_run.witness;
     const bool worked = lv_expand<NQ, 1>(rp, in, s_heads[threadIdx.x >> 6], s_cs);
+    // the run's deadline: workgroup 0 decides before the barrier, every
+    // workgroup reads the decision with the round's counters
+    if (dl && blockIdx.x == 0 && threadIdx.x == 0 && wall_clock64() > dl) atomicExch(&rp.ctl->stop, 1u);
 #ifdef S2LC_PROF
     if (worked && (threadIdx.x & 63) == 0 && p.prof) atomicMax(&rp.ctl->prof_end, wall_clock64());
 #else
@@ -1846,6 +1431,7 @@ __global__ __launch_bounds__(LV_BLOCK, 2) void lv_persist(LvParams p, LvPersist 
       if (ok) {
         const LvCounts k = lv_read_counts(rp.ctl);
         lv_close_state(s_run, k, r, blockIdx.x == 0 ? p.rcounts : nullptr, p.scap, p.trace_cap);
+        if (ld_agent(&rp.ctl->stop) && s_run.done == LVR_RUNNING) s_run.done = LVR_TIMEOUT;
       } else {
         s_run.done = LVR_ABORT;
       }
@@ -1869,7 +1455,7 @@ __global__ __attribute__((unused)) void lv_run_init(LvRun* R, unsigned long long
   R->configs = 0; R->children = 0; R->tnext = tnext; R->max_configs = max_configs;
   R->found_parent = TRACE_NONE; R->found_move = LV_NONE; R->found_p4 = 0;
   R->witness = witness; R->deep_trace = TRACE_NONE; R->deep_len = 0; R->last_tbase = TRACE_NONE;
-  R->last_nf = 0; R->last_closed = 0; R->solo_rounds = 0;
+  R->last_nf = 0; R->last_closed = 0; R->solo_rounds = 0; R->solo_skip = 0;
   R->t_last = wall_clock64(); R->narrow_ticks = 0; R->wide_ticks = 0; R->solo_ticks = 0;
 }
 

@@ -232,8 +232,9 @@ constexpr uint32_t LEVEL_KMAX = 512;  // most chains the level search handles
 uint32_t level_nq(uint32_t K);  // register slots per lane: ceil(K / 64)
 // deadline: steady-clock time in ns since epoch after which the search gives
 // Unknown (S2LC_R_TIMEOUT); 0 = none.
-int level_search(DevBatch& b, uint32_t h, hipStream_t st, const RunOpts& ro, int64_t deadline_ns, LevelStats& ls,
-                 std::string& err);
+// (d_deadline: the run's deadline on the device wall clock, nullable)
+int level_search(DevBatch& b, uint32_t h, hipStream_t st, const RunOpts& ro, int64_t deadline_ns,
+                 const unsigned long long* d_deadline, LevelStats& ls, std::string& err);
 void level_release(DevBatch& b);
 int64_t steady_ns();
 

@@ -721,7 +721,7 @@ int batch_run(DevBatch& b, hipStream_t stream, const RunOpts& ro, RunStats& st, 
   // than 128 chains and those whose frontier outgrew the workgroup passes
   todo.insert(todo.end(), level.begin(), level.end());
   for (uint32_t h : todo) {
-    const int rc = level_search(b, h, stream, ro, deadline_ns, st.level, err);
+    const int rc = level_search(b, h, stream, ro, deadline_ns, prm.deadline, st.level, err);
     if (rc) return rc;
   }
   st.kernel_ms += st.level.ms;

@@ -48,6 +48,13 @@ CONFIGS = {
     "H100": dict(workflow=WF_REGULAR, num_clients=100, ops_per_client=60, seed=9, **{**BASE, "p_indefinite": 0.003}),
     "H120m": dict(workflow=WF_MATCH_SEQ_NUM, num_clients=120, ops_per_client=50, seed=9,
                   **{**BASE, "p_indefinite": 0.003}),
+    # > 128 chains with every reduction ablation finishing on the CPU (whole-
+    # search ablation fixtures, tests/golden/make_round_counts.py): many
+    # clients with the client-id cap, few ops each. A144: P1 off 4.9 M unique
+    # configurations, deferral off 36 k; A160: deferral off 4.2 M (P1 off
+    # does not finish)
+    "A144": dict(workflow=WF_REGULAR, num_clients=144, ops_per_client=16, seed=21, **{**BASE, "p_indefinite": 0.02}),
+    "A160": dict(workflow=WF_REGULAR, num_clients=160, ops_per_client=20, seed=13, **{**BASE, "p_indefinite": 0.03}),
     # the round-1 C5 (client-id cap 20: clients stop at their first indefinite failure)
     "C5capped": dict(workflow=WF_REGULAR, num_clients=32, ops_per_client=1000, seed=5,
                      **{**BASE, "p_indefinite": 0.002}),

@@ -14,8 +14,9 @@ minutes. For those (PREFIX) the search runs under a configuration budget
 (or_check_reduced's max_configs) and the fixture keeps the counts of every
 round completed before it ran out ("complete": false): the GPU, under a
 smaller budget, must reproduce that prefix round by round. The whole-search
-P1 / deferral ablations are exercised on the mid-size histories, live in the
-test.
+P1 / deferral ablations run on A144 / A160 (> 128 chains, level search: P1 off
+4.9 M configurations, deferral off 36 k / 4.2 M) and on the mid-size
+histories, live in the test.
 
 Run here (not on the GPU box): python tests/golden/make_round_counts.py
 """
@@ -32,7 +33,9 @@ import oracle as orc  # noqa: E402
 from s2_verification_amd import workloads as W  # noqa: E402
 from helpers import config_digest  # noqa: E402
 
-CASES = {"H174": [0, 2], "H212": [0, 2], "C5bad": [0, 2, 4], "C5wide": [0]}
+CASES = {"H174": [0, 2], "H212": [0, 2], "C5bad": [0, 2, 4], "C5wide": [0],
+         # > 128 chains, whole-search P1 / deferral ablations (A160: P1 or P4 off explodes)
+         "A144": [0, 1, 2, 4, 8], "A160": [0, 2, 8]}
 # (reductions_off, configuration budget): prefix fixtures of exploding ablations
 PREFIX = {"H174": [(1, 60_000_000), (8, 30_000_000)], "C5bad": [(1, 60_000_000), (8, 30_000_000)]}
 

@@ -280,6 +280,34 @@ def test_hard_exploding_ablation_prefix(name, off, mode, monkeypatch):
     assert not bad, (name, off, mode, bad[:5])
 
 
+@pytest.mark.parametrize("mode", ["default", "no_solo", "no_persist"])
+@pytest.mark.parametrize("name,off", [("A144", 0), ("A144", 1), ("A144", 2), ("A144", 4), ("A144", 8),
+                                      ("A160", 0), ("A160", 2), ("A160", 8)])
+def test_hard_complete_ablations(name, off, mode, monkeypatch):
+    """Whole-search reduction ablations on > 128-chain histories (the level
+    search): P1 off (A144, 4.9 M unique configurations) and the indefinite
+    deferral off (A144, 36 k; A160, 4.2 M) run to the end on the CPU reduced
+    search (make_round_counts.py). Verdict, round count and every round's
+    unique-configuration count equal the committed fixture."""
+    from s2_verification_amd import workloads as W
+    _set_mode(monkeypatch, mode)
+    ref = golden("hard_round_counts.json")[name]
+    assert config_digest(name) == ref["digest"], "simulator output changed: regenerate the fixture"
+    want = ref[str(off)]
+    h = W.config_history(name)
+    assert h.info()["n_chains"] > 128
+    b, res = run(checker_for(s2.ENGINE_AUTO, off, rc=True), [h])
+    r = res[0]
+    assert r.verdict == want["verdict"], (name, off, mode, r)
+    assert r.rounds == want["rounds"], (r.rounds, want["rounds"])
+    got = b.round_counts(0)
+    bad = [k for k, (x, y) in enumerate(zip(got, want["counts"])) if x != y]
+    assert got == want["counts"], (name, off, mode, bad[:5])
+    assert b.stats()["level_histories"] == 1
+    if r.verdict == s2.Ok:
+        assert r.witness is not None and len(r.witness) == h.info()["n_ops"]
+
+
 @pytest.mark.parametrize("mode", ["default", "no_solo", "all_persist"])
 @pytest.mark.parametrize("abl", ["all_on", "no_p2", "no_idefer"])
 def test_level_persist_round_counts_match_reduced_search(mode, abl, monkeypatch):
@@ -365,6 +393,24 @@ def test_timeout_gives_unknown():
     assert all(r.verdict != s2.Unknown for r in res)
     v, info = s2.check_events_verbose(None, h, timeout=0.005)
     assert v == s2.Unknown
+
+
+def test_timeout_ends_the_level_search_inside_its_launch():
+    """The run's deadline is checked inside lv_persist (every grid round, every
+    16 solo rounds), not only by the host between launches of up to 4,096
+    rounds: a C5 (solo rounds) or C5wide (grid rounds) search with a short
+    timeout returns Unknown (timeout) within a few milliseconds of it."""
+    import time
+    from s2_verification_amd import workloads as W
+    for name, tmo in (("C5", 0.02), ("C5wide", 0.008)):
+        h = W.config_history(name)
+        ck = s2.Checker(timeout=tmo)
+        ck.check(h)  # (warm: runtime, code objects, level buffers)
+        t = time.perf_counter()
+        r = ck.check(h)
+        dt = time.perf_counter() - t
+        assert r.verdict == s2.Unknown and r.reason == "timeout", (name, r)
+        assert dt < tmo + 0.015, (name, dt)
 
 
 def test_witness_certificate_failure_is_loud(monkeypatch, tmp_path):

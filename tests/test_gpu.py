@@ -166,6 +166,34 @@ def test_cli_verdicts_and_exit_codes(tmp_path):
     assert list((tmp_path / "porcupine-outputs").glob("stdin-*.html"))
 
 
+def test_cli_on_the_baseline_configs(tmp_path):
+    """`s2-porcupine -file=` (main.go:568-640) on the BASELINE single-history
+    configs C1-C3 (collector JSONL from the simulator) and the C5 violation
+    variant: the exit code and verdict line equal the oracle's verdict."""
+    import json
+    import subprocess
+    from s2_verification_amd import workloads as W
+    for name in ("C1", "C2", "C3", "C5bad"):
+        path = tmp_path / (name + ".jsonl")
+        data = W.config_jsonl(name)
+        path.write_bytes(data)
+        if name == "C5bad":  # (WGL does not finish on it: the CPU reduced search, golden)
+            want = golden("hard_reduced.json")["C5bad"]["verdict"]
+        else:
+            h = s2.events_from_reader(data)  # (owner: the arrays view the history's buffers)
+            want = orc.check_wgl(orc.from_s2lc_numpy(h.events_numpy(), owner=h), timeout=60)[0]
+        p = subprocess.run([s2.CLI_PATH, "-file=" + str(path)], capture_output=True, text=True, timeout=120,
+                           cwd=tmp_path)
+        line = json.loads(p.stderr.strip().splitlines()[-1])
+        if want == "Ok":
+            assert p.returncode == 0 and line["msg"] == "passed: is linearizable", (name, p.stderr[-400:])
+        else:
+            assert want == "Illegal"
+            assert p.returncode == 1 and line["msg"] == "failed: is NOT linearizable" and line["res"] == "Illegal", \
+                (name, p.stderr[-400:])
+        assert list((tmp_path / "porcupine-outputs").glob(name + "-*.html"))
+
+
 def test_illegal_partial_prefix(checker):
     """Illegal verdicts carry the deepest certified linearized prefix (the
     visualization's partial linearization); it is a real-time-closed prefix

@@ -61,12 +61,15 @@ def test_search_kernels_use_no_scratch():
            if re.search(r"(pack_kernel|search_kernel|lv_round|lv_insert|lv_persist|literal_kernel)", n)}
     assert len(hot) >= 30, sorted(hot)
     for n, v in hot.items():
-        # lv_persist<5> is bounded to 2 waves/SIMD (256 VGPRs); the compiler
-        # spills a few round-invariant values (32 bytes since the grouped
-        # head loads): stored before the round loop, reloaded once per round,
-        # never inside the item or closure loops. lv_insert declares a
+        # lv_persist runs its solo rounds in a noinline function
+        # (lv_solo_wave, solo_dev.h: its own register allocation, no VGPR
+        # spill inside the solo round loop); the call splits lv_persist's
+        # own allocation, and values live across it (and some grid-round
+        # temporaries) sit in lv_persist's scratch frame. Grid rounds
+        # measured 34.7 us/round with the frame against 35.4 before it
+        # (profiles/r04/solo_v5_ab.txt). lv_insert declares a
         # 20-byte frame its body never touches (no scratch instruction: the
         # round close's counters, addressed flat)
-        limit = 32 if "lv_persistILi5E" in n else 20 if "lv_insert" in n else 0
+        limit = 512 if "lv_persist" in n else 20 if "lv_insert" in n else 0
         assert v.get("scratch", 0) <= limit, (n, v)
         assert v.get("vgpr", 0) <= 256, (n, v)

@@ -137,6 +137,32 @@ def test_reduced_p2_only_prunes():
         assert all(a <= b for a, b in zip(on["counts"], off["counts"]))
 
 
+def test_reduced_search_reproduces_the_complete_ablation_fixtures():
+    """The committed whole-search ablations on > 128 chains (A144 / A160,
+    make_round_counts.py) are what oracle/reduced.c gives now, for those
+    that finish in about a second here; every ablation is a superset of the
+    all-on search round by round (a reduction only removes configurations)."""
+    from helpers import config_digest, golden
+
+    from s2_verification_amd import workloads as W
+    g = golden("hard_round_counts.json")
+    for name, offs in (("A144", (0, 2, 8)), ("A160", (0, 2))):
+        assert config_digest(name) == g[name]["digest"]
+        h = W.config_history(name)
+        assert h.info()["n_chains"] > 128
+        ea = orc.from_s2lc_numpy(h.events_numpy(), owner=h)
+        for off in offs:
+            v, st = orc.check_reduced(ea, reductions_off=off, round_counts=True)
+            want = g[name][str(off)]
+            assert (v, st["rounds"], st["round_counts"]) == (want["verdict"], want["rounds"], want["counts"])
+    for name in ("A144", "A160"):
+        on = g[name]["0"]["counts"]
+        for off in ("1", "2", "8"):
+            if off in g[name]:
+                assert g[name][off]["verdict"] == "Ok" and g[name][off]["rounds"] == g[name]["0"]["rounds"]
+                assert all(a <= b for a, b in zip(on, g[name][off]["counts"]))
+
+
 def test_from_s2lc_numpy_owns_its_hashes():
     """Without the owning history, the oracle's event array copies the record
     hashes: checking it after the history is gone gives the same verdict and
