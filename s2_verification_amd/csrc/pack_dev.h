@@ -375,8 +375,24 @@ __global__ __launch_bounds__(PACK_BLOCK, S2LC_PACK_MINW) void pack_kernel(Params
         ch.at(pcnt);
         const OpRec& r = ch.r;
         const bool cand = on && !(r.flags & (OPF_SENTINEL | OPF_CLS_E)) && r.call_ev < pmin;
-        bool take_opt = false, take_id = false;
+        bool take_opt = false, take_id = false, pre_dead = false;
         State opt = s;
+        // P1 precheck: the smallest required tail among the OTHER chains'
+        // heads (the group's smallest, or its second smallest in the lane
+        // holding the smallest). Lane j's opt child above it is dead at its
+        // closure's first pass (that pass's bound is the min over the same
+        // heads and chain j's next one, never larger), so it is counted as a
+        // child and dropped here: no broadcast, closure pass or window load
+        uint32_t p1x = 0xFFFFFFFFu;
+        if (hd.flags & H_NOWRAP) {
+          const uint32_t s_lo = (uint32_t)r.sufmin, s_hi = (uint32_t)(r.sufmin >> 32);
+          const uint32_t b32 = s_hi == 0 ? min(s_lo, 0xFFFFFFFDu)
+                               : s_hi == 0xFFFFFFFFu && s_lo >= 0xFFFFFFFEu ? s_lo : 0xFFFFFFFDu;
+          const uint32_t m1 = gmin_u32<L>(b32);
+          const int fl = __ffsll((unsigned long long)(__ballot(b32 == m1) & gmask)) - 1;
+          const uint32_t m2 = gmin_u32<L>(lane == fl ? 0xFFFFFFFFu : b32);
+          p1x = lane == fl ? m2 : m1;
+        }
         if (cand) {
           const bool g = append_guards_ok(r, s);
           opt.tail = s.tail + r.num_records;
@@ -386,6 +402,7 @@ __global__ __launch_bounds__(PACK_BLOCK, S2LC_PACK_MINW) void pack_kernel(Params
           } else {
             take_opt = g;
           }
+          if (take_opt && opt.tail > (uint64_t)p1x) { take_opt = false; pre_dead = true; }
           if (take_opt) {
             if (f == 0 && pcnt == pf_cc)
               opt.hash = fold_hashes_pf(s.hash, pf, p.pool + r.hash_off, r.hash_cnt);
@@ -397,7 +414,7 @@ __global__ __launch_bounds__(PACK_BLOCK, S2LC_PACK_MINW) void pack_kernel(Params
         PK_LAP(0);
         uint64_t mo = __ballot(take_opt) & gmask;
         uint64_t mi = __ballot(take_id) & gmask;
-        children += __popcll(mo) + __popcll(mi);
+        children += __popcll(mo) + __popcll(mi) + __popcll(__ballot(pre_dead) & gmask);
         // consume the children one at a time: close, dedupe, insert
         while ((mo | mi) && !found && !overflow) {
           const bool is_id = mo == 0;
