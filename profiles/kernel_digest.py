@@ -13,7 +13,7 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 CSRC = os.path.join(ROOT, "s2_verification_amd", "csrc")
 FILES = {
     "c4": ("model.h", "search.h", "search_dev.h", "pack_dev.h", "search.hip"),
-    "c5": ("model.h", "search.h", "level_dev.h", "level.hip"),
+    "c5": ("model.h", "search.h", "level_dev.h", "solo_dev.h", "level.hip"),
 }
 
 

@@ -522,16 +522,18 @@ int batch_run(DevBatch& b, hipStream_t stream, const RunOpts& ro, RunStats& st, 
         if (const char* e = getenv("S2LC_PACK_BPC")) bpc = std::max(1, atoi(e));  // (diagnostics: grid blocks per CU)
         b.pack_bpc[li] = bpc;
       }
-      // lane groups per wave that take histories: the fewest (1, 2, 4, ...)
-      // with at most ~2.5 histories per group over the resident waves. The
-      // groups of a wave run in lockstep, so fewer per wave give shorter
-      // rounds; past that, more groups keep more histories in flight. C4
-      // sweep (tools/gpw_sweep.sh, profiles/r03): 1,000 histories 1.58 / 1.93 /
-      // 2.42 ms at 1 / 2 / 4 groups, 10,000: 2.66 / 2.02 / 2.59 ms.
+      // lane groups per wave that take histories: 1 up to half a history per
+      // resident wave, 2 up to 2.5, then 4 (x2 per x5). The groups of a wave
+      // run in lockstep, so fewer per wave give shorter rounds; more groups
+      // per wave issue one instruction stream for several histories, which
+      // wins once the SIMDs are shared. C4 sweep with the expand-time P1
+      // precheck (tools/gpw_sweep.sh, profiles/r04/gpw_sweep.txt), ms at
+      // 1 / 2 / 4 groups: 1,000 histories 0.97 / 1.10 / 1.26; 2,500 1.53 /
+      // 1.10 / 1.27; 6,000 1.90 / 1.28 / 1.34; 10,000 2.38 / 1.63 / 1.35.
       const uint32_t gpw_all = 64 / L;
       const uint64_t waves = (uint64_t)n_cu * (uint64_t)bpc * (PACK_BLOCK / 64);
       uint32_t gpw = 1;
-      while (gpw < gpw_all && (uint64_t)n_l * 2 > waves * gpw * 5) gpw *= 2;
+      for (uint64_t lim2 = 1; gpw < gpw_all && (uint64_t)n_l * 2 > waves * lim2; lim2 *= 5) gpw *= 2;
       if (const char* e = getenv("S2LC_PACK_GPW")) gpw = std::max<uint32_t>(1, std::min<uint32_t>(gpw_all, (uint32_t)atoi(e)));
       pp.gpw = gpw < gpw_all ? gpw : 0u;
       const uint32_t groups = (PACK_BLOCK / 64) * gpw;
