@@ -428,6 +428,7 @@ typedef struct s2lc_dist_info_t {
   uint64_t max_frontier;
   double device_ms;        /* device time of this rank's kernels */
   uint64_t trace_len;
+  uint64_t frontier_cap;   /* configurations one round may insert on this rank (world x exchange cap <= this) */
 } s2lc_dist_info_t;
 int s2lc_dist_create(s2lc_ctx* ctx, const s2lc_history* h, int rank, int world, s2lc_dist** out);
 void s2lc_dist_free(s2lc_dist* d);
@@ -457,6 +458,50 @@ int s2lc_dist_local_run(s2lc_dist* d, uint32_t wide, uint64_t* n_next, int32_t* 
 int s2lc_dist_keep_owned(s2lc_dist* d, uint64_t* n_kept);
 int s2lc_dist_frontier_pack(s2lc_dist* d, void* buf);
 int s2lc_dist_frontier_load(s2lc_dist* d, void* buf, uint64_t n);
+/* Host-free partitioned rounds: the driver queues rounds with no host
+ * synchronization and reads each round's status a round or two later.
+ *   s2lc_dist_x_begin   the device run state from this rank's frontier (after
+ *                       s2lc_dist_keep_owned or a partitioned round)
+ *   s2lc_dist_x_send    expand + close the frontier and copy the staged
+ *                       children into world fixed-capacity blocks of
+ *                       (cap + 1) * config_bytes bytes, owner-major, a header
+ *                       in each block's first slot (count, found, staging
+ *                       overflow, the sender's largest block and total)
+ *   (caller)            equal-split all-to-all of send into recv (no sizes)
+ *   s2lc_dist_x_recv    decide the round from the received headers and insert
+ *                       this rank's configurations; *round = its number; recv
+ *                       is the next frontier (kept alive by the caller for at
+ *                       least 8 rounds: a re-run reads it)
+ *   s2lc_dist_x_wait    wait for a queued round and read its status; every
+ *                       rank reads the same decision
+ *   s2lc_dist_x_rewind  a round whose status is S2LC_DIST_X_CAPACITY inserted
+ *                       nothing: drop it and the rounds queued after it, so
+ *                       the next send re-runs it (with a larger cap)
+ *   s2lc_dist_x_end     wait for everything queued; the host-side state
+ *                       (s2lc_dist_info, the frontier) catches up; *done =
+ *                       the stop (S2LC_DIST_X_*), *configs = configurations
+ *                       this rank inserted since s2lc_dist_x_begin */
+enum {
+  S2LC_DIST_X_RUNNING = 0,
+  S2LC_DIST_X_FOUND = 1,     /* a child completed on some rank: Ok */
+  S2LC_DIST_X_EMPTY = 2,     /* no rank staged a child: Illegal */
+  S2LC_DIST_X_CAPACITY = 4,  /* an exchange block over its capacity: rewind and re-run */
+  S2LC_DIST_X_ABORT = 5      /* a rank's staging overflowed (device buffers) */
+};
+typedef struct s2lc_dist_xstat {
+  uint32_t ran;        /* the round ran and published its status (0: the run had stopped before it) */
+  uint32_t done;       /* S2LC_DIST_X_* decided in this round */
+  uint32_t nf;         /* this rank's next frontier */
+  uint32_t maxblk;     /* the largest block any rank sent: the capacity this round needed */
+  uint64_t nf_global;  /* the global frontier this round expanded */
+  uint64_t staged;     /* configurations staged by all ranks this round */
+} s2lc_dist_xstat;
+int s2lc_dist_x_begin(s2lc_dist* d);
+int s2lc_dist_x_send(s2lc_dist* d, void* send /* device */, uint32_t cap);
+int s2lc_dist_x_recv(s2lc_dist* d, void* recv /* device */, uint32_t cap, uint32_t* round);
+int s2lc_dist_x_wait(s2lc_dist* d, uint32_t round, s2lc_dist_xstat* out);
+int s2lc_dist_x_rewind(s2lc_dist* d, uint32_t round);
+int s2lc_dist_x_end(s2lc_dist* d, uint32_t* done, uint64_t* configs);
 /* Copy this rank's trace pool ({parent id, move} u32 pairs) to host memory;
  * with out_pairs == NULL only *n is set. */
 int s2lc_dist_trace(s2lc_dist* d, uint32_t* out_pairs, uint64_t cap_entries, uint64_t* n);

@@ -140,7 +140,17 @@ class c_dist_info(ctypes.Structure):
     _fields_ = [("config_bytes", ctypes.c_uint64), ("n_chains", ctypes.c_uint32), ("round", ctypes.c_uint32),
                 ("frontier", ctypes.c_uint32), ("found_parent", ctypes.c_uint32), ("found_move", ctypes.c_uint32),
                 ("found_p4", ctypes.c_uint32), ("configs", ctypes.c_uint64), ("children", ctypes.c_uint64),
-                ("max_frontier", ctypes.c_uint64), ("device_ms", ctypes.c_double), ("trace_len", ctypes.c_uint64)]
+                ("max_frontier", ctypes.c_uint64), ("device_ms", ctypes.c_double), ("trace_len", ctypes.c_uint64),
+                ("frontier_cap", ctypes.c_uint64)]
+
+
+class c_dist_xstat(ctypes.Structure):
+    _fields_ = [("ran", ctypes.c_uint32), ("done", ctypes.c_uint32), ("nf", ctypes.c_uint32),
+                ("maxblk", ctypes.c_uint32), ("nf_global", ctypes.c_uint64), ("staged", ctypes.c_uint64)]
+
+
+# s2lc_dist_x_* stops (include/s2lincheck.h)
+DIST_X_RUNNING, DIST_X_FOUND, DIST_X_EMPTY, DIST_X_CAPACITY, DIST_X_ABORT = 0, 1, 2, 4, 5
 
 
 # s2lc_event as a numpy structured dtype (bulk export without Python loops)
@@ -221,6 +231,12 @@ SIGNATURES = [
     ("s2lc_dist_keep_owned", ctypes.c_int, [_P, ctypes.POINTER(ctypes.c_uint64)]),
     ("s2lc_dist_frontier_pack", ctypes.c_int, [_P, _P]),
     ("s2lc_dist_frontier_load", ctypes.c_int, [_P, _P, ctypes.c_uint64]),
+    ("s2lc_dist_x_begin", ctypes.c_int, [_P]),
+    ("s2lc_dist_x_send", ctypes.c_int, [_P, _P, ctypes.c_uint32]),
+    ("s2lc_dist_x_recv", ctypes.c_int, [_P, _P, ctypes.c_uint32, ctypes.POINTER(ctypes.c_uint32)]),
+    ("s2lc_dist_x_wait", ctypes.c_int, [_P, ctypes.c_uint32, ctypes.POINTER(c_dist_xstat)]),
+    ("s2lc_dist_x_rewind", ctypes.c_int, [_P, ctypes.c_uint32]),
+    ("s2lc_dist_x_end", ctypes.c_int, [_P, ctypes.POINTER(ctypes.c_uint32), ctypes.POINTER(ctypes.c_uint64)]),
 ]
 
 _lib = None

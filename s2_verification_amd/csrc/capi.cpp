@@ -1077,6 +1077,41 @@ int s2lc_dist_keep_owned(s2lc_dist* x, uint64_t* n_kept) {
   return dist_keep_owned(x->d, n_kept, x->ctx->err);
 }
 
+int s2lc_dist_x_begin(s2lc_dist* x) {
+  if (!x) return S2LC_EINVAL;
+  return dist_x_begin(x->d, x->ctx->err);
+}
+
+int s2lc_dist_x_send(s2lc_dist* x, void* send, uint32_t cap) {
+  if (!x || !send || !cap) return S2LC_EINVAL;
+  return dist_x_send(x->d, (uint8_t*)send, cap, x->ctx->err);
+}
+
+int s2lc_dist_x_recv(s2lc_dist* x, void* recv, uint32_t cap, uint32_t* round) {
+  if (!x || !recv || !cap) return S2LC_EINVAL;
+  return dist_x_recv(x->d, (uint8_t*)recv, cap, round, x->ctx->err);
+}
+
+int s2lc_dist_x_wait(s2lc_dist* x, uint32_t round, s2lc_dist_xstat* out) {
+  if (!x || !out) return S2LC_EINVAL;
+  DistXStat st;
+  const int rc = dist_x_wait(x->d, round, &st, x->ctx->err);
+  if (rc) return rc;
+  out->ran = st.ran; out->done = st.done; out->nf = st.nf; out->maxblk = st.maxblk;
+  out->nf_global = st.nf_global; out->staged = st.staged;
+  return 0;
+}
+
+int s2lc_dist_x_rewind(s2lc_dist* x, uint32_t round) {
+  if (!x) return S2LC_EINVAL;
+  return dist_x_rewind(x->d, round, x->ctx->err);
+}
+
+int s2lc_dist_x_end(s2lc_dist* x, uint32_t* done, uint64_t* configs) {
+  if (!x || !done || !configs) return S2LC_EINVAL;
+  return dist_x_end(x->d, done, configs, x->ctx->err);
+}
+
 int s2lc_dist_frontier_pack(s2lc_dist* x, void* buf) {
   if (!x || (!buf && x->d.nf)) return S2LC_EINVAL;
   return dist_frontier_pack(x->d, (uint8_t*)buf, x->ctx->err);
@@ -1102,6 +1137,7 @@ int s2lc_dist_info(const s2lc_dist* x, s2lc_dist_info_t* out) {
   out->max_frontier = d.max_frontier;
   out->device_ms = d.ms;
   out->trace_len = d.tnext;
+  out->frontier_cap = d.b.lv.scap;
   return 0;
 }
 

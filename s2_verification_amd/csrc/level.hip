@@ -38,7 +38,7 @@ namespace {
     }                                                                    \
   } while (0)
 
-enum LvKernel { LK_ROUND = 0, LK_INSERT, LK_BUCKET, LK_SCATTER, LK_KEEP, LK_GATHER, LK_CLOSE };
+enum LvKernel { LK_ROUND = 0, LK_INSERT, LK_BUCKET, LK_SCATTER, LK_KEEP, LK_GATHER, LK_CLOSE, LK_XSEND };
 
 size_t lv_cfg_bytes(uint32_t nq) { return 128 + 128 * (size_t)nq; }
 
@@ -54,6 +54,7 @@ hipError_t lv_launch(int which, uint32_t grid, const LvParams& p, hipStream_t st
     case LK_SCATTER: hipLaunchKernelGGL(lv_scatter<NQ>, dim3(grid), dim3(LV_BLOCK), 0, st, p); break;
     case LK_KEEP: hipLaunchKernelGGL(lv_keep<NQ>, dim3(grid), dim3(LV_BLOCK), 0, st, p, (uint32_t)(p.tgid >> 29)); break;
     case LK_GATHER: hipLaunchKernelGGL(lv_gather_frontier<NQ>, dim3(grid), dim3(LV_BLOCK), 0, st, p); break;
+    case LK_XSEND: hipLaunchKernelGGL(lv_xsend<NQ>, dim3(grid), dim3(LV_BLOCK), 0, st, p); break;
     default: hipLaunchKernelGGL(lv_close_kernel, dim3(1), dim3(1), 0, st, p); break;
   }
   return hipGetLastError();
@@ -632,6 +633,14 @@ int dist_create(DistLevel& d, const History* h, uint32_t rank, uint32_t world, u
 }
 
 void dist_release(DistLevel& d) {
+  if (d.xrun) (void)hipFree(d.xrun);
+  if (d.xstat) (void)hipHostFree(d.xstat);
+  for (hipEvent_t& e : d.xev) {
+    if (e) (void)hipEventDestroy(e);
+    e = nullptr;
+  }
+  d.xrun = nullptr;
+  d.xstat = nullptr;
   if (d.snap) (void)hipFree(d.snap);
   d.snap = nullptr;
   d.snap_cap = 0;
@@ -759,6 +768,163 @@ int dist_insert(DistLevel& d, uint8_t* recv, uint64_t n_recv, uint64_t* n_next, 
   d.max_frontier = std::max<uint64_t>(d.max_frontier, hc->nnext);
   d.round++;
   *n_next = hc->nnext;
+  return 0;
+}
+
+// ---- host-free partitioned rounds -------------------------------------------
+// The caller queues rounds back to back with no host synchronization:
+//   dist_x_send(send, cap)  expand + close this rank's frontier (lv_round) and
+//                           copy the staged children into fixed-capacity
+//                           blocks, one per owner, header first (lv_xsend)
+//   (caller)                equal-split all-to-all of the blocks
+//   dist_x_recv(recv, cap)  decide the round from the received headers, then
+//                           insert what this rank received (lv_insert, xcap
+//                           mode); the last block closes the round and
+//                           publishes its status to the host-mapped ring
+// and reads a round's status with dist_x_wait a round or two later. Every
+// rank decides the same from the same headers: found (Ok), nothing staged
+// anywhere (Illegal), staging overflow on any rank (abort), or a block over
+// its capacity (nothing inserted: dist_x_rewind(round) and re-run it with a
+// larger cap). A stopped run turns the rounds queued after it into no-ops.
+// S2LC_XSYNC=1 (diagnostics): wait after every queued step, so a fault is
+// reported by the call that queued it
+static const bool g_xsync = getenv("S2LC_XSYNC") != nullptr;
+
+static int dist_x_alloc(DistLevel& d, std::string& err) {
+  if (d.xrun) return 0;
+  LVCHK(hipMalloc(&d.xrun, sizeof(LvRun)));
+  LVCHK(hipHostMalloc(&d.xstat, LV_XRING * sizeof(LvXStat), hipHostMallocMapped));
+  for (hipEvent_t& e : d.xev) LVCHK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+  return 0;
+}
+
+int dist_x_begin(DistLevel& d, std::string& err) {
+  if (d.round == 0) { err = "partitioned rounds start after round 0"; return S2LC_EINVAL; }
+  if (dist_x_alloc(d, err)) return S2LC_EHIP;
+  LvRun R;
+  memset(&R, 0, sizeof R);
+  R.round = d.round;
+  R.nf = d.nf;
+  R.tnext = d.tnext;
+  R.witness = d.tnext + d.b.lv.scap <= d.trace_cap ? 1u : 0u;
+  R.found_parent = TRACE_NONE;
+  R.found_move = LV_NONE;
+  R.deep_trace = TRACE_NONE;
+  R.last_tbase = TRACE_NONE;
+  LVCHK(hipMemcpyAsync(d.xrun, &R, sizeof R, hipMemcpyHostToDevice, d.stream));
+  // the owner counters start at zero (lv_xsend's last block clears them for
+  // the round after; the sized rounds leave them counted)
+  LVCHK(hipMemsetAsync(d.own_cnt, 0, 8 * sizeof(uint32_t), d.stream));
+  LVCHK(hipStreamSynchronize(d.stream));
+  LvXStat* x = reinterpret_cast<LvXStat*>(d.xstat);
+  for (uint32_t i = 0; i < LV_XRING; ++i) x[i].round = 0xFFFFFFFFu;
+  d.xround = d.round + 1;
+  return 0;
+}
+
+static LvParams dist_x_params(DistLevel& d, uint32_t cap) {
+  LvParams p = dist_params(d);
+  p.run = reinterpret_cast<LvRun*>(d.xrun);
+  p.xcap = cap;
+  p.round = d.xround;
+  return p;
+}
+
+int dist_x_send(DistLevel& d, uint8_t* send, uint32_t cap, std::string& err) {
+  if (!d.xrun) { err = "dist_x_begin first"; return S2LC_EINVAL; }
+  if (cap == 0 || !send) { err = "exchange capacity 0 / null send buffer"; return S2LC_EINVAL; }
+  hipStream_t st = d.stream;
+  LvParams p = dist_x_params(d, cap);
+  p.f0 = 0;
+  p.f1 = LV_NONE;  // the frontier size lives on the device
+  p.clear_slots = 1;
+  p.send = send;
+  const uint32_t max_grid = (uint32_t)n_cus(err) * 8;
+  LVCHK(hipMemsetAsync(p.ctl, 0, sizeof(LvCtl), st));
+  LVCHK(lv_dispatch(d.nq, LK_ROUND, d.b.lv.grid_round, p, st));
+  LVCHK(lv_dispatch(d.nq, LK_XSEND, max_grid / 2, p, st));
+  // on a stream of its own the caller's collective is not ordered after these
+  // kernels on the device: the host waits (the gloo tests; one process per
+  // GPU passes its stream and queues with no wait)
+  if (d.own_stream || g_xsync) LVCHK(hipStreamSynchronize(st));
+  return 0;
+}
+
+int dist_x_recv(DistLevel& d, uint8_t* recv, uint32_t cap, uint32_t* round, std::string& err) {
+  if (!d.xrun) { err = "dist_x_begin first"; return S2LC_EINVAL; }
+  if (cap == 0 || !recv) { err = "exchange capacity 0 / null receive buffer"; return S2LC_EINVAL; }
+  const uint64_t slots = (uint64_t)d.world * (cap + 1);
+  // (what one round inserts stays within the next frontier's index list, and
+  // the device stops recording the trace before the pool fills)
+  if ((uint64_t)d.world * cap > d.b.lv.scap) { err = "exchange blocks exceed the frontier capacity"; return S2LC_ENOMEM; }
+  hipStream_t st = d.stream;
+  const uint32_t r = d.xround % LV_XRING;
+  d.xcur[r] = d.cur;
+  d.xsel[r] = d.cur_sel;
+  const int sel = d.cur_sel ^ 1;
+  LvParams p = dist_x_params(d, cap);
+  p.stg = recv;
+  p.nxt_idx = d.b.lv.idx[sel];
+  p.dense = (uint32_t)slots;
+  p.close_round = 1;
+  void* xs = nullptr;
+  LVCHK(hipHostGetDevicePointer(&xs, d.xstat, 0));
+  p.xstat = reinterpret_cast<LvXStat*>(xs);
+  const uint32_t max_grid = (uint32_t)n_cus(err) * 8;
+  LVCHK(lv_dispatch(d.nq, LK_INSERT, (uint32_t)std::min<uint64_t>(max_grid, (slots + LV_BLOCK - 1) / LV_BLOCK), p, st));
+  LVCHK(hipEventRecord(d.xev[r], st));
+  if (g_xsync) LVCHK(hipStreamSynchronize(st));
+  if (round) *round = d.xround;
+  d.cur = recv;
+  d.cur_sel = sel;
+  d.xround++;
+  return 0;
+}
+
+int dist_x_wait(DistLevel& d, uint32_t round, DistXStat* out, std::string& err) {
+  if (!d.xrun || round >= d.xround || round + LV_XRING < d.xround) {
+    err = "round not queued (or no longer in the status ring)";
+    return S2LC_EINVAL;
+  }
+  LVCHK(hipEventSynchronize(d.xev[round % LV_XRING]));
+  const volatile LvXStat* x = reinterpret_cast<const volatile LvXStat*>(d.xstat) + round % LV_XRING;
+  out->ran = x->round == round ? 1u : 0u;
+  out->done = out->ran ? x->done : 0u;
+  out->nf = x->nf;
+  out->maxblk = x->maxblk;
+  out->nf_global = x->nf_global;
+  out->staged = x->staged;
+  return 0;
+}
+
+int dist_x_rewind(DistLevel& d, uint32_t round, std::string& err) {
+  if (!d.xrun || round >= d.xround || round + LV_XRING < d.xround) {
+    err = "round not queued (or no longer in the status ring)";
+    return S2LC_EINVAL;
+  }
+  LVCHK(hipStreamSynchronize(d.stream));
+  d.cur = d.xcur[round % LV_XRING];
+  d.cur_sel = d.xsel[round % LV_XRING];
+  d.xround = round;
+  const uint32_t zero = LVR_RUNNING;
+  LVCHK(hipMemcpy(d.xrun, &zero, sizeof zero, hipMemcpyHostToDevice));  // (LvRun::done)
+  return 0;
+}
+
+int dist_x_end(DistLevel& d, uint32_t* done, uint64_t* configs, std::string& err) {
+  if (!d.xrun) { err = "dist_x_begin first"; return S2LC_EINVAL; }
+  LVCHK(hipStreamSynchronize(d.stream));
+  LvRun R;
+  LVCHK(hipMemcpy(&R, d.xrun, sizeof R, hipMemcpyDeviceToHost));
+  d.round = R.round;
+  d.nf = R.done ? 0u : R.nf;
+  d.tnext = R.tnext;
+  d.configs += R.configs;
+  d.children += R.children;
+  d.max_frontier = std::max<uint64_t>(d.max_frontier, R.max_frontier);
+  if (R.done == LVR_FOUND) { d.found_parent = R.found_parent; d.found_move = R.found_move; d.found_p4 = R.found_p4; }
+  *done = R.done;
+  *configs = R.configs;
   return 0;
 }
 

@@ -78,7 +78,8 @@ struct LvCtl {
   unsigned long long children;  // children generated this round
   unsigned long long prof_end;  // S2LC_PROF: latest expansion end of the round (wall clock)
   uint32_t stop;      // lv_persist: the run's deadline passed (set by workgroup 0 before the round's barrier)
-  uint32_t _pad[3];
+  uint32_t xblocks;   // lv_xsend blocks finished (the last one writes the exchange headers)
+  uint32_t _pad[2];
   uint32_t lo[LV_STRIPES];        // lv_insert: first slot of each stripe not inserted yet (chunked rounds)
   uint32_t cnt[LV_STRIPES * 16];  // stripe s reserves slots at cnt[16 s] (holes included)
 };
@@ -162,6 +163,11 @@ struct LvParams {
   uint32_t* own_pos;     // per staged configuration: owner << 27 | position within the owner's bucket
   uint8_t* send;         // bucketed configurations, owner-major
   uint64_t own_off[8];   // first configuration of each owner's bucket in send
+  // host-free partitioned rounds: fixed-capacity exchange blocks (xcap
+  // configurations per owner, header in the block's first slot; 0 = the
+  // variable-size buckets above) and the host-mapped status ring
+  uint32_t xcap;
+  struct LvXStat* xstat;
   unsigned long long* prof;  // S2LC_PROF builds: lv_round phase cycles (nullable)
   // per-op longest partial linearizations (s2lc_check_partials): for every
   // inserted configuration c and chain j, pmax[cs[j] + cnt_c[j]] = max of
@@ -1155,14 +1161,74 @@ __device__ __forceinline__ void lv_close_round(const LvParams& p) {
   if (p.publish && (p.publish_always || R.done)) lv_publish(R, p.publish);
 }
 
+// ---- fixed-capacity exchange blocks (host-free partitioned rounds; the kernels
+// that fill and read them follow lv_scatter) ----
+struct LvXHdr {
+  uint32_t count;     // configurations the sender staged for this block's owner (> xcap: overflow)
+  uint32_t maxblk;    // the sender's largest block this round
+  uint32_t found, fpar, fmov, fp4;  // a closed child completed (Ok) on the sender
+  uint32_t sovf;      // the sender's staging overflowed (the round is incomplete)
+  uint32_t nf;        // the frontier the sender expanded this round
+  unsigned long long staged;  // the sender's staged configurations, all owners
+};
+struct LvXStat {       // one per round in a ring of LV_XRING (host-mapped)
+  uint32_t round;      // written last: the entry is complete when it equals the round
+  uint32_t done;       // LVR_* once the search stopped in this round (0: running)
+  uint32_t nf;         // this rank's next frontier
+  uint32_t maxblk;     // the largest block of any sender: the capacity this round needed
+  unsigned long long nf_global;  // the global frontier this round expanded
+  unsigned long long staged;     // configurations staged this round, all ranks
+  uint32_t found_parent, found_move, found_p4, _pad;
+};
+constexpr uint32_t LV_XRING = 8;
+
+template <int NQ>
+__device__ __forceinline__ LvXHdr* lv_xhdr(uint8_t* buf, uint32_t o, uint32_t cap) {
+  return reinterpret_cast<LvXHdr*>(buf + (size_t)o * (cap + 1) * sizeof(LCfg<NQ>));
+}
+
+struct LvXDecision {
+  uint32_t halt;      // LVR_* (0: insert the round)
+  uint32_t maxblk;
+  uint32_t fpar, fmov, fp4;
+  unsigned long long nf_global, staged;
+};
+template <int NQ>
+__device__ __forceinline__ LvXDecision lv_xdecide(const LvParams& p);
+template <int NQ>
+__device__ __forceinline__ void lv_xhalt(const LvParams& p, const LvXDecision& d);
+template <int NQ>
+__device__ __forceinline__ void lv_xclose(const LvParams& p);
+
 // ---- insert: one lane per staged configuration -----------------------------
 // Striped staging: lane l of every wave walks stripe l (slot l * scs + i for
 // i = lo[l] .. cnt[l]); the grid strides over i. Winners take next-frontier
-// positions with one atomic per block.
+// positions with one atomic per block. Dense mode (p.dense): configurations
+// 0 .. dense-1 of p.stg (a distributed receive; with p.xcap, exchange blocks).
 template <int NQ>
 __global__ __launch_bounds__(LV_BLOCK) void lv_insert(LvParams p) {
-  if (p.run && p.run->done) return;
   __shared__ uint32_t s_wcnt[LV_BLOCK / 64], s_base, s_hi, s_last;
+  if (p.xcap) {
+    // exchanged round: every block takes the round's decision from the
+    // received headers; a halting round inserts nothing (block 0 records it).
+    // One thread reads the run state for the whole block: block 0 may stop
+    // the run while other blocks start, and every wave of a block must leave
+    // or stay together
+    __shared__ uint32_t s_halt;
+    if (threadIdx.x == 0) {
+      uint32_t h = p.run->done ? LVR_ABORT : 0u;  // (stopped in an earlier round)
+      if (!h) {
+        const LvXDecision d = lv_xdecide<NQ>(p);
+        h = d.halt;
+        if (h && blockIdx.x == 0) lv_xhalt<NQ>(p, d);
+      }
+      s_halt = h;
+    }
+    __syncthreads();
+    if (s_halt) return;
+  } else if (p.run && p.run->done) {
+    return;
+  }
   const int lane = (int)(threadIdx.x & 63), wv = (int)(threadIdx.x >> 6);
   const bool wit = p.run ? p.run->witness != 0 : p.witness_host != 0;
   const uint32_t tbase = p.run ? (uint32_t)p.run->tnext : p.tbase_host;
@@ -1191,6 +1257,10 @@ __global__ __launch_bounds__(LV_BLOCK) void lv_insert(LvParams p) {
     if (p.dense) {
       k = itb * LV_BLOCK + threadIdx.x;
       valid = k < p.dense;
+      if (valid && p.xcap) {  // exchange blocks: slot 0 is the header, then the block's count
+        const uint32_t b = k / (p.xcap + 1), i = k - b * (p.xcap + 1);
+        valid = i >= 1 && i - 1 < min(lv_xhdr<NQ>(p.stg, b, p.xcap)->count, p.xcap);
+      }
     } else {
       const uint32_t i = itb * (LV_BLOCK / 64) + (uint32_t)wv;
       valid = i >= lo && i < hi;
@@ -1246,7 +1316,10 @@ __global__ __launch_bounds__(LV_BLOCK) void lv_insert(LvParams p) {
   __syncthreads();
   if (threadIdx.x == 0) s_last = atomicAdd(&p.ctl->done_blocks, 1u) == gridDim.x - 1;
   __syncthreads();
-  if (s_last && threadIdx.x == 0) lv_close_round(p);
+  if (s_last && threadIdx.x == 0) {
+    if (p.xcap) lv_xclose<NQ>(p);
+    else lv_close_round(p);
+  }
 }
 
 // ---- persistent narrow rounds ---------------------------------------------
@@ -1496,6 +1569,147 @@ __global__ __launch_bounds__(LV_BLOCK) void lv_scatter(LvParams p) {
     const uint4* src = reinterpret_cast<const uint4*>(lv_cfg<NQ>(p.stg, slot));
     reinterpret_cast<uint4*>(p.send + dst * sizeof(LCfg<NQ>))[c] = src[c];
   }
+}
+
+// ---- host-free partitioned rounds (distributed.py) ---------
+// Every rank sends every other rank a block of fixed capacity (xcap
+// configurations) through one equal-split all-to-all, so no size travels to
+// the host. Block o of a send buffer is sizeof(LCfg) * (xcap + 1) bytes: an
+// LvXHdr in slot 0, then the configurations this rank staged for owner o.
+// Every header carries what all ranks need to take the same decision after
+// the exchange (found, the largest block, staging overflow, the staged
+// total), so termination and capacity overflow are decided on the device,
+// identically on every rank, and published to a host-mapped status ring the
+// host reads a round or two behind while the next rounds are already queued.
+
+// stripe walk bound of the round's staging (64 x the longest stripe), from
+// the device counters (every wave computes it)
+__device__ __forceinline__ uint32_t lv_stage_dense(const LvParams& p) {
+  const uint32_t lane = threadIdx.x & 63;
+  return 64u * wave_max_u32(min(ld_agent(&p.ctl->cnt[16 * lane]), p.scs));
+}
+
+// stage -> fixed-capacity blocks: one wave per 64 staging slots (lane = stripe)
+// takes owner positions with atomics, then copies each of its configurations
+// cooperatively (16 bytes per lane); the last block writes the headers and
+// clears the owner counters for the next round
+template <int NQ>
+__global__ __launch_bounds__(LV_BLOCK) void lv_xsend(LvParams p) {
+  if (p.run->done) return;
+  __shared__ uint32_t s_last;
+  constexpr uint32_t PER = sizeof(LCfg<NQ>) / 16;
+  const uint32_t lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  const uint32_t dense = lv_stage_dense(p), cap = p.xcap;
+  const uint4* src = reinterpret_cast<const uint4*>(p.stg);
+  uint4* dst = reinterpret_cast<uint4*>(p.send);
+  for (uint32_t k0 = (blockIdx.x * (LV_BLOCK / 64) + wv) * 64; k0 < dense; k0 += gridDim.x * LV_BLOCK) {
+    const uint32_t i = k0 / 64, slot = lane * p.scs + i;
+    bool v = i < min(ld_agent(&p.ctl->cnt[16 * lane]), p.scs);
+    uint32_t to = 0;
+    if (v) {
+      const LCfg<NQ>* c = lv_cfg<NQ>(p.stg, slot);
+      v = c->move != LV_HOLE;
+      if (v) {
+        const uint32_t o = lv_owner(c->fp, p.world);
+        const uint32_t pos = atomicAdd(&p.own_cnt[o], 1u);
+        v = pos < cap;
+        to = o * (cap + 1) + 1 + pos;
+      }
+    }
+    for (uint64_t m = __ballot(v); m; m &= m - 1) {
+      const int l = __ffsll((unsigned long long)m) - 1;
+      const uint32_t d = (uint32_t)__shfl((int)to, l, 64), sl = (uint32_t)__shfl((int)slot, l, 64);
+      for (uint32_t c = lane; c < PER; c += 64) dst[(size_t)d * PER + c] = src[(size_t)sl * PER + c];
+    }
+  }
+  __threadfence();
+  __syncthreads();
+  if (threadIdx.x == 0) s_last = atomicAdd(&p.ctl->xblocks, 1u) == gridDim.x - 1;
+  __syncthreads();
+  if (!s_last || threadIdx.x >= 64) return;
+  const uint32_t c = lane < p.world ? atomicExch(&p.own_cnt[lane], 0u) : 0u;
+  const uint32_t mb = wave_max_u32(c);
+  unsigned long long tot = c;
+  for (int d = 32; d >= 1; d >>= 1) tot += __shfl_xor(tot, d, 64);
+  if (lane < p.world) {
+    LvXHdr h;
+    h.count = c; h.maxblk = mb;
+    h.found = ld_agent(&p.ctl->found);
+    h.fpar = ld_agent(&p.ctl->found_parent); h.fmov = ld_agent(&p.ctl->found_move);
+    h.fp4 = ld_agent(&p.ctl->found_p4);
+    h.sovf = ld_agent(&p.ctl->overflow);
+    h.nf = p.run->nf;
+    h.staged = tot;
+    *lv_xhdr<NQ>(p.send, lane, cap) = h;
+  }
+}
+
+// the decision of an exchanged round, from the received headers (every rank
+// reads the same values, so every rank decides the same)
+template <int NQ>
+__device__ __forceinline__ LvXDecision lv_xdecide(const LvParams& p) {
+  LvXDecision d;
+  d.halt = 0; d.maxblk = 0; d.fpar = TRACE_NONE; d.fmov = LV_NONE; d.fp4 = 0; d.nf_global = 0; d.staged = 0;
+  bool found = false, sovf = false;
+  for (uint32_t s = 0; s < p.world; ++s) {
+    const LvXHdr* h = lv_xhdr<NQ>(const_cast<uint8_t*>(p.stg), s, p.xcap);
+    d.maxblk = max(d.maxblk, h->maxblk);
+    d.nf_global += h->nf;
+    d.staged += h->staged;
+    sovf |= h->sovf != 0;
+    if (h->found && !found) { found = true; d.fpar = h->fpar; d.fmov = h->fmov; d.fp4 = h->fp4; }
+  }
+  d.halt = found ? LVR_FOUND : sovf ? LVR_ABORT : d.maxblk > p.xcap ? LVR_OVERFLOW : d.staged == 0 ? LVR_EMPTY : 0u;
+  return d;
+}
+
+// publish round p.round's status to the host-mapped ring (the round last)
+__device__ __forceinline__ void lv_xpublish(const LvParams& p, const LvRun& R, const LvXDecision& d) {
+  volatile LvXStat* x = p.xstat + (p.round % LV_XRING);
+  x->done = R.done; x->nf = R.nf; x->maxblk = d.maxblk;
+  x->nf_global = d.nf_global; x->staged = d.staged;
+  x->found_parent = R.found_parent; x->found_move = R.found_move; x->found_p4 = R.found_p4;
+  __threadfence_system();
+  x->round = p.round;
+  __threadfence_system();
+}
+
+// a halting exchanged round (block 0 of lv_insert): the run stops, nothing inserted
+template <int NQ>
+__device__ __forceinline__ void lv_xhalt(const LvParams& p, const LvXDecision& d) {
+  LvRun& R = *p.run;
+  R.done = d.halt;
+  if (d.halt == LVR_FOUND) {
+    R.round = p.round;
+    R.found_parent = R.witness ? d.fpar : TRACE_NONE;
+    R.found_move = d.fmov;
+    R.found_p4 = d.fp4;
+  } else if (d.halt == LVR_EMPTY) {
+    R.round = p.round;
+  }
+  lv_xpublish(p, R, d);
+}
+
+// the close of an exchanged round (the last lv_insert block): this rank's
+// share of the next frontier
+template <int NQ>
+__device__ __forceinline__ void lv_xclose(const LvParams& p) {
+  const LvCounts k = lv_read_counts(p.ctl);
+  const LvXDecision d = lv_xdecide<NQ>(p);
+  LvRun& R = *p.run;
+  R.children += k.ch;
+  R.last_nf = R.nf;
+  R.last_closed = k.closed;
+  R.nf = k.nn;
+  R.round = p.round;
+  R.configs += k.nn;
+  R.max_frontier = max(R.max_frontier, k.nn);
+  if (R.witness) {
+    R.last_tbase = (uint32_t)R.tnext;
+    R.tnext += k.nn;
+    if (R.tnext + p.scap > p.trace_cap) R.witness = 0;
+  }
+  lv_xpublish(p, R, d);
 }
 
 // keep the frontier configurations this rank owns (replicated -> partitioned)

@@ -257,6 +257,15 @@ struct DistLevel {
   double ms = 0;
   uint8_t* snap = nullptr;       // the frontier entering persistent replicated rounds (restored if they abort)
   size_t snap_cap = 0;
+  // host-free partitioned rounds (dist_x_*): device run state, host-mapped
+  // status ring, one event per ring entry, and the frontier each queued round
+  // started from (a capacity overflow re-runs that round)
+  void* xrun = nullptr;
+  void* xstat = nullptr;
+  hipEvent_t xev[8] = {};
+  const uint8_t* xcur[8] = {};
+  int xsel[8] = {};
+  uint32_t xround = 0;           // the next round to queue
 };
 int dist_create(DistLevel& d, const History* h, uint32_t rank, uint32_t world, uint32_t reductions_off,
                 hipStream_t stream, std::string& err);
@@ -270,6 +279,13 @@ int dist_local_run(DistLevel& d, uint32_t wide, uint64_t* n_next, int* found, ui
 int dist_keep_owned(DistLevel& d, uint64_t* n_kept, std::string& err);
 int dist_frontier_pack(DistLevel& d, uint8_t* buf, std::string& err);
 int dist_frontier_load(DistLevel& d, uint8_t* buf, uint64_t n, std::string& err);
+struct DistXStat { uint32_t ran, done, nf, maxblk; uint64_t nf_global, staged; };
+int dist_x_begin(DistLevel& d, std::string& err);
+int dist_x_send(DistLevel& d, uint8_t* send, uint32_t cap, std::string& err);
+int dist_x_recv(DistLevel& d, uint8_t* recv, uint32_t cap, uint32_t* round, std::string& err);
+int dist_x_wait(DistLevel& d, uint32_t round, DistXStat* out, std::string& err);
+int dist_x_rewind(DistLevel& d, uint32_t round, std::string& err);
+int dist_x_end(DistLevel& d, uint32_t* done, uint64_t* configs, std::string& err);
 
 // Host reconstruction of a full linearization (dense op ids) from the device
 // move list; returns false if any move is not a legal successor.

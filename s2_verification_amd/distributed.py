@@ -25,7 +25,8 @@ import numpy as np
 import torch
 import torch.distributed as dist
 
-from . import History, Ok, Illegal, S2LCError, c_dist_info, lib
+from . import (DIST_X_ABORT, DIST_X_CAPACITY, DIST_X_EMPTY, DIST_X_FOUND, History, Illegal, Ok, S2LCError,
+               c_dist_info, c_dist_xstat, lib)
 
 _NONE = 0xFFFFFFFF
 _RANK_SHIFT = 29
@@ -44,6 +45,8 @@ class DistResult:
     witness: Optional[List[int]] = None
     witness_valid: Optional[bool] = None
     per_rank_configs: List[int] = field(default_factory=list)  # [partitioned rounds]
+    xreruns: int = 0         # partitioned rounds re-run with larger exchange blocks
+    part_s: float = 0.0      # wall time of the partitioned rounds (the switches to them included)
 
 
 class DistSearch:
@@ -127,6 +130,33 @@ class DistSearch:
     def frontier_load(self, buf: torch.Tensor, n: int):
         self._chk(lib().s2lc_dist_frontier_load(self._d, ctypes.c_void_p(buf.data_ptr()), n), "dist_frontier_load")
 
+    # host-free partitioned rounds (s2lc_dist_x_*, include/s2lincheck.h)
+    def x_begin(self):
+        self._chk(lib().s2lc_dist_x_begin(self._d), "dist_x_begin")
+
+    def x_send(self, send: torch.Tensor, cap: int):
+        self._chk(lib().s2lc_dist_x_send(self._d, ctypes.c_void_p(send.data_ptr()), cap), "dist_x_send")
+
+    def x_recv(self, recv: torch.Tensor, cap: int) -> int:
+        r = ctypes.c_uint32(0)
+        self._chk(lib().s2lc_dist_x_recv(self._d, ctypes.c_void_p(recv.data_ptr()), cap, ctypes.byref(r)),
+                  "dist_x_recv")
+        return r.value
+
+    def x_wait(self, round_: int) -> c_dist_xstat:
+        st = c_dist_xstat()
+        self._chk(lib().s2lc_dist_x_wait(self._d, round_, ctypes.byref(st)), "dist_x_wait")
+        return st
+
+    def x_rewind(self, round_: int):
+        self._chk(lib().s2lc_dist_x_rewind(self._d, round_), "dist_x_rewind")
+
+    def x_end(self):
+        done = ctypes.c_uint32(0)
+        configs = ctypes.c_uint64(0)
+        self._chk(lib().s2lc_dist_x_end(self._d, ctypes.byref(done), ctypes.byref(configs)), "dist_x_end")
+        return done.value, configs.value
+
     def trace(self) -> np.ndarray:
         n = ctypes.c_uint64(0)
         self._chk(lib().s2lc_dist_trace(self._d, None, 0, ctypes.byref(n)), "dist_trace")
@@ -152,7 +182,7 @@ class _Exchange:
         self.same_stream = lib_stream != 0 and lib_stream == torch.cuda.current_stream(device).cuda_stream
 
     def _lib_sync(self):
-        if not self.same_stream:
+        if not self.same_stream and self.device.type == "cuda":
             torch.cuda.current_stream(self.device).synchronize()  # the library reads on its own stream
 
     def counts(self, counts, found: bool, staged: int, frontier: int = 0):
@@ -177,6 +207,21 @@ class _Exchange:
         recv_h = torch.empty(total, dtype=torch.uint8)
         dist.all_to_all_single(recv_h, send.cpu(), out_bytes, in_bytes, group=self.group)
         recv = recv_h.to(self.device) if total else torch.empty(1, dtype=torch.uint8, device=self.device)
+        self._lib_sync()
+        return recv
+
+    def payload_fixed(self, send: torch.Tensor) -> torch.Tensor:
+        """Equal-split all-to-all of `world` fixed-capacity blocks: no sizes
+        on the host. On CUDA tensors (RCCL) it is queued behind the library's
+        kernels on the same stream with no host synchronization."""
+        if self.on_gpu:
+            recv = torch.empty_like(send)
+            dist.all_to_all_single(recv, send, group=self.group)
+            self._lib_sync()
+            return recv
+        recv_h = torch.empty(send.numel(), dtype=torch.uint8)
+        dist.all_to_all_single(recv_h, send.cpu(), group=self.group)
+        recv = recv_h.to(self.device)
         self._lib_sync()
         return recv
 
@@ -238,9 +283,119 @@ def _walk(traces: List[np.ndarray], parent: int, move: int) -> Optional[List[int
     return moves
 
 
+def bind_stream(device=None) -> int:
+    """Make a dedicated torch stream current and return its handle, for
+    Checker(stream=...): the library's kernels and the RCCL collectives are
+    then ordered on the device, and partitioned rounds queue with no host
+    synchronization. (The default stream's handle is 0, which the C ABI reads
+    as "a stream of your own": the rounds then wait on the host.)"""
+    s = torch.cuda.Stream(device=device)
+    torch.cuda.set_stream(s)
+    return s.cuda_stream
+
+
+_XDEPTH = 2      # partitioned rounds queued beyond the newest status the host has read
+_XDEBUG = bool(int(__import__("os").environ.get("S2LC_XDEBUG", "0") or 0))  # (diagnostics: every round's status)
+_XRING = 8       # the library's status ring (LV_XRING): receive buffers a re-run may read
+
+
+def _xcap(n: int, limit: int) -> int:
+    """Exchange block capacity for an expected largest block of n: twice it,
+    a power of two (a round that needs more is re-run), within the limit."""
+    c = 256
+    while c < 2 * n:
+        c *= 2
+    return max(1, min(c, limit))
+
+
+@dataclass
+class _XPhase:
+    stop: int = 0          # DIST_X_* of the stop (0: the frontier narrowed)
+    rounds: int = 0        # rounds closed in the phase (the stopping one included)
+    sent_bytes: int = 0
+    reruns: int = 0        # rounds re-run with a larger block capacity
+    cap: int = 0           # the last block capacity
+    bufs: list = field(default_factory=list)  # receive buffers; the last holds the frontier (keep it alive)
+
+
+def _partitioned_rounds(ds: "DistSearch", ex: "_Exchange", device, cb: int, world: int, wide: int,
+                        cap: int) -> _XPhase:
+    """Partitioned rounds with no host synchronization per round
+    (s2lc_dist_x_*): each round is queued as expand + block copy, one
+    equal-split all-to-all of fixed-capacity blocks, and the decision +
+    insert, and the host reads round r's status (the largest block it needed,
+    the global frontier, the stop) while rounds r+1 .. r+_XDEPTH are queued
+    behind it. A block over its capacity inserts nothing on any rank: the
+    round is re-run with twice the largest block. The phase ends at a stop or
+    when the global frontier narrows below wide / 4."""
+    from collections import deque
+    info = ds.info()
+    limit = max(1, int(info.frontier_cap) // world)
+    round0 = info.round
+    ph = _XPhase(cap=min(cap, limit))
+    ds.x_begin()
+    if _XDEBUG:
+        print(f"[x] rank {ds.rank} phase from round {round0} frontier {info.frontier} cap {ph.cap} "
+              f"limit {limit}", flush=True)
+    queued = deque()                 # rounds whose status is not read yet
+    keep = deque(maxlen=_XRING + 1)  # receive buffers a re-run may start from
+    while True:
+        send = torch.empty(world * (ph.cap + 1) * cb, dtype=torch.uint8, device=device)
+        if _XDEBUG:
+            print(f"[x] rank {ds.rank} queue cap {ph.cap} send {send.data_ptr():#x}+{send.numel()}", flush=True)
+        ds.x_send(send, ph.cap)
+        recv = ex.payload_fixed(send)
+        r = ds.x_recv(recv, ph.cap)
+        if _XDEBUG:
+            print(f"[x] rank {ds.rank} queued round {r} recv {recv.data_ptr():#x}+{recv.numel()}", flush=True)
+        queued.append(r)
+        keep.append(recv)
+        ph.sent_bytes += (world - 1) * (ph.cap + 1) * cb
+        if len(queued) <= _XDEPTH:
+            continue
+        r0 = queued.popleft()
+        st = ds.x_wait(r0)
+        if _XDEBUG:
+            print(f"[x] rank {ds.rank} round {r0} cap {ph.cap} ran {st.ran} done {st.done} nf {st.nf} "
+                  f"maxblk {st.maxblk} nf_global {st.nf_global} staged {st.staged}", flush=True)
+        if st.done == DIST_X_CAPACITY:
+            if st.maxblk > limit:
+                ds.x_end()
+                raise S2LCError(-5, f"distributed round {r0}: an exchange block of {st.maxblk} configurations "
+                                    f"exceeds the frontier capacity ({limit} per rank)")
+            ds.x_rewind(r0)
+            queued.clear()
+            ph.reruns += 1
+            ph.cap = _xcap(st.maxblk, limit)
+            continue
+        if st.done:
+            break
+        ph.cap = _xcap(st.maxblk, limit)
+        if wide > 0 and r0 > round0 + 1 and st.nf_global < wide // 4:
+            # narrow again. The rounds still queued run to the end of the
+            # phase; one of them may stop the search or outgrow its blocks
+            # (then the phase ends before it: the switch reads the frontier
+            # it started from)
+            for r in queued:
+                st = ds.x_wait(r)
+                if st.done == DIST_X_CAPACITY:
+                    ds.x_rewind(r)
+                    break
+                if st.done:
+                    break
+            break
+    ph.stop, _ = ds.x_end()
+    if ph.stop == DIST_X_ABORT:
+        raise S2LCError(-5, "distributed round exceeds the device buffers")
+    ph.rounds = ds.info().round - round0
+    ph.bufs = list(keep)  # (the library's frontier is the last one queued)
+    return ph
+
+
 def check_distributed(checker, history: History, group=None, witness: bool = True,
                       wide: int = 4096, persistent: Optional[bool] = None,
-                      self_exchange: bool = False) -> DistResult:
+                      self_exchange: bool = False, sized_exchange: bool = False,
+                      xcap0: Optional[int] = None) -> DistResult:
     """Check one history with every rank of `group` (default: the world).
 
     Rounds whose frontier is narrower than `wide` configurations run
@@ -261,7 +416,15 @@ def check_distributed(checker, history: History, group=None, witness: bool = Tru
 
     self_exchange: with one rank, still switch to partitioned rounds at
     `wide` (every child goes through the all-to-all to rank 0 itself): the
-    multi-GPU round sequence, rehearsed on one GPU."""
+    multi-GPU round sequence, rehearsed on one GPU.
+
+    Partitioned rounds run host-free (_partitioned_rounds: fixed-capacity
+    blocks, device-side decisions, no host synchronization per round);
+    sized_exchange=True runs them the round-3 way instead (host-read counts,
+    a variable-split all-to-all, three host synchronizations per round), kept
+    for measurement. xcap0: the first exchange block capacity of each
+    partitioned phase (default: from the frontier at the switch; a smaller one
+    is grown by re-running the rounds that overflow it)."""
     rank = dist.get_rank(group)
     world = dist.get_world_size(group)
     device = torch.device("cuda", torch.cuda.current_device())
@@ -280,6 +443,9 @@ def check_distributed(checker, history: History, group=None, witness: bool = Tru
     phase_rounds = 0  # partitioned rounds since the last switch to them
     nn_local = 0      # this rank's frontier after the last partitioned round (reported with the next counts)
     replicated = wide > 0  # wide = 0: every round partitioned (also on one rank: a self-exchange)
+    nn_switch = 1          # the frontier at the switch to partitioned rounds (sizes the first exchange blocks)
+    xreruns = 0            # partitioned rounds re-run with larger exchange blocks
+    part_s = 0.0
     t0 = time.perf_counter()
     first = True  # round 0 closes the initial configuration; rounds counts the ones after it
     try:
@@ -305,8 +471,58 @@ def check_distributed(checker, history: History, group=None, witness: bool = Tru
                     break
                 if split and nn >= wide:
                     ds.keep_owned()
+                    nn_switch = nn
                     replicated = False
                 continue
+            if not sized_exchange and ds.info().round == 0:
+                # (wide = 0) round 0 closes the initial configuration on every
+                # rank; partitioned rounds start from it
+                nn, found = ds.local_round()
+                if found:
+                    verdict = Ok
+                    break
+                if nn == 0:
+                    verdict = Illegal
+                    break
+                configs += nn
+                ds.keep_owned()
+                nn_switch = nn
+                continue
+            if not sized_exchange:
+                tp = time.perf_counter()
+                c0 = ds.info().configs
+                cap0 = xcap0 if xcap0 else _xcap(max(1024, 4 * nn_switch // world), 1 << 31)
+                ph = _partitioned_rounds(ds, ex, device, cb, world, wide, cap0)
+                keep = ph.bufs  # the frontier lives in the last one until frontier_load replaces it
+                xreruns += ph.reruns
+                rounds += ph.rounds - 1  # (this iteration counted one)
+                part_rounds += ph.rounds
+                sent_bytes += ph.sent_bytes
+                configs += ex.sum(ds.info().configs - c0)
+                part_s += time.perf_counter() - tp
+                if ph.stop == DIST_X_FOUND:
+                    found = True
+                    verdict = Ok
+                    break
+                if ph.stop == DIST_X_EMPTY:
+                    verdict = Illegal
+                    break
+                # narrow again: every rank takes the whole frontier
+                nn = ds.info().frontier
+                sizes_n = [x[0] for x in ex.gather_small([nn])]
+                total = sum(sizes_n)
+                mine = torch.empty(max(1, nn * cb), dtype=torch.uint8, device=device)
+                if nn:
+                    ds.frontier_pack(mine)
+                full = ex.gather_frontier(mine, [x * cb for x in sizes_n])
+                ds.frontier_load(full, total)
+                keep = [full]
+                replicated = True
+                if total == 0:
+                    verdict = Illegal
+                    break
+                continue
+            tp = time.perf_counter()
             counts, found = ds.expand()
             # (the previous round's global frontier travels with this round's
             # counts: no collective of its own; an empty frontier shows up here
@@ -331,6 +547,7 @@ def check_distributed(checker, history: History, group=None, witness: bool = Tru
             keep = [recv]
             part_rounds += 1
             phase_rounds += 1
+            part_s += time.perf_counter() - tp
             if wide > 0 and phase_rounds > 1 and prev_total < wide // 4:
                 # the frontier was narrow a round ago: the exact sizes of this
                 # one (an all-gather the switch needs anyway) decide
@@ -357,7 +574,8 @@ def check_distributed(checker, history: History, group=None, witness: bool = Tru
                                  info.children, info.max_frontier, int(info.device_ms * 1e3)])
         res = DistResult(verdict=verdict, rounds=rounds, configs=configs, children=sum(s[4] for s in stats),
                          max_frontier=max(s[5] for s in stats), device_ms=max(s[6] for s in stats) / 1e3,
-                         wall_s=wall, exchanged_bytes=sent_bytes, per_rank_configs=[part_rounds])
+                         wall_s=wall, exchanged_bytes=sent_bytes, per_rank_configs=[part_rounds],
+                         xreruns=xreruns, part_s=part_s)
         if verdict == Ok and witness:
             src = next(s for s in stats if s[0])
             traces = ex.gather_traces(ds.trace())

@@ -29,30 +29,41 @@ def exchange_worker(rank, world, port, q):
         assert front == sum(100 + r for r in range(world))
         tr = np.array([[0xFFFFFFFF, 0xFFFFFFFF], [(rank << 29) | 0, rank + 1]], dtype=np.uint32)
         traces = ex.gather_traces(tr)
-        q.put((rank, recv, found_any, staged, [t.tolist() for t in traces]))
+        # fixed-capacity blocks (equal split, no sizes): block w of rank r's
+        # send buffer holds bytes (r, w, 0, 1, ...); block s of what rank r
+        # receives is what rank s sent to r
+        blk = 24
+        send = torch.zeros(world * blk, dtype=torch.uint8)
+        for w in range(world):
+            send[w * blk:(w + 1) * blk] = torch.tensor([rank, w] + list(range(blk - 2)), dtype=torch.uint8)
+        got = ex.payload_fixed(send)
+        blocks = [got[s_ * blk:(s_ + 1) * blk].tolist()[:2] for s_ in range(world)]
+        q.put((rank, recv, found_any, staged, [t.tolist() for t in traces], blocks))
         dist.destroy_process_group()
     except Exception:
         q.put((rank, "error", traceback.format_exc()))
 
 
-def search_worker(rank, world, port, backend, names, wide, persistent, self_exchange, q):
+def search_worker(rank, world, port, backend, names, wide, persistent, self_exchange, q, sized=False, xcap0=None):
     """GPU: every rank checks the named histories with check_distributed."""
     try:
         import torch
         import s2_verification_amd as s2
         from s2_verification_amd import workloads as W
-        from s2_verification_amd.distributed import check_distributed
+        from s2_verification_amd.distributed import bind_stream, check_distributed
         torch.cuda.set_device(0 if backend == "gloo" else rank)
         dist = _init(rank, world, port, backend)
         # nccl: the library on torch's stream (no host syncs around the collectives)
         checker = s2.Checker(device=torch.cuda.current_device(),
-                             stream=torch.cuda.current_stream().cuda_stream if backend == "nccl" else 0)
+                             stream=bind_stream() if backend == "nccl" else 0)
         out = []
         for name in names:
             h = W.config_history(name)
-            r = check_distributed(checker, h, wide=wide, persistent=persistent, self_exchange=self_exchange)
+            r = check_distributed(checker, h, wide=wide, persistent=persistent, self_exchange=self_exchange,
+                                  sized_exchange=sized, xcap0=xcap0)
             out.append((name, r.verdict, r.rounds, r.configs, r.witness_valid,
-                        None if r.witness is None else len(r.witness), h.info()["n_ops"]))
+                        None if r.witness is None else len(r.witness), h.info()["n_ops"], r.xreruns,
+                        r.per_rank_configs[0]))
         q.put((rank, out))
         dist.destroy_process_group()
     except Exception:
