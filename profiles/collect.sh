@@ -7,8 +7,8 @@
 #    summarised for pack_kernel<16>                -> gpurun_out/<tag>/pmc_c4.json
 # 4. rocprofv3 --kernel-trace --stats of C5        -> gpurun_out/<tag>/c5stats/
 # Every GPU step has its own time limit; the first failure ends the script.
-# (C5 under rocprofv3: plain persistent launches, S2LC_PERSIST_PLAIN=1 -- the
-# profiler faulted at process exit after cooperative launches, r03)
+# (C5 under rocprofv3: the shipping cooperative launches, with tools/exit_hook.so (S2LC_EXIT_HOOK=1): the
+# HIP runtime's own destructor faults at exit after cooperative launches under the profiler)
 set -euo pipefail
 TAG=${1:-run}
 OUT=gpurun_out/$TAG
@@ -23,5 +23,5 @@ timeout -s KILL 120 rocprofv3 --pmc FETCH_SIZE --output-format csv -d "$OUT/pmc_
 timeout -s KILL 120 rocprofv3 --pmc WRITE_SIZE --output-format csv -d "$OUT/pmc_write" -o c4 -- \
   python3 bench.py $SHORT > "$OUT/pmc_write_bench.json" 2> "$OUT/pmc_write.err"
 python3 profiles/pmc_summary.py "$OUT/pmc_fetch" "$OUT/pmc_write" "$OUT/pmc_c4.json" "pack_kernel<16>" "$OUT/pmc_fetch_bench.json"
-S2LC_PERSIST_PLAIN=1 timeout -k 10 200 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/c5stats" -o c5 -- \
+S2LC_EXIT_HOOK=1 timeout -k 10 200 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/c5stats" -o c5 -- \
   python3 tools/c5run.py C5 > "$OUT/c5run.log" 2> "$OUT/c5stats.err"

@@ -6,8 +6,8 @@
 #   C4 (bench.py, C4 leg only)  -> pack_kernel<16>
 #   C5 (tools/c5run.py C5: cold + warm run) -> lv_persist / lv_round / lv_insert
 # Summaries: python3 profiles/pmc_sq.py gpurun_out/<tag> > profiles/<round>/pmc_sq.json
-# (C5 under rocprofv3: plain persistent launches, S2LC_PERSIST_PLAIN=1 -- the
-# profiler faulted at process exit after cooperative launches, r03)
+# (C5 under rocprofv3: the shipping cooperative launches, with tools/exit_hook.so (S2LC_EXIT_HOOK=1): the
+# HIP runtime's own destructor faults at exit after cooperative launches under the profiler)
 set -euo pipefail
 TAG=${1:-pmc}
 OUT=gpurun_out/$TAG
@@ -20,7 +20,7 @@ pmc() {  # name, workload, counters...
     timeout -s KILL 90 rocprofv3 --pmc "$@" --output-format csv -d "$OUT/$name" -o run -- \
       python3 bench.py $SHORT > "$OUT/$name.out" 2> "$OUT/$name.err"
   else
-    S2LC_PERSIST_PLAIN=1 timeout -s KILL 90 rocprofv3 --pmc "$@" --output-format csv -d "$OUT/$name" -o run -- \
+    S2LC_EXIT_HOOK=1 timeout -s KILL 90 rocprofv3 --pmc "$@" --output-format csv -d "$OUT/$name" -o run -- \
       python3 tools/c5run.py C5 > "$OUT/$name.out" 2> "$OUT/$name.err"
   fi
 }

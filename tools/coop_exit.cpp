@@ -5,7 +5,7 @@
 // backtrace (with the shared object of every frame).
 //   hipcc -O1 -g -I include tools/coop_exit.cpp -o tools/coop_exit \
 //     -L s2_verification_amd -ls2lincheck -Wl,-rpath,$PWD/s2_verification_amd
-//   rocprofv3 --kernel-trace --stats -d gpurun_out/ce -- tools/coop_exit [plain]
+//   rocprofv3 --kernel-trace --stats -d gpurun_out/ce -- tools/coop_exit [plain|reset]
 #include <dlfcn.h>
 #include <execinfo.h>
 #include <signal.h>
@@ -13,6 +13,8 @@
 #include <stdlib.h>
 #include <string.h>
 #include <unistd.h>
+
+#include <hip/hip_runtime_api.h>
 
 #include "s2lincheck.h"
 
@@ -48,6 +50,7 @@ int main(int argc, char** argv) {
   sigaction(SIGSEGV, &sa, nullptr);
   sigaction(SIGBUS, &sa, nullptr);
   atexit(at_exit_mark);
+  const bool reset = argc > 1 && !strcmp(argv[1], "reset");
   if (argc > 1 && !strcmp(argv[1], "plain")) setenv("S2LC_PERSIST_PLAIN", "1", 1);
   s2lc_sim_params sp;
   s2lc_sim_params_default(&sp);
@@ -78,6 +81,10 @@ int main(int argc, char** argv) {
   s2lc_destroy(c);
   fprintf(stderr, "coop_exit: context destroyed\n");
   s2lc_history_free(h);
+  if (reset) {
+    (void)hipDeviceReset();
+    fprintf(stderr, "coop_exit: device reset\n");
+  }
   fprintf(stderr, "coop_exit: returning from main\n");
   return rc ? 4 : 0;
 }
