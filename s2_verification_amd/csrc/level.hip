@@ -819,14 +819,18 @@ int dist_x_begin(DistLevel& d, std::string& err) {
   LvXStat* x = reinterpret_cast<LvXStat*>(d.xstat);
   for (uint32_t i = 0; i < LV_XRING; ++i) x[i].round = 0xFFFFFFFFu;
   d.xround = d.round + 1;
+  d.xfresh = true;
   return 0;
 }
 
+// exchanged round r counts in ctl[r & 1]; its lv_round zeroes ctl[(r + 1) & 1]
+// for the round after (whose last user, round r - 1, has ended)
 static LvParams dist_x_params(DistLevel& d, uint32_t cap) {
   LvParams p = dist_params(d);
   p.run = reinterpret_cast<LvRun*>(d.xrun);
   p.xcap = cap;
   p.round = d.xround;
+  p.ctl = reinterpret_cast<LvCtl*>(d.b.lv.ctl) + (d.xround & 1);
   return p;
 }
 
@@ -839,10 +843,30 @@ int dist_x_send(DistLevel& d, uint8_t* send, uint32_t cap, std::string& err) {
   p.f1 = LV_NONE;  // the frontier size lives on the device
   p.clear_slots = 1;
   p.send = send;
-  const uint32_t max_grid = (uint32_t)n_cus(err) * 8;
-  LVCHK(hipMemsetAsync(p.ctl, 0, sizeof(LvCtl), st));
-  LVCHK(lv_dispatch(d.nq, LK_ROUND, d.b.lv.grid_round, p, st));
-  LVCHK(lv_dispatch(d.nq, LK_XSEND, max_grid / 2, p, st));
+  if (d.xfresh) {  // the first round after x_begin / x_rewind: its counters
+    LVCHK(hipMemsetAsync(p.ctl, 0, sizeof(LvCtl), st));
+    d.xfresh = false;
+  }
+  // grids from the latest status the host can see without waiting (this
+  // rank's frontier after the previous round, when published): a narrow
+  // round gets small grids (any grid is correct; the kernels stride)
+  uint32_t hint_nf = UINT32_MAX;
+  uint64_t hint_staged = UINT64_MAX;
+  {
+    const volatile LvXStat* xs = reinterpret_cast<const volatile LvXStat*>(d.xstat);
+    for (uint32_t back = 1; back <= 2 && back < d.xround; ++back) {
+      const uint32_t r = d.xround - back;
+      const volatile LvXStat& e = xs[r % LV_XRING];
+      if (e.round == r && !e.done) { hint_nf = back == 1 ? e.nf : UINT32_MAX; hint_staged = e.staged; break; }
+    }
+  }
+  const uint32_t ncu = (uint32_t)n_cus(err);
+  const uint32_t g_round = hint_nf <= 16 ? std::min<uint32_t>(d.b.lv.grid_round, ncu / 4) : d.b.lv.grid_round;
+  const uint32_t g_send = hint_staged <= 4096 ? std::max<uint32_t>(1, ncu / 16) : ncu;
+  p.ctl_next = reinterpret_cast<LvCtl*>(d.b.lv.ctl) + ((d.xround + 1) & 1);
+  LVCHK(lv_dispatch(d.nq, LK_ROUND, g_round, p, st));
+  p.ctl_next = nullptr;
+  LVCHK(lv_dispatch(d.nq, LK_XSEND, g_send, p, st));
   // on a stream of its own the caller's collective is not ordered after these
   // kernels on the device: the host waits (the gloo tests; one process per
   // GPU passes its stream and queues with no wait)
@@ -906,6 +930,7 @@ int dist_x_rewind(DistLevel& d, uint32_t round, std::string& err) {
   d.cur = d.xcur[round % LV_XRING];
   d.cur_sel = d.xsel[round % LV_XRING];
   d.xround = round;
+  d.xfresh = true;
   const uint32_t zero = LVR_RUNNING;
   LVCHK(hipMemcpy(d.xrun, &zero, sizeof zero, hipMemcpyHostToDevice));  // (LvRun::done)
   return 0;

@@ -1198,7 +1198,7 @@ __device__ __forceinline__ LvXDecision lv_xdecide(const LvParams& p);
 template <int NQ>
 __device__ __forceinline__ void lv_xhalt(const LvParams& p, const LvXDecision& d);
 template <int NQ>
-__device__ __forceinline__ void lv_xclose(const LvParams& p);
+__device__ __forceinline__ void lv_xclose(const LvParams& p, const LvXDecision& d);
 
 // ---- insert: one lane per staged configuration -----------------------------
 // Striped staging: lane l of every wave walks stripe l (slot l * scs + i for
@@ -1208,6 +1208,7 @@ __device__ __forceinline__ void lv_xclose(const LvParams& p);
 template <int NQ>
 __global__ __launch_bounds__(LV_BLOCK) void lv_insert(LvParams p) {
   __shared__ uint32_t s_wcnt[LV_BLOCK / 64], s_base, s_hi, s_last;
+  LvXDecision xd;  // (thread 0: the exchanged round's decision, reused by the close)
   if (p.xcap) {
     // exchanged round: every block takes the round's decision from the
     // received headers; a halting round inserts nothing (block 0 records it).
@@ -1218,9 +1219,9 @@ __global__ __launch_bounds__(LV_BLOCK) void lv_insert(LvParams p) {
     if (threadIdx.x == 0) {
       uint32_t h = p.run->done ? LVR_ABORT : 0u;  // (stopped in an earlier round)
       if (!h) {
-        const LvXDecision d = lv_xdecide<NQ>(p);
-        h = d.halt;
-        if (h && blockIdx.x == 0) lv_xhalt<NQ>(p, d);
+        xd = lv_xdecide<NQ>(p);
+        h = xd.halt;
+        if (h && blockIdx.x == 0) lv_xhalt<NQ>(p, xd);
       }
       s_halt = h;
     }
@@ -1317,7 +1318,7 @@ __global__ __launch_bounds__(LV_BLOCK) void lv_insert(LvParams p) {
   if (threadIdx.x == 0) s_last = atomicAdd(&p.ctl->done_blocks, 1u) == gridDim.x - 1;
   __syncthreads();
   if (s_last && threadIdx.x == 0) {
-    if (p.xcap) lv_xclose<NQ>(p);
+    if (p.xcap) lv_xclose<NQ>(p, xd);
     else lv_close_round(p);
   }
 }
@@ -1589,10 +1590,36 @@ __device__ __forceinline__ uint32_t lv_stage_dense(const LvParams& p) {
   return 64u * wave_max_u32(min(ld_agent(&p.ctl->cnt[16 * lane]), p.scs));
 }
 
+// the exchange headers (one wave): block o's count, the sender's largest
+// block and total, the round's found / staging-overflow flags; clears the
+// owner counters for the next round
+template <int NQ>
+__device__ __forceinline__ void lv_xhdr_wave(const LvParams& p) {
+  const uint32_t lane = threadIdx.x & 63;
+  const uint32_t c = lane < p.world ? atomicExch(&p.own_cnt[lane], 0u) : 0u;
+  const uint32_t mb = wave_max_u32(c);
+  unsigned long long tot = c;
+  for (int d = 32; d >= 1; d >>= 1) tot += __shfl_xor(tot, d, 64);
+  if (lane < p.world) {
+    LvXHdr h;
+    h.count = c; h.maxblk = mb;
+    h.found = ld_agent(&p.ctl->found);
+    h.fpar = ld_agent(&p.ctl->found_parent); h.fmov = ld_agent(&p.ctl->found_move);
+    h.fp4 = ld_agent(&p.ctl->found_p4);
+    h.sovf = ld_agent(&p.ctl->overflow);
+    h.nf = p.run->nf;
+    h.staged = tot;
+    *lv_xhdr<NQ>(p.send, lane, p.xcap) = h;
+  }
+}
+
 // stage -> fixed-capacity blocks: one wave per 64 staging slots (lane = stripe)
 // takes owner positions with atomics, then copies each of its configurations
-// cooperatively (16 bytes per lane); the last block writes the headers and
-// clears the owner counters for the next round
+// cooperatively (16 bytes per lane); the last block to finish writes the
+// headers. It reads only the owner counters (device-scope atomics, complete
+// before each block's arrival) and values earlier kernels wrote, so the
+// hand-off needs no fence (an agent-scope __threadfence per block cost ~60 us
+// per round at 4 blocks per CU: MI355X_MICROARCH.md).
 template <int NQ>
 __global__ __launch_bounds__(LV_BLOCK) void lv_xsend(LvParams p) {
   if (p.run->done) return;
@@ -1622,26 +1649,10 @@ __global__ __launch_bounds__(LV_BLOCK) void lv_xsend(LvParams p) {
       for (uint32_t c = lane; c < PER; c += 64) dst[(size_t)d * PER + c] = src[(size_t)sl * PER + c];
     }
   }
-  __threadfence();
-  __syncthreads();
+  __syncthreads();  // (every wave's owner atomics have returned)
   if (threadIdx.x == 0) s_last = atomicAdd(&p.ctl->xblocks, 1u) == gridDim.x - 1;
   __syncthreads();
-  if (!s_last || threadIdx.x >= 64) return;
-  const uint32_t c = lane < p.world ? atomicExch(&p.own_cnt[lane], 0u) : 0u;
-  const uint32_t mb = wave_max_u32(c);
-  unsigned long long tot = c;
-  for (int d = 32; d >= 1; d >>= 1) tot += __shfl_xor(tot, d, 64);
-  if (lane < p.world) {
-    LvXHdr h;
-    h.count = c; h.maxblk = mb;
-    h.found = ld_agent(&p.ctl->found);
-    h.fpar = ld_agent(&p.ctl->found_parent); h.fmov = ld_agent(&p.ctl->found_move);
-    h.fp4 = ld_agent(&p.ctl->found_p4);
-    h.sovf = ld_agent(&p.ctl->overflow);
-    h.nf = p.run->nf;
-    h.staged = tot;
-    *lv_xhdr<NQ>(p.send, lane, cap) = h;
-  }
+  if (s_last && threadIdx.x < 64) lv_xhdr_wave<NQ>(p);
 }
 
 // the decision of an exchanged round, from the received headers (every rank
@@ -1670,8 +1681,7 @@ __device__ __forceinline__ void lv_xpublish(const LvParams& p, const LvRun& R, c
   x->nf_global = d.nf_global; x->staged = d.staged;
   x->found_parent = R.found_parent; x->found_move = R.found_move; x->found_p4 = R.found_p4;
   __threadfence_system();
-  x->round = p.round;
-  __threadfence_system();
+  x->round = p.round;  // (the kernel's end makes it visible; the host reads after the round's event)
 }
 
 // a halting exchanged round (block 0 of lv_insert): the run stops, nothing inserted
@@ -1693,9 +1703,8 @@ __device__ __forceinline__ void lv_xhalt(const LvParams& p, const LvXDecision& d
 // the close of an exchanged round (the last lv_insert block): this rank's
 // share of the next frontier
 template <int NQ>
-__device__ __forceinline__ void lv_xclose(const LvParams& p) {
+__device__ __forceinline__ void lv_xclose(const LvParams& p, const LvXDecision& d) {
   const LvCounts k = lv_read_counts(p.ctl);
-  const LvXDecision d = lv_xdecide<NQ>(p);
   LvRun& R = *p.run;
   R.children += k.ch;
   R.last_nf = R.nf;

@@ -266,6 +266,7 @@ struct DistLevel {
   const uint8_t* xcur[8] = {};
   int xsel[8] = {};
   uint32_t xround = 0;           // the next round to queue
+  bool xfresh = true;            // the next queued round zeroes its counters on the host
 };
 int dist_create(DistLevel& d, const History* h, uint32_t rank, uint32_t world, uint32_t reductions_off,
                 hipStream_t stream, std::string& err);

@@ -789,7 +789,7 @@ __device__ void lv_solo_rounds(const LvParams& p, const LvPersist& q, LvRun& R, 
     a.K = p.K; a.hflags = p.hflags; a.scap = p.scap; a.scs = p.scs; a.tgid = p.tgid;
     a.max_rounds = max_rounds;
     // more live moves than this in a round: the grid expands it (S2LC_SOLO_MAXLIVE)
-    a.max_live = q.solo_maxlive ? q.solo_maxlive : 16u;
+    a.max_live = q.solo_maxlive ? q.solo_maxlive : 8u;  // (sweep: profiles/r04/maxlive_sweep.txt)
     const uint32_t ex = lv_solo_wave<NQ>(a, R, PL, NX, FR, s_cs, S);
     if (threadIdx.x == 0) s_ex = ex;
   }

@@ -296,6 +296,7 @@ def bind_stream(device=None) -> int:
 
 _XDEPTH = 2      # partitioned rounds queued beyond the newest status the host has read
 _XDEBUG = bool(int(__import__("os").environ.get("S2LC_XDEBUG", "0") or 0))  # (diagnostics: every round's status)
+_XTIME = bool(int(__import__("os").environ.get("S2LC_XTIME", "0") or 0))    # (diagnostics: host time per step)
 _XRING = 8       # the library's status ring (LV_XRING): receive buffers a re-run may read
 
 
@@ -338,14 +339,28 @@ def _partitioned_rounds(ds: "DistSearch", ex: "_Exchange", device, cb: int, worl
         print(f"[x] rank {ds.rank} phase from round {round0} frontier {info.frontier} cap {ph.cap} "
               f"limit {limit}", flush=True)
     queued = deque()                 # rounds whose status is not read yet
+    prev_blk = 1                     # the largest block of the previous status read
     keep = deque(maxlen=_XRING + 1)  # receive buffers a re-run may start from
+    tm = [0.0] * 5 if _XTIME else None
     while True:
+        if tm:
+            t0 = time.perf_counter()
         send = torch.empty(world * (ph.cap + 1) * cb, dtype=torch.uint8, device=device)
         if _XDEBUG:
             print(f"[x] rank {ds.rank} queue cap {ph.cap} send {send.data_ptr():#x}+{send.numel()}", flush=True)
+        if tm:
+            t1 = time.perf_counter()
         ds.x_send(send, ph.cap)
+        if tm:
+            t2 = time.perf_counter()
         recv = ex.payload_fixed(send)
+        if tm:
+            t3 = time.perf_counter()
         r = ds.x_recv(recv, ph.cap)
+        if tm:
+            t4 = time.perf_counter()
+            for i, (a, b) in enumerate(((t0, t1), (t1, t2), (t2, t3), (t3, t4))):
+                tm[i] += b - a
         if _XDEBUG:
             print(f"[x] rank {ds.rank} queued round {r} recv {recv.data_ptr():#x}+{recv.numel()}", flush=True)
         queued.append(r)
@@ -354,7 +369,11 @@ def _partitioned_rounds(ds: "DistSearch", ex: "_Exchange", device, cb: int, worl
         if len(queued) <= _XDEPTH:
             continue
         r0 = queued.popleft()
+        if tm:
+            t5 = time.perf_counter()
         st = ds.x_wait(r0)
+        if tm:
+            tm[4] += time.perf_counter() - t5
         if _XDEBUG:
             print(f"[x] rank {ds.rank} round {r0} cap {ph.cap} ran {st.ran} done {st.done} nf {st.nf} "
                   f"maxblk {st.maxblk} nf_global {st.nf_global} staged {st.staged}", flush=True)
@@ -370,7 +389,10 @@ def _partitioned_rounds(ds: "DistSearch", ex: "_Exchange", device, cb: int, worl
             continue
         if st.done:
             break
-        ph.cap = _xcap(st.maxblk, limit)
+        # the status is _XDEPTH rounds old: extrapolate one step of its growth
+        grow = min(8.0, max(1.0, st.maxblk / max(1, prev_blk)))
+        prev_blk = st.maxblk
+        ph.cap = _xcap(int(st.maxblk * grow), limit)
         if wide > 0 and r0 > round0 + 1 and st.nf_global < wide // 4:
             # narrow again. The rounds still queued run to the end of the
             # phase; one of them may stop the search or outgrow its blocks
@@ -385,6 +407,10 @@ def _partitioned_rounds(ds: "DistSearch", ex: "_Exchange", device, cb: int, worl
                     break
             break
     ph.stop, _ = ds.x_end()
+    if tm:
+        print(f"[x] rank {ds.rank} phase host time (ms): alloc {tm[0]*1e3:.2f} send {tm[1]*1e3:.2f} "
+              f"exchange {tm[2]*1e3:.2f} recv {tm[3]*1e3:.2f} wait {tm[4]*1e3:.2f} "
+              f"over {ds.info().round - round0} rounds", flush=True)
     if ph.stop == DIST_X_ABORT:
         raise S2LCError(-5, "distributed round exceeds the device buffers")
     ph.rounds = ds.info().round - round0
