@@ -1107,8 +1107,8 @@ __device__ __forceinline__ LvCounts lv_read_counts(LvCtl* c) {
 // Close round `rnd` on the run state R: per-round count, run counters, and
 // the decision (found / empty / budget / overflow / witness off).
 __device__ __forceinline__ void lv_close_state(LvRun& R, const LvCounts& k, uint32_t rnd, uint32_t* rcounts,
-                                               uint32_t scap, uint64_t trace_cap) {
-  {
+                                               uint32_t scap, uint64_t trace_cap, bool clock = true) {
+  if (clock) {  // (solo rounds account their phase's time once, at its end)
     const unsigned long long now = wall_clock64();
     if (rnd > 0) (R.nf >= LV_WIDE_NF ? R.wide_ticks : R.narrow_ticks) += now - R.t_last;
     R.t_last = now;

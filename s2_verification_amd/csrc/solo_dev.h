@@ -610,10 +610,10 @@ __device__ __attribute__((noinline)) uint32_t lv_solo_wave(const SoloArgs p, LvR
       LvCounts kc;
       kc.nn = alive; kc.ovf = ovf; kc.fnd = found;
       kc.fpar = fpar; kc.fmov = fmov; kc.fp4 = fp4; kc.ch = kids; kc.closed = 0;
-      const unsigned long long t_prev = R.t_last;
-      lv_close_state(R, kc, r, p.rcounts, p.scap, p.trace_cap);
+      // (no clock read per round: s_memrealtime is a scalar-memory round
+      // trip; the phase's time is added at its end)
+      lv_close_state(R, kc, r, p.rcounts, p.scap, p.trace_cap, false);
       R.solo_rounds++;
-      R.solo_ticks += R.t_last - t_prev;
       // the first survivor's trace entry (it was not staged)
       if (!found && !ovf && alive && wit) p.trace[tbase] = TraceEnt{ptrace, kmv};
 #ifdef S2LC_PROF
@@ -682,6 +682,11 @@ __device__ __attribute__((noinline)) uint32_t lv_solo_wave(const SoloArgs p, LvR
     }
   }
   if (lane == 0) {
+    // the phase's rounds (narrow, solo) in the run's wall-clock split
+    const unsigned long long now = wall_clock64();
+    R.narrow_ticks += now - R.t_last;
+    R.solo_ticks += now - R.t_last;
+    R.t_last = now;
     S.tail = ptail; S.hash = phash; S.tok = ptok; S.pmin = pmin; S.ptrace = ptrace;
 #ifdef S2LC_PROF
     if (p.prof) {
