@@ -849,12 +849,14 @@ __device__ __forceinline__ bool lv_expand(const LvParams& p, const LvRoundIn& in
       else wave_min2_hot<NQ>(H, b_min, b_2nd);
     }
 #ifndef S2LC_PRE_GROUP
-#define S2LC_PRE_GROUP 0
+#define S2LC_PRE_GROUP 1
 #endif
-    // (S2LC_PRE_GROUP) grid rounds: the rest of every candidate's record and
-    // its next record's P1 bound loaded for all slots before the precheck
-    // uses any (one latency instead of one per slot with a candidate)
-    constexpr bool PG = NQ <= 5 && S2LC_PRE_GROUP;
+    // grid rounds: the rest of every candidate's record and its next record's
+    // P1 bound loaded for all slots before the precheck uses any (one latency
+    // instead of one per slot with a candidate). NQ <= 4: C5wide (NQ = 4)
+    // 0.0394 -> 0.0361 s; at NQ = 5 the 50 more live VGPRs cost C5 0.6 %
+    // (profiles/r04/pre_group_ab.txt)
+    constexpr bool PG = NQ <= 4 && S2LC_PRE_GROUP;
     uint4 pm0[PG ? NP : 1], pm3[PG ? NP : 1];
     uint64_t pns[PG ? NP : 1];
     if (PG) {
