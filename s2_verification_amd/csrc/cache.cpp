@@ -383,9 +383,9 @@ int s2lc_history_load_many(const uint8_t* buf, size_t len, int n_threads, s2lc_h
   auto one = [&](size_t i) {
     if (bad.load(std::memory_order_relaxed)) return;
     try {
-      s2lc_history* h = new s2lc_history();
+      s2lc_history* h = history_acquire();
       if (!read_section(payload + off[i], payload + off[i + 1], h->h)) {
-        delete h;
+        history_release(h);
         bad = S2LC_EDECODE;
         return;
       }
@@ -401,7 +401,7 @@ int s2lc_history_load_many(const uint8_t* buf, size_t len, int n_threads, s2lc_h
   }
   if (bad) {
     for (uint64_t i = 0; i < nn; ++i) {
-      delete out[i];
+      history_release(out[i]);
       out[i] = nullptr;
     }
     *n = 0;

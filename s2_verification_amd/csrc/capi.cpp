@@ -182,12 +182,12 @@ int s2lc_load_jsonl(const char* path, const uint8_t* buf, size_t len, s2lc_histo
       buf = data.data();
       len = data.size();
     }
-    s2lc_history* h = new s2lc_history();
+    s2lc_history* h = history_acquire();
     std::string e;
     int rc = load_jsonl(buf, len, h->h, e);
-    if (rc) { set_err(err, errlen, e); delete h; return rc; }
+    if (rc) { set_err(err, errlen, e); history_release(h); return rc; }
     rc = h->h.finalize();
-    if (rc) { set_err(err, errlen, h->h.error); delete h; return rc; }
+    if (rc) { set_err(err, errlen, h->h.error); history_release(h); return rc; }
     *out = h;
     return 0;
   } catch (const std::bad_alloc&) {
@@ -214,14 +214,14 @@ int s2lc_load_jsonl_many(const uint8_t* const* bufs, const size_t* lens, size_t 
       const size_t i = next.fetch_add(1);
       if (i >= n) return;
       try {
-        s2lc_history* h = new s2lc_history();
+        s2lc_history* h = history_acquire();
         int rc = load_jsonl(bufs[i], lens[i], h->h, errs[i]);
         if (!rc) {
           rc = h->h.finalize();
           if (rc) errs[i] = h->h.error;
         }
         if (rc) {
-          delete h;
+          history_release(h);
           rcs[i] = rc;
           size_t cur = first_bad.load();
           while (i < cur && !first_bad.compare_exchange_weak(cur, i)) {}
@@ -243,7 +243,7 @@ int s2lc_load_jsonl_many(const uint8_t* const* bufs, const size_t* lens, size_t 
   const size_t bad = first_bad.load();
   if (bad != SIZE_MAX) {
     for (size_t i = 0; i < n; ++i) {
-      delete out[i];
+      history_release(out[i]);
       out[i] = nullptr;
     }
     if (err_index) *err_index = bad;
@@ -257,7 +257,7 @@ int s2lc_history_from_events(const s2lc_event* ev, size_t n, s2lc_history** out,
   if (!out || (!ev && n)) return S2LC_EINVAL;
   *out = nullptr;
   try {
-    s2lc_history* h = new s2lc_history();
+    s2lc_history* h = history_acquire();
     History& H = h->h;
     H.events.reserve(n);
     for (size_t i = 0; i < n; ++i) {
@@ -265,7 +265,7 @@ int s2lc_history_from_events(const s2lc_event* ev, size_t n, s2lc_history** out,
       Event e;
       if (x.kind != S2LC_CALL_EVENT && x.kind != S2LC_RETURN_EVENT) {
         set_err(err, errlen, "event " + std::to_string(i) + ": bad kind");
-        delete h;
+        history_release(h);
         return S2LC_EINVAL;
       }
       e.kind = x.kind;
@@ -282,7 +282,7 @@ int s2lc_history_from_events(const s2lc_event* ev, size_t n, s2lc_history** out,
         e.hash_off = H.pool.size();
         e.hash_cnt = x.n_record_hashes;
         if (x.n_record_hashes) {
-          if (!x.record_hashes) { delete h; set_err(err, errlen, "null record_hashes"); return S2LC_EINVAL; }
+          if (!x.record_hashes) { history_release(h); set_err(err, errlen, "null record_hashes"); return S2LC_EINVAL; }
           H.pool.insert(H.pool.end(), x.record_hashes, x.record_hashes + x.n_record_hashes);
         }
       } else {
@@ -296,7 +296,7 @@ int s2lc_history_from_events(const s2lc_event* ev, size_t n, s2lc_history** out,
       H.events.push_back(e);
     }
     int rc = H.finalize();
-    if (rc) { set_err(err, errlen, H.error); delete h; return rc; }
+    if (rc) { set_err(err, errlen, H.error); history_release(h); return rc; }
     *out = h;
     return 0;
   } catch (const std::bad_alloc&) {
@@ -308,7 +308,7 @@ int s2lc_history_from_events(const s2lc_event* ev, size_t n, s2lc_history** out,
   }
 }
 
-void s2lc_history_free(s2lc_history* h) { delete h; }
+void s2lc_history_free(s2lc_history* h) { history_release(h); }
 
 size_t s2lc_history_event_count(const s2lc_history* h) { return h ? h->h.n_events() : 0; }
 
@@ -1184,10 +1184,10 @@ int s2lc_simulate_history(const s2lc_sim_params* p, s2lc_history** out) {
   if (!p || !out) return S2LC_EINVAL;
   *out = nullptr;
   try {
-    s2lc_history* h = new s2lc_history();
+    s2lc_history* h = history_acquire();
     int rc = simulate(*p, &h->h, nullptr);
     if (!rc) rc = h->h.finalize();
-    if (rc) { delete h; return rc; }
+    if (rc) { history_release(h); return rc; }
     *out = h;
     return 0;
   } catch (...) {

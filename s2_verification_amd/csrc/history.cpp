@@ -4,6 +4,8 @@
 // Reference semantics:
 //   renumber / makeLinkedEntries / checkSingle  porcupine v1.0.3 (upstream)
 //   s2Model.Step                                main.go:264-335
+#include <stdlib.h>
+
 #include <algorithm>
 #include <queue>
 
@@ -64,19 +66,43 @@ int History::finalize() {
   const size_t E = events.size();
   if (E >= (size_t)EV_INF) { status = S2LC_EUNSUPPORTED; error = "too many events"; return status; }
 
+  // working arrays: per decoder thread, reused from history to history
+  thread_local struct {
+    std::vector<uint32_t> dense, dir, val, ncall, nret, call, ret, chain_of, chain_len, last, fill;
+    std::vector<int64_t> ids, key;
+    std::vector<int32_t> reg;
+  } S;
   // porcupine renumber(): ids -> 0..m-1 in order of first appearance
-  // (an open-addressing map: one allocation, no per-id nodes)
-  std::vector<uint32_t> dense(E);
-  std::vector<int64_t> ids;
-  ids.reserve(E / 2 + 1);
+  // (an open-addressing map, no per-id nodes)
+  std::vector<uint32_t>& dense = S.dense;
+  std::vector<int64_t>& ids = S.ids;
+  dense.resize(E);
+  ids.clear();
   {
     size_t cap = 16;
     while (cap < 2 * E) cap <<= 1;
-    std::vector<int64_t> key(cap);
-    std::vector<uint32_t> val(cap, EV_INF);
+    std::vector<int64_t>& key = S.key;
+    std::vector<uint32_t>& val = S.val;
+    std::vector<uint32_t>& dir = S.dir;  // ids in [0, cap) (the collector's: 0, 1, 2, ...) index directly
+    dir.assign(cap, EV_INF);
+    bool hashed = false;
     const size_t mask = cap - 1;
     for (size_t i = 0; i < E; ++i) {
       const int64_t id = events[i].op_id;
+      if ((uint64_t)id < (uint64_t)cap) {
+        uint32_t& d = dir[(size_t)id];
+        if (d == EV_INF) {
+          d = (uint32_t)ids.size();
+          ids.push_back(id);
+        }
+        dense[i] = d;
+        continue;
+      }
+      if (!hashed) {
+        key.resize(cap);
+        val.assign(cap, EV_INF);
+        hashed = true;
+      }
       uint64_t x = (uint64_t)id * 0x9E3779B97F4A7C15ull;
       size_t s_ = (size_t)(x ^ (x >> 29)) & mask;
       while (val[s_] != EV_INF && key[s_] != id) s_ = (s_ + 1) & mask;
@@ -89,7 +115,11 @@ int History::finalize() {
     }
   }
   const uint32_t m = (uint32_t)ids.size();
-  std::vector<uint32_t> ncall(m, 0), nret(m, 0), call(m, EV_INF), ret(m, EV_INF);
+  std::vector<uint32_t>&ncall = S.ncall, &nret = S.nret, &call = S.call, &ret = S.ret;
+  ncall.assign(m, 0);
+  nret.assign(m, 0);
+  call.assign(m, EV_INF);
+  ret.assign(m, EV_INF);
   for (size_t i = 0; i < E; ++i) {
     const uint32_t d = dense[i];
     if (events[i].kind == 0) { ncall[d]++; call[d] = (uint32_t)i; }
@@ -118,7 +148,8 @@ int History::finalize() {
     // nearest later one with its id; two calls may take the same return)
     lit_id.assign(dense.begin(), dense.end());
     lit_match.assign(E, -1);
-    std::vector<int32_t> reg(m, -1);
+    std::vector<int32_t>& reg = S.reg;
+    reg.assign(m, -1);
     for (size_t i = E; i-- > 0;) {
       if (events[i].kind == 1) reg[dense[i]] = (int32_t)i;
       else lit_match[i] = reg[dense[i]];
@@ -167,10 +198,13 @@ int History::finalize() {
 
   // Greedy interval colouring (ops by call order; reuse the chain that
   // finished earliest if it finished before this call): K = max overlap.
-  std::vector<uint32_t> chain_of(m), chain_len;
+  std::vector<uint32_t>&chain_of = S.chain_of, &chain_len = S.chain_len;
+  chain_of.resize(m);
+  chain_len.clear();
   {
     // the chain with the smallest (last ret, index) that ended before the call
-    std::vector<uint32_t> last;  // last ret of each chain
+    std::vector<uint32_t>& last = S.last;  // last ret of each chain
+    last.clear();
     using P = std::pair<uint32_t, uint32_t>;  // (last ret, chain), for wide histories
     std::priority_queue<P, std::vector<P>, std::greater<P>> heap;
     bool use_heap = false;
@@ -209,18 +243,28 @@ int History::finalize() {
     max_chain_len = std::max<uint32_t>(max_chain_len, chain_len[c]);
   }
   chain_start[K] = pos;
-  recs.assign(pos, OpRec{});
   rec_op.assign(pos, EV_INF);
   {
-    std::vector<uint32_t> fill(chain_start.begin(), chain_start.end() - 1);  // next slot of each chain
+    std::vector<uint32_t>& fill = S.fill;  // next slot of each chain
+    fill.assign(chain_start.begin(), chain_start.end() - 1);
     for (uint32_t d = 0; d < m; ++d) {  // call order within every chain
       const uint32_t p = fill[chain_of[d]]++;
-      OpRec& r = recs[p];
-      r = rec_of(d);
-      if (r.flags & OPF_CLS_E) n_ident++;
       rec_op[p] = d;
       op_rec[d] = p;
     }
+  }
+  // the records in position order, each written once (assign() would zero
+  // them first); a sentinel is completed below
+  recs.clear();
+  recs.reserve(pos);
+  for (uint32_t p = 0; p < pos; ++p) {
+    const uint32_t d = rec_op[p];
+    if (d == EV_INF) {
+      recs.push_back(OpRec{});
+      continue;
+    }
+    recs.push_back(rec_of(d));
+    if (recs.back().flags & OPF_CLS_E) n_ident++;
   }
   for (uint32_t c = 0; c < K; ++c) {
     const uint32_t p = chain_start[c + 1] - 1;
@@ -250,6 +294,91 @@ int History::finalize() {
   if (tokens.size() > 0xFFFF) { status = S2LC_EUNSUPPORTED; error = "more than 65535 distinct fencing tokens"; }
   if (pool.size() > 0xFFFFFFFFull) { status = S2LC_EUNSUPPORTED; error = "more than 2^32 record hashes"; }
   return status;
+}
+
+// ------------------------------------------------------------- recycling ---
+template <class V>
+static size_t used(const V& v) {
+  return v.size() * sizeof(typename V::value_type);
+}
+
+size_t History::used_bytes() const {
+  return used(events) + used(pool) + used(op_call) + used(op_ret) + used(op_ids) + used(chain_start) + used(recs) +
+         used(rec_op) + used(op_rec) + used(lit_id) + used(lit_match) + used(lazy_client) + used(tokens);
+}
+
+void History::recycle() {
+  History f;  // every scalar and member back to its default ...
+  auto keep = [](auto& dst, auto& src) {  // ... and every array to empty with its capacity
+    src.clear();
+    dst.swap(src);
+  };
+  keep(f.events, events);
+  keep(f.pool, pool);
+  keep(f.op_call, op_call);
+  keep(f.op_ret, op_ret);
+  keep(f.op_ids, op_ids);
+  keep(f.chain_start, chain_start);
+  keep(f.recs, recs);
+  keep(f.rec_op, rec_op);
+  keep(f.op_rec, op_rec);
+  keep(f.lit_id, lit_id);
+  keep(f.lit_match, lit_match);
+  keep(f.lazy_client, lazy_client);
+  *this = std::move(f);
+  pooled_bytes = 0;
+}
+
+namespace {
+struct HistoryPool {
+  std::mutex mu;
+  std::vector<s2lc_history*> free;
+  size_t bytes = 0;
+  size_t budget;
+  HistoryPool() {
+    const char* e = getenv("S2LC_HISTORY_POOL_MB");
+    budget = (size_t)(e && *e ? strtoull(e, nullptr, 10) : 4096ull) << 20;
+  }
+};
+// never destroyed: a history freed by another static destructor at exit must
+// still find it
+HistoryPool& hpool() {
+  static HistoryPool* p = new HistoryPool();
+  return *p;
+}
+}  // namespace
+
+s2lc_history* history_acquire() {
+  HistoryPool& P = hpool();
+  {
+    std::lock_guard<std::mutex> g(P.mu);
+    if (!P.free.empty()) {
+      s2lc_history* h = P.free.back();
+      P.free.pop_back();
+      P.bytes -= h->h.pooled_bytes;
+      return h;
+    }
+  }
+  return new s2lc_history();
+}
+
+void history_release(s2lc_history* h) {
+  if (!h) return;
+  HistoryPool& P = hpool();
+  // (accounted by the bytes in use at release: the pages a history touched
+  // stay resident, reserved capacity beyond them costs address space only)
+  const size_t b = h->h.used_bytes();
+  if (P.budget && b <= P.budget) {
+    h->h.recycle();  // outside the lock: frees the token strings, keeps the arrays
+    h->h.pooled_bytes = b;
+    std::lock_guard<std::mutex> g(P.mu);
+    if (P.bytes + b <= P.budget) {
+      P.free.push_back(h);
+      P.bytes += b;
+      return;
+    }
+  }
+  delete h;
 }
 
 }  // namespace s2lc

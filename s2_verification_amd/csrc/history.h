@@ -83,6 +83,12 @@ struct History {
   std::unique_ptr<std::once_flag> lazy_once;  // builds `events` once (thread-safe)
   size_t n_events() const { return lazy_once ? lazy_client.size() : events.size(); }
   void ensure_events() const;                 // no-op unless loaded from the cache
+
+  // ---- recycling (history_acquire / history_release) ----
+  // Back to the freshly constructed state, keeping every array's capacity.
+  void recycle();
+  size_t used_bytes() const;
+  size_t pooled_bytes = 0;  // used_bytes() when it was parked
 };
 
 // JSONL loader (eventsFromReader, main.go:529-563). Returns 0 or S2LC_EDECODE.
@@ -96,3 +102,15 @@ struct SimParams;
 struct s2lc_history {
   s2lc::History h;
 };
+
+namespace s2lc {
+// Decoders take their History from a process-wide pool of released ones, and
+// s2lc_history_free parks a history there (cleared, capacity kept) instead of
+// returning its arrays to the C heap. A long-running checker decodes batch N+1
+// into batch N's storage: no page faults, no heap growth or trim, no
+// address-space lock shared by the decoder threads. The pool is
+// bounded by S2LC_HISTORY_POOL_MB of array bytes in use at release (default
+// 4096; 0 = off).
+s2lc_history* history_acquire();
+void history_release(s2lc_history* h);
+}  // namespace s2lc

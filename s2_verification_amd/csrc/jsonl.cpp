@@ -467,6 +467,7 @@ struct Dec {
 struct Fast {
   const uint8_t* p;
   const uint8_t* end;
+  const uint8_t* lo;  // the record's first byte (tail8 reads up to 8 bytes before a digit run)
   // the literal w at p (eight bytes per compare; w is a compile-time constant)
   template <size_t N>
   bool lit(const char (&w)[N]) {
@@ -492,11 +493,22 @@ struct Fast {
   static uint32_t eight(const uint8_t* q) {
     uint64_t v;
     memcpy(&v, q, 8);
+    return eight_v(v);
+  }
+  static uint32_t eight_v(uint64_t v) {
     v -= 0x3030303030303030ull;
     v = v * 10 + (v >> 8);
     v = (((v & 0x000000FF000000FFull) * 0x000F424000000064ull) +
          (((v >> 16) & 0x000000FF000000FFull) * 0x0000271000000001ull)) >> 32;
     return (uint32_t)v;
+  }
+  // the k (1..8) digits ending at e: the eight bytes before e with the
+  // leading 8 - k replaced by '0'
+  static uint32_t tail8(const uint8_t* e, size_t k) {
+    uint64_t v;
+    memcpy(&v, e - 8, 8);
+    const uint64_t keep = ~0ull << (8 * (8 - k));
+    return eight_v((v & keep) | (0x3030303030303030ull & ~keep));
   }
   // length of the digit run at s (eight bytes per step: the first byte whose
   // high nibble is not 3, or whose value + 6 leaves the 0x3_ range, ends it)
@@ -519,11 +531,24 @@ struct Fast {
     p += digits(s);
     const size_t n = (size_t)(p - s);
     if (n == 0 || n > 20 || (n > 1 && s[0] == '0')) return false;
-    if (n == 20 && memcmp(s, "18446744073709551615", 20) > 0) return false;  // beyond uint64
     uint64_t r = 0;
-    size_t k = 0;
-    for (; k + 8 <= n; k += 8) r = r * 100000000ull + eight(s + k);
-    for (; k < n; ++k) r = r * 10 + (uint64_t)(s[k] - '0');
+    if (s - lo >= 8) {  // (always, after a record's key) right-aligned 8-digit groups, no digit loop
+      if (n <= 8) {
+        r = tail8(p, n);
+      } else if (n <= 16) {
+        r = (uint64_t)tail8(p - 8, n - 8) * 100000000ull + eight(p - 8);
+      } else {
+        const uint64_t hi = tail8(p - 16, n - 16);  // the leading 1..4 digits
+        const uint64_t rest = (uint64_t)eight(p - 16) * 100000000ull + eight(p - 8);
+        if (hi > 1844 || (hi == 1844 && rest > 6744073709551615ull)) return false;  // beyond uint64
+        r = hi * 10000000000000000ull + rest;
+      }
+    } else {
+      if (n == 20 && memcmp(s, "18446744073709551615", 20) > 0) return false;  // beyond uint64
+      size_t k = 0;
+      for (; k + 8 <= n; k += 8) r = r * 100000000ull + eight(s + k);
+      for (; k < n; ++k) r = r * 10 + (uint64_t)(s[k] - '0');
+    }
     v = r;
     return !(p < end && (*p == '.' || *p == 'e' || *p == 'E'));
   }
@@ -558,7 +583,7 @@ struct Fast {
 // One record at buf[off..]; returns the bytes consumed (0: not in the
 // collector's form, nothing was changed).
 size_t fast_record(const uint8_t* base, const uint8_t* end, History& h) {
-  Fast F{base, end};
+  Fast F{base, end, base};
   h.events.emplace_back();  // decoded in place; dropped again if the record is not in the collector's form
   Event& e = h.events.back();
   size_t pool0 = h.pool.size();

@@ -24,6 +24,8 @@
 
 #include <algorithm>
 #include <chrono>
+#include <memory>
+#include <thread>
 #include <numeric>
 #include <string>
 
@@ -229,8 +231,16 @@ int batch_upload(DevBatch& b, const std::vector<const History*>& hs, uint32_t re
   b.moves = reinterpret_cast<uint32_t*>(b.arena + o_moves);
   b.rcounts = reinterpret_cast<uint32_t*>(b.arena + o_rc);
   b.list = reinterpret_cast<uint32_t*>(b.arena + o_list);
-  // pack every history into the pinned stage (in parallel: ~0.5 GB for C4)
-  parallel_for(n, 64, [&](size_t i) {
+  // Pack every history into the pinned stage (in parallel: ~0.5 GB for C4).
+  // The records and the hash pool (nearly all of the stage) go up in slices
+  // of histories as the slices complete: this thread queues each slice's two
+  // ranges (async from pinned memory) while the packer threads fill the next,
+  // so the DMA overlaps the packing; the small sections follow at the end.
+  const size_t n_sl = n >= 2048 ? 16 : 1;
+  const size_t sl_len = (n + n_sl - 1) / std::max<size_t>(n_sl, 1);
+  std::unique_ptr<std::atomic<uint32_t>[]> sl_left(new std::atomic<uint32_t>[n_sl]);
+  for (size_t k = 0; k < n_sl; ++k) sl_left[k] = (uint32_t)(std::min(n, (k + 1) * sl_len) - std::min(n, k * sl_len));
+  auto pack_one = [&](size_t i) {
     const History& h = *hs[i];
     HistDesc& d = b.h_hist[i];
     size_t pr = off_rec[i], pc = off_cs[i];
@@ -255,7 +265,29 @@ int batch_upload(DevBatch& b, const std::vector<const History*>& hs, uint32_t re
     R = HistResult{};
     R.verdict = V_UNKNOWN;
     R.witness_off = b.h_moves_off[i];
-  });
+    sl_left[i / sl_len].fetch_sub(1, std::memory_order_release);
+  };
+  if (n_sl == 1) {
+    parallel_for(n, 64, pack_one);
+  } else {
+    std::thread packer([&]() { parallel_for(n, 64, pack_one); });
+    hipError_t ce = hipSuccess;
+    for (size_t k = 0; k < n_sl; ++k) {
+      while (sl_left[k].load(std::memory_order_acquire) != 0) std::this_thread::yield();
+      const size_t i0 = k * sl_len, i1 = std::min(n, (k + 1) * sl_len);
+      if (i0 >= i1 || ce != hipSuccess) continue;
+      const size_t r0 = off_rec[i0], r1 = i1 < n ? off_rec[i1] : n_recs;
+      const size_t p0 = off_pool[i0], p1 = i1 < n ? off_pool[i1] : n_pool;
+      if (r1 > r0)
+        ce = hipMemcpyAsync(b.arena + o_recs + r0 * sizeof(OpRec), b.stage + o_recs + r0 * sizeof(OpRec),
+                            (r1 - r0) * sizeof(OpRec), hipMemcpyHostToDevice, 0);
+      if (ce == hipSuccess && p1 > p0)
+        ce = hipMemcpyAsync(b.arena + o_pool + p0 * sizeof(uint64_t), b.stage + o_pool + p0 * sizeof(uint64_t),
+                            (p1 - p0) * sizeof(uint64_t), hipMemcpyHostToDevice, 0);
+    }
+    packer.join();
+    HIPCHK(ce);
+  }
   for (size_t i = 0; i < n; ++i) b.algo_bytes_inputs += b.h_in_bytes[i];
   for (size_t i = 0; i < n; ++i)
     if (b.literal[i]) literal_prepare(*hs[i], (uint32_t)i, off_pool[i], b.lit_desc, b.lit_ev);
@@ -312,7 +344,12 @@ int batch_upload(DevBatch& b, const std::vector<const History*>& hs, uint32_t re
     }
   }
   b.h_res_stale = false;
-  HIPCHK(hipMemcpy(b.arena, b.stage, stage_bytes, hipMemcpyHostToDevice));
+  if (n_sl == 1) {
+    HIPCHK(hipMemcpy(b.arena, b.stage, stage_bytes, hipMemcpyHostToDevice));
+  } else {  // the rest of the stage after the records and the pool, then wait for every slice
+    HIPCHK(hipMemcpyAsync(b.arena + o_cs, b.stage + o_cs, stage_bytes - o_cs, hipMemcpyHostToDevice, 0));
+    HIPCHK(hipStreamSynchronize(0));
+  }
   return 0;
 }
 

@@ -225,3 +225,33 @@ def test_fast_path_decodes_like_the_general_parser(monkeypatch):
         assert fast == general, data[:300]
         n_err += fast[0] == "error"
     assert 0 < n_err < len(cases)
+
+
+def test_fast_path_integers_at_every_length(monkeypatch):
+    """The fast path parses a digit run as right-aligned 8-digit groups (and
+    bounds a 20-digit one arithmetically): every length 1..20, the uint64 /
+    int64 limits and one past them decode (or fail) as the general parser does."""
+    vals = ["0", "01", "00"]
+    for k in range(1, 21):
+        vals += [str(10 ** k - 1), str(10 ** (k - 1)), "1234567890123456789012"[:k]]
+    vals += ["18446744073709551615", "18446744073709551616", "18446744073709551625", "18446744073709552615",
+             "18440000000000000000", "18449999999999999999", "18450000000000000000", "99999999999999999999",
+             "184467440737095516150", "9223372036854775807", "9223372036854775808"]
+    n_err = 0
+    for v in vals:
+        for where in ("hash", "tail", "client", "op"):
+            h = v if where == "hash" else "5"
+            t = v if where == "tail" else "3"
+            c = v if where == "client" else "1"
+            o = v if where == "op" else "0"
+            data = ('{"event":{"Start":{"Append":{"num_records":1,"record_hashes":[%s],"set_fencing_token":null,'
+                    '"fencing_token":null,"match_seq_num":%s}}},"client_id":%s,"op_id":%s}\n'
+                    '{"event":{"Finish":{"ReadSuccess":{"tail":%s,"stream_hash":%s}}},"client_id":%s,"op_id":%s}\n'
+                    % (h, t, c, o, t, h, c, o)).encode()
+            monkeypatch.delenv("S2LC_JSONL_GENERAL", raising=False)
+            fast = _canon_or_error(data)
+            monkeypatch.setenv("S2LC_JSONL_GENERAL", "1")
+            general = _canon_or_error(data)
+            assert fast == general, (v, where)
+            n_err += fast[0] == "error"
+    assert 0 < n_err < 4 * len(vals)
