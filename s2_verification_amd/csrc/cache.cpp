@@ -380,11 +380,20 @@ int s2lc_history_load_many(const uint8_t* buf, size_t len, int n_threads, s2lc_h
     if (off[i] > off[i + 1] || off[i + 1] > plen || (off[i] & 7)) return S2LC_EDECODE;
   for (uint64_t i = 0; i < nn; ++i) out[i] = nullptr;
   std::atomic<int> bad{0};
+  std::vector<s2lc_history*> pre(nn, nullptr);
+  try {
+    history_acquire_many(nn, pre.data());
+  } catch (...) {
+    *n = 0;
+    return S2LC_ENOMEM;
+  }
   auto one = [&](size_t i) {
     if (bad.load(std::memory_order_relaxed)) return;
     try {
-      s2lc_history* h = history_acquire();
-      if (!read_section(payload + off[i], payload + off[i + 1], h->h)) {
+      s2lc_history* h = pre[i];  // (stays in pre[] until it is out[i] or released: an exception leaks nothing)
+      const bool ok = read_section(payload + off[i], payload + off[i + 1], h->h);
+      pre[i] = nullptr;
+      if (!ok) {
         history_release(h);
         bad = S2LC_EDECODE;
         return;
@@ -399,6 +408,7 @@ int s2lc_history_load_many(const uint8_t* buf, size_t len, int n_threads, s2lc_h
   } else {
     parallel_for(nn, 64, one);
   }
+  for (uint64_t i = 0; i < nn; ++i) history_release(pre[i]);  // (taken up front, not reached)
   if (bad) {
     for (uint64_t i = 0; i < nn; ++i) {
       history_release(out[i]);

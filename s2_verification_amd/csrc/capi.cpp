@@ -209,17 +209,25 @@ int s2lc_load_jsonl_many(const uint8_t* const* bufs, const size_t* lens, size_t 
   std::atomic<size_t> first_bad{SIZE_MAX};
   std::vector<int> rcs(n, 0);
   std::vector<std::string> errs(n);
+  std::vector<s2lc_history*> pre(n, nullptr);
+  try {
+    history_acquire_many(n, pre.data());
+  } catch (...) {
+    set_err(err, errlen, "out of memory");
+    return S2LC_ENOMEM;
+  }
   auto work = [&]() {
     for (;;) {
       const size_t i = next.fetch_add(1);
       if (i >= n) return;
       try {
-        s2lc_history* h = history_acquire();
+        s2lc_history* h = pre[i];  // (stays in pre[] until it is out[i] or released: an exception leaks nothing)
         int rc = load_jsonl(bufs[i], lens[i], h->h, errs[i]);
         if (!rc) {
           rc = h->h.finalize();
           if (rc) errs[i] = h->h.error;
         }
+        pre[i] = nullptr;
         if (rc) {
           history_release(h);
           rcs[i] = rc;
@@ -241,6 +249,7 @@ int s2lc_load_jsonl_many(const uint8_t* const* bufs, const size_t* lens, size_t 
   work();
   for (auto& t : ts) t.join();
   const size_t bad = first_bad.load();
+  for (size_t i = 0; i < n; ++i) history_release(pre[i]);  // (taken up front, not reached)
   if (bad != SIZE_MAX) {
     for (size_t i = 0; i < n; ++i) {
       history_release(out[i]);

@@ -362,6 +362,25 @@ s2lc_history* history_acquire() {
   return new s2lc_history();
 }
 
+void history_acquire_many(size_t n, s2lc_history** out) {
+  HistoryPool& P = hpool();
+  size_t k = 0;
+  {
+    std::lock_guard<std::mutex> g(P.mu);
+    for (; k < n && !P.free.empty(); ++k) {
+      out[k] = P.free.back();
+      P.free.pop_back();
+      P.bytes -= out[k]->h.pooled_bytes;
+    }
+  }
+  try {
+    for (; k < n; ++k) out[k] = new s2lc_history();
+  } catch (...) {
+    for (size_t i = 0; i < k; ++i) history_release(out[i]);
+    throw;
+  }
+}
+
 void history_release(s2lc_history* h) {
   if (!h) return;
   HistoryPool& P = hpool();

@@ -16,17 +16,18 @@
 
 namespace s2lc {
 
-struct Event {
-  int32_t kind = 0;  // 0 call, 1 return
+struct Event {  // (80 bytes: the 8-byte fields first, no padding holes)
   int64_t op_id = 0;
   int64_t client_id = 0;
-  uint8_t input_type = 0, has_num_records = 0, has_msn = 0;
   uint64_t num_records = 0, msn = 0;
-  uint32_t set_tok = 0, batch_tok = 0;  // interned ids, 0 = nil
   uint64_t hash_off = 0, hash_cnt = 0;  // into History::pool
-  uint8_t failure = 0, definite = 0, has_tail = 0, has_hash = 0;
   uint64_t tail = 0, stream_hash = 0;
+  uint32_t set_tok = 0, batch_tok = 0;  // interned ids, 0 = nil
+  uint8_t kind = 0;                     // 0 call, 1 return
+  uint8_t input_type = 0, has_num_records = 0, has_msn = 0;
+  uint8_t failure = 0, definite = 0, has_tail = 0, has_hash = 0;
 };
+static_assert(sizeof(Event) == 80, "Event layout");
 
 // Per-history search flags (HistDesc.flags). Each gates one verdict-exact
 // reduction; batch_upload clears the ones a context disables
@@ -112,5 +113,7 @@ namespace s2lc {
 // bounded by S2LC_HISTORY_POOL_MB of array bytes in use at release (default
 // 4096; 0 = off).
 s2lc_history* history_acquire();
+// n histories under one lock (the parallel loaders take theirs up front)
+void history_acquire_many(size_t n, s2lc_history** out);
 void history_release(s2lc_history* h);
 }  // namespace s2lc

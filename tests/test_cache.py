@@ -139,10 +139,10 @@ def test_wrapping_hash_range_is_refused():
     assert s2.load_cache(img)[0].events() == h.events()
     hdr = (24 + 8 * 2 + 7) & ~7
     off0 = struct.unpack_from("<Q", img, 24)[0]
-    ev0 = hdr + off0 + 72  # the section header is 72 bytes; Event: hash_off at +56, hash_cnt at +64
-    assert struct.unpack_from("<QQ", img, ev0 + 56) == (0, 1)
+    ev0 = hdr + off0 + 72  # the section header is 72 bytes; Event (history.h): hash_off at +32, hash_cnt at +40
+    assert struct.unpack_from("<QQ", img, ev0 + 32) == (0, 1)
     t = bytearray(img)
-    struct.pack_into("<QQ", t, ev0 + 56, (1 << 64) - 1, 2)
+    struct.pack_into("<QQ", t, ev0 + 32, (1 << 64) - 1, 2)
     with pytest.raises(s2.S2LCError) as e:
         s2.load_cache(bytes(t))
     assert e.value.status == -2
