@@ -729,6 +729,53 @@ class Checker:
     def check_batch(self, hs: Sequence[History]) -> List[CheckResult]:
         return Batch(self, hs).check()
 
+    def check_jsonl_many(self, blobs: Sequence[bytes], threads: int = 0, slices: int = 2,
+                         with_witness: bool = True) -> dict:
+        """Collector JSONL blobs (one history each) -> Batch.results_flat's
+        arrays, in input order, pipelined over `slices` slices of the input:
+        slice k+1 decodes on the host cores while slice k uploads and runs on
+        the device, and slice k's witnesses are certified while slice k+1
+        uploads and runs (the copy engine and the GPU work beside the decoder
+        and certifier threads). Two device batches alternate and are kept on
+        the checker for the next call (a long-running checker: warm buffers)."""
+        from concurrent.futures import ThreadPoolExecutor
+        n = len(blobs)
+        S = max(1, min(int(slices), n))
+        cuts = [n * k // S for k in range(S + 1)]
+        if not hasattr(self, "_pipe"):
+            self._pipe = [None, None]
+
+        def device(slot, hs):
+            b = self._pipe[slot]
+            if b is None:
+                b = self._pipe[slot] = Batch(self, hs)
+            else:
+                b.load(hs)
+            b.run()
+            return b
+
+        outs = []
+        with ThreadPoolExecutor(1) as ex:
+            fut = None
+            for k in range(S):
+                hs = load_many(blobs[cuts[k]:cuts[k + 1]], threads=threads)  # (ctypes: the GIL is released)
+                prev = fut.result() if fut is not None else None
+                fut = ex.submit(device, k % 2, hs)
+                del hs
+                if prev is not None:
+                    outs.append(prev.results_flat(with_witness))
+            outs.append(fut.result().results_flat(with_witness))
+        res = {}
+        for key in ("verdict", "reason", "configs", "rounds"):
+            res[key] = np.concatenate([o[key] for o in outs])
+        res["witness_ids"] = np.concatenate([o["witness_ids"] for o in outs])
+        offs, base = [np.zeros(1, np.uint64)], 0
+        for o in outs:
+            offs.append(o["witness_offs"][1:] + np.uint64(base))
+            base += int(o["witness_offs"][-1])
+        res["witness_offs"] = np.concatenate(offs)
+        return res
+
     def batch(self, hs: Sequence[History]) -> Batch:
         return Batch(self, hs)
 
