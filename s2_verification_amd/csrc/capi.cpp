@@ -454,8 +454,7 @@ int collect_results(DevBatch& B, const RunStats& stats, bool witness_recorded, s
           continue;
         }
         if (r.verdict == V_OK) {
-          const bool ok = rebuild_linearization(H, moves, n_moves, r.p4 != 0, order, ident, false) &&
-                          replay_path(H, order.data(), ident.data(), order.size());
+          const bool ok = rebuild_and_replay(H, moves, n_moves, r.p4 != 0, order, ident);
           if (!ok) {
             o.verdict = S2LC_UNKNOWN;
             o.reason = S2LC_R_WITNESS_INVALID;

@@ -310,5 +310,10 @@ bool replay_literal(const History& h, const uint32_t* order, size_t n);
 // one of s2Model.Step's successors (main.go:264-335). A path of states is a
 // certificate that the powerset run never empties.
 bool replay_path(const History& h, const uint32_t* order, const uint8_t* ident, size_t n);
+// rebuild_linearization (full, not partial) + replay_path in one pass: the
+// replay steps each op with its own state as the rebuild writes it (the same
+// checks, the two hash folds overlapped), then the real-time check.
+bool rebuild_and_replay(const History& h, const uint32_t* moves, uint32_t n_moves, bool p4,
+                        std::vector<uint32_t>& order, std::vector<uint8_t>& ident);
 
 }  // namespace s2lc

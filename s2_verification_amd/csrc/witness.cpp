@@ -42,6 +42,19 @@ bool claim_ok(const OpRec& r, const State& s, const uint64_t* pool, bool applied
   return true;
 }
 
+// One step of the certifying replay (replay_states): order's next op, with the
+// outcome the linearization claims, from the replay's own state.
+inline bool replay_step(const History& h, uint32_t op, uint8_t ident, State& s) {
+  const OpRec& r = h.recs[h.op_rec[op]];
+  // the outcome this linearization claims: the optimistic successor for an
+  // append taken as applied, the unchanged state otherwise
+  const bool applied = !ident && !(r.flags & OPF_CLS_E) && (r.flags & OPF_KIND_MASK) == 0;
+  State next;
+  if (!claim_ok(r, s, h.pool.data(), applied, next)) return false;
+  s = next;
+  return true;
+}
+
 void prefetch_range(const void* p, size_t bytes) {
   const char* c = static_cast<const char*>(p);
   for (size_t o = 0; o < bytes; o += 64) __builtin_prefetch(c + o, 0, 3);
@@ -75,6 +88,12 @@ struct Rebuild {
   uint8_t* ident;
   uint32_t n = 0;  // ops written
   State s{0, 0, 0};
+  // the certifying replay run alongside (rebuild_and_replay): its own state,
+  // stepped through each op as the rebuild writes it, so the two folds of the
+  // record hashes (the rebuild's and the replay's) are independent dependency
+  // chains in flight together instead of two passes
+  bool rep = false, rep_ok = true;
+  State rs{0, 0, 0};
   Rebuild(const History& h_, Head* hd_, uint32_t* ord, uint8_t* id)
       : h(h_), recs(h_.recs.data()), hd(hd_), K(h_.K), order(ord), ident(id) {
     for (uint32_t q = 0; q < K; ++q) load(q, recs + h.chain_start[q]);
@@ -109,6 +128,7 @@ struct Rebuild {
     const OpRec* r = hd[q].rec;
     order[n] = h.rec_op[(size_t)(r - recs)];
     ident[n] = id;
+    if (rep && rep_ok) rep_ok = replay_step(h, order[n], id, rs);
     ++n;
     load(q, r + 1);
   }
@@ -130,8 +150,8 @@ struct Rebuild {
 
 }  // namespace
 
-bool rebuild_linearization(const History& h, const uint32_t* moves, uint32_t n_moves, bool p4,
-                           std::vector<uint32_t>& order, std::vector<uint8_t>& ident, bool partial) {
+static bool rebuild(const History& h, const uint32_t* moves, uint32_t n_moves, bool p4, std::vector<uint32_t>& order,
+                    std::vector<uint8_t>& ident, bool partial, bool replay) {
   order.clear();
   ident.clear();
   if (h.structural) return false;
@@ -146,6 +166,7 @@ bool rebuild_linearization(const History& h, const uint32_t* moves, uint32_t n_m
   ident.resize(h.n_ops);
   t_scr.head.resize(h.K);
   Rebuild c(h, t_scr.head.data(), order.data(), ident.data());
+  c.rep = replay;
   c.close();
   for (uint32_t m = 0; m < n_moves; ++m) {
     const uint32_t j = moves[m] & 0xFFFFu;
@@ -175,8 +196,22 @@ bool rebuild_linearization(const History& h, const uint32_t* moves, uint32_t n_m
     std::sort(rest.begin(), rest.end(), [&](uint32_t a, uint32_t b) { return h.op_ret[a] < h.op_ret[b]; });
     order.insert(order.end(), rest.begin(), rest.end());
     ident.resize(order.size(), 1);
+    if (replay)
+      for (uint32_t op : rest)
+        if (c.rep_ok) c.rep_ok = replay_step(h, op, 1, c.rs);
   }
-  return order.size() == h.n_ops;
+  return order.size() == h.n_ops && (!replay || c.rep_ok);
+}
+
+bool rebuild_linearization(const History& h, const uint32_t* moves, uint32_t n_moves, bool p4,
+                           std::vector<uint32_t>& order, std::vector<uint8_t>& ident, bool partial) {
+  return rebuild(h, moves, n_moves, p4, order, ident, partial, false);
+}
+
+bool rebuild_and_replay(const History& h, const uint32_t* moves, uint32_t n_moves, bool p4,
+                        std::vector<uint32_t>& order, std::vector<uint8_t>& ident) {
+  return rebuild(h, moves, n_moves, p4, order, ident, false, true) &&
+         real_time_ok(h, order.data(), order.size());
 }
 
 // (The op's record is recs[op_rec[d]]: History::finalize builds it with
@@ -184,17 +219,8 @@ bool rebuild_linearization(const History& h, const uint32_t* moves, uint32_t n_m
 // rebuild has just read it, so the replay runs from cache.)
 static bool replay_states(const History& h, const uint32_t* order, const uint8_t* ident, size_t n) {
   State s{0, 0, 0};
-  const OpRec* recs = h.recs.data();
-  const uint32_t* op_rec = h.op_rec.data();
-  for (size_t i = 0; i < n; ++i) {
-    const OpRec& r = recs[op_rec[order[i]]];
-    // the outcome this linearization claims: the optimistic successor for an
-    // append taken as applied, the unchanged state otherwise
-    const bool applied = !ident[i] && !(r.flags & OPF_CLS_E) && (r.flags & OPF_KIND_MASK) == 0;
-    State next;
-    if (!claim_ok(r, s, h.pool.data(), applied, next)) return false;
-    s = next;
-  }
+  for (size_t i = 0; i < n; ++i)
+    if (!replay_step(h, order[i], ident[i], s)) return false;
   return true;
 }
 
