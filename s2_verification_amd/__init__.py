@@ -730,18 +730,23 @@ class Checker:
         return Batch(self, hs).check()
 
     def check_jsonl_many(self, blobs: Sequence[bytes], threads: int = 0, slices: int = 2,
-                         with_witness: bool = True) -> dict:
+                         with_witness: bool = True, overlap: Optional[bool] = None) -> dict:
         """Collector JSONL blobs (one history each) -> Batch.results_flat's
         arrays, in input order, pipelined over `slices` slices of the input:
         slice k+1 decodes on the host cores while slice k uploads and runs on
         the device, and slice k's witnesses are certified while slice k+1
         uploads and runs (the copy engine and the GPU work beside the decoder
-        and certifier threads). Two device batches alternate and are kept on
-        the checker for the next call (a long-running checker: warm buffers)."""
+        and certifier threads). With `overlap` (default: S2LC_PIPE_OVERLAP=1)
+        the certification of slice k also runs beside the decode of slice k+2
+        on a thread of its own, instead of between the decodes. Two device
+        batches alternate and are kept on the checker for the next call (a
+        long-running checker: warm buffers)."""
         from concurrent.futures import ThreadPoolExecutor
         n = len(blobs)
         S = max(1, min(int(slices), n))
         cuts = [n * k // S for k in range(S + 1)]
+        if overlap is None:
+            overlap = os.environ.get("S2LC_PIPE_OVERLAP", "0") == "1"
         if not hasattr(self, "_pipe"):
             self._pipe = [None, None]
 
@@ -754,17 +759,40 @@ class Checker:
             b.run()
             return b
 
+        def certify(b):
+            o = b.results_flat(with_witness)
+            # release the slice's host histories as soon as they are certified:
+            # the next slice's decode then reuses their storage (the history
+            # pool) instead of faulting in fresh pages. The pipe batch is not
+            # read again before its next load().
+            b.histories = []
+            return o
+
         outs = []
-        with ThreadPoolExecutor(1) as ex:
+        with ThreadPoolExecutor(1) as ex, ThreadPoolExecutor(1) as cx:
             fut = None
+            slot_cert = [None, None]  # (overlap) the pending certification of each device batch
             for k in range(S):
                 hs = load_many(blobs[cuts[k]:cuts[k + 1]], threads=threads)  # (ctypes: the GIL is released)
                 prev = fut.result() if fut is not None else None
+                if overlap:
+                    if prev is not None:
+                        slot_cert[(k - 1) % 2] = cx.submit(certify, prev)
+                        outs.append(slot_cert[(k - 1) % 2])
+                    if slot_cert[k % 2] is not None:  # its batch held slice k-2: certified before reuse
+                        slot_cert[k % 2].result()
+                    fut = ex.submit(device, k % 2, hs)
+                    del hs
+                    continue
                 fut = ex.submit(device, k % 2, hs)
                 del hs
                 if prev is not None:
-                    outs.append(prev.results_flat(with_witness))
-            outs.append(fut.result().results_flat(with_witness))
+                    outs.append(certify(prev))
+            if overlap:
+                outs.append(cx.submit(certify, fut.result()))
+                outs = [f.result() for f in outs]
+            else:
+                outs.append(certify(fut.result()))
         res = {}
         for key in ("verdict", "reason", "configs", "rounds"):
             res[key] = np.concatenate([o[key] for o in outs])

@@ -131,7 +131,8 @@ def test_pipelined_jsonl_check_matches_the_batch_path(checker):
     """Checker.check_jsonl_many (slices decode / upload + search / certify side
     by side, two device batches reused across calls) returns what one batch
     over the same histories returns: verdicts and certified witnesses, in
-    input order, for 1, 2 and 5 slices, twice (warm batches)."""
+    input order, for 1, 2 and 5 slices, twice (warm batches), with the
+    certification between the decodes and on its own thread (overlap)."""
     import numpy as np
     from s2_verification_amd import workloads as W
     blobs = [s2.simulate_jsonl(**W.c4_params(sd)) for sd in range(700, 1003)]
@@ -141,8 +142,8 @@ def test_pipelined_jsonl_check_matches_the_batch_path(checker):
     ref = b.results_flat(with_witness=True)
     expect = [orc.check_wgl(orc.from_s2lc_numpy(h.events_numpy(), owner=h))[0] for h in hs[:60]]
     assert [{s2.S2LC_OK: "Ok", s2.S2LC_ILLEGAL: "Illegal"}[int(v)] for v in ref["verdict"][:60]] == expect
-    for slices in (1, 2, 5, 2):
-        got = checker.check_jsonl_many(blobs, threads=4, slices=slices)
+    for slices, overlap in ((1, False), (2, False), (5, True), (2, True), (3, False), (1, True)):
+        got = checker.check_jsonl_many(blobs, threads=4, slices=slices, overlap=overlap)
         for k in ("verdict", "reason", "witness_offs"):  # (witnesses: certified by the library, same lengths)
             assert np.array_equal(got[k], ref[k]), (slices, k)
         assert len(got["witness_ids"]) == len(ref["witness_ids"])
