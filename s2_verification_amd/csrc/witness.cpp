@@ -132,24 +132,6 @@ struct Rebuild {
     ++n;
     load(q, r + 1);
   }
-  // A move the rebuild has just checked with claim_ok from state `from`, with
-  // the outcome the replay would claim (applied = !id: a move is never an
-  // E-class op, and a read / check-tail move is always an identity), giving
-  // `to`. When the replay stands at the same state its own claim_ok would be
-  // the same call on the same arguments, so it takes `to` instead of folding
-  // the op's record hashes a second time; otherwise it replays the op itself.
-  void take_move(uint32_t q, uint8_t id, const State& from, const State& to) {
-    if (rep && rep_ok && state_eq(rs, from)) {
-      const OpRec* r = hd[q].rec;
-      order[n] = h.rec_op[(size_t)(r - recs)];
-      ident[n] = id;
-      rs = to;
-      ++n;
-      load(q, r + 1);
-      return;
-    }
-    take(q, id);
-  }
   // legal minimal identity ops, to the fixpoint (search.hip's closure)
   void close() {
     for (;;) {
@@ -198,9 +180,8 @@ static bool rebuild(const History& h, const uint32_t* moves, uint32_t n_moves, b
       ident.resize(c.n);
       return false;
     }
-    const State from = c.s;
     c.s = next;
-    c.take_move(j, is_id ? 1 : 0, from, next);
+    c.take(j, is_id ? 1 : 0);
     c.close();
   }
   order.resize(c.n);
