@@ -184,6 +184,8 @@ bool read_section(const uint8_t* p, const uint8_t* end, History& h) {
   else r.arr(h.events, hd.n_events);
   r.arr(h.pool, hd.n_pool);
   h.tokens.clear();
+  h.tok_ix.clear();
+  h.tok_ix_n = 0;
   for (uint32_t i = 0; i < hd.n_tokens && r.ok; ++i) {
     uint32_t len = 0;
     if ((size_t)(end - r.p) < 4) { r.ok = false; break; }

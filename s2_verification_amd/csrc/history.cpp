@@ -15,9 +15,25 @@
 namespace s2lc {
 
 uint32_t History::intern(const std::string& s) {
-  for (size_t i = 0; i < tokens.size(); ++i)
-    if (tokens[i] == s) return (uint32_t)(i + 1);
+  const size_t n = tokens.size();
+  if (n < 32) {  // the collector's histories: a handful of tokens
+    for (size_t i = 0; i < n; ++i)
+      if (tokens[i] == s) return (uint32_t)(i + 1);
+    tokens.push_back(s);
+    return (uint32_t)tokens.size();
+  }
+  // many distinct tokens (one per append, say): a hash index instead of a
+  // scan per token, which would make the decode quadratic
+  if (tok_ix_n > n) {
+    tok_ix.clear();
+    tok_ix_n = 0;
+  }
+  for (; tok_ix_n < n; ++tok_ix_n) tok_ix.emplace(tokens[tok_ix_n], (uint32_t)(tok_ix_n + 1));  // (first id wins)
+  const auto it = tok_ix.find(s);
+  if (it != tok_ix.end()) return it->second;
   tokens.push_back(s);
+  tok_ix.emplace(s, (uint32_t)tokens.size());
+  tok_ix_n = tokens.size();
   return (uint32_t)tokens.size();
 }
 

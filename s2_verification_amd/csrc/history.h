@@ -10,6 +10,7 @@
 #include <memory>
 #include <mutex>
 #include <string>
+#include <unordered_map>
 #include <vector>
 
 #include "model.h"
@@ -47,6 +48,11 @@ struct History {
   mutable std::vector<Event> events;
   std::vector<uint64_t> pool;         // record hashes
   std::vector<std::string> tokens;    // token id i+1 -> string
+  // token -> id index for histories with many distinct tokens (intern():
+  // a scan below 32 tokens); it covers tokens[0, tok_ix_n) and is rebuilt
+  // when tokens shrank (a cache load refills them)
+  std::unordered_map<std::string, uint32_t> tok_ix;
+  size_t tok_ix_n = 0;
 
   uint32_t intern(const std::string& s);
 

@@ -255,3 +255,30 @@ def test_fast_path_integers_at_every_length(monkeypatch):
             assert fast == general, (v, where)
             n_err += fast[0] == "error"
     assert 0 < n_err < 4 * len(vals)
+
+
+@pytest.mark.parametrize("general", [False, True])
+def test_many_distinct_fencing_tokens(monkeypatch, general):
+    """A history with thousands of distinct fencing tokens (one per append)
+    interns each once and maps every event back to its own string, through
+    both decoders; reused tokens keep their first id (the number of distinct
+    tokens, n_tokens, counts each once)."""
+    import time
+    if general:
+        monkeypatch.setenv("S2LC_JSONL_GENERAL", "1")
+    n = 6000
+    lines = []
+    for i in range(n):
+        lines.append('{"event":{"Start":{"Append":{"num_records":0,"record_hashes":[],"set_fencing_token":"s%d",'
+                     '"fencing_token":%s,"match_seq_num":null}}},"client_id":1,"op_id":%d}'
+                     % (i, '"s%d"' % (i // 2) if i % 3 else "null", i))
+        lines.append('{"event":{"Finish":"AppendDefiniteFailure"},"client_id":1,"op_id":%d}' % i)
+    t0 = time.perf_counter()
+    h = load("\n".join(lines).encode())
+    assert time.perf_counter() - t0 < 5.0  # (a scan per token: ~18 M string compares)
+    evs = h.events()
+    for i in range(n):
+        v = evs[2 * i].Value
+        assert v.SetFencingToken == "s%d" % i
+        assert v.BatchFencingToken == ("s%d" % (i // 2) if i % 3 else None)
+    assert h.info()["n_tokens"] == n
