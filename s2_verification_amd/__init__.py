@@ -565,13 +565,22 @@ class Batch:
         if rc:
             raise S2LCError(rc, self.checker.last_error())
         self.histories = hs
+        self._detached = False
+
+    def _check_attached(self):
+        # (check_jsonl_many releases a pipe batch's histories once certified:
+        # its device results then have no host histories to refer to)
+        if getattr(self, "_detached", False):
+            raise RuntimeError("the batch's histories were released; load() new histories first")
 
     def run(self):
+        self._check_attached()
         rc = lib().s2lc_batch_run(self.checker._ctx, self._b)
         if rc:
             raise S2LCError(rc, self.checker.last_error())
 
     def results(self, with_witness=True, as_numpy=False) -> List[CheckResult]:
+        self._check_attached()
         n = len(self.histories)
         res = (c_result * max(n, 1))()
         rc = lib().s2lc_batch_results(self.checker._ctx, self._b, res, int(with_witness))
@@ -586,6 +595,7 @@ class Batch:
         """s2lc_batch_results_flat: numpy arrays (verdict, reason, configs,
         rounds per history; certified Ok witnesses as one int64 array of op ids
         with offsets: history i's witness = witness_ids[offs[i]:offs[i+1]])."""
+        self._check_attached()
         n = len(self.histories)
         out = {"verdict": np.zeros(n, np.int32), "reason": np.zeros(n, np.int32),
                "configs": np.zeros(n, np.uint64), "rounds": np.zeros(n, np.uint64),
@@ -766,6 +776,7 @@ class Checker:
             # pool) instead of faulting in fresh pages. The pipe batch is not
             # read again before its next load().
             b.histories = []
+            b._detached = True
             return o
 
         outs = []

@@ -231,3 +231,19 @@ def test_illegal_partial_prefix(checker):
         ids = [e.Id for e in h.events()]
         assert len(set(r.partial)) == len(r.partial) and set(r.partial) <= set(ids)
         assert len(r.partial) < h.info()["n_ops"]
+
+
+def test_pipelined_batches_refuse_reads_after_release(checker):
+    """check_jsonl_many releases each slice's host histories once certified:
+    its kept device batches then refuse run() / results() until a load()."""
+    import pytest
+    from s2_verification_amd import workloads as W
+    blobs = [s2.simulate_jsonl(**W.c4_params(sd)) for sd in range(40, 60)]
+    checker.check_jsonl_many(blobs, threads=2, slices=2)
+    b = checker._pipe[0]
+    for call in (b.run, b.results, b.results_flat):
+        with pytest.raises(RuntimeError):
+            call()
+    b.load(s2.load_many(blobs[:3]))
+    b.run()
+    assert len(b.results()) == 3
