@@ -272,12 +272,17 @@ int or_check_reduced(const or_event* ev, size_t n_ev, uint64_t max_configs, uint
         for (int k = 0; k < nk; k++) {
           /* I-op identity child only when the op holds minret */
           if (c.idefer && o->cls == 2 && rs_eq(&kids[k], ps) && o->ret != mr) {
-            /* unless it is also the opt outcome (opt == s) */
+            /* unless it is also the opt outcome (guards pass and opt == s: a
+             * 0-record append with no hashes); with failing guards the
+             * child is the identity outcome alone, deferred like any other */
+            const or_event* in = o->in;
+            const int guards = !(in->batch_tok && (ps->tok == 0 || ps->tok != in->batch_tok)) &&
+                               !(in->has_msn && in->msn != ps->tail);
             rst opt;
-            opt.tail = ps->tail + o->in->num_records;
-            opt.hash = or_fold(ps->hash, o->in->hashes, o->in->n_hashes);
-            opt.tok = o->in->set_tok ? o->in->set_tok : ps->tok;
-            if (!rs_eq(&opt, ps)) continue;
+            opt.tail = ps->tail + in->num_records;
+            opt.hash = or_fold(ps->hash, in->hashes, in->n_hashes);
+            opt.tok = in->set_tok ? in->set_tok : ps->tok;
+            if (!guards || !rs_eq(&opt, ps)) continue;
           }
           memcpy(tmp, pc, cw * sizeof(uint16_t));
           tmp[q]++;

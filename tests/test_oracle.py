@@ -56,6 +56,55 @@ def test_wgl_matches_brute_force_on_random_histories():
     assert seen == {"Ok", "Illegal"}
 
 
+def test_u64_regimes_wgl_brute_reduced_agree():
+    """The u64 edges of s2Model.Step (main.go:279 wrap, main_test.go:313-343
+    truncation) on concurrent histories: num_records independent of the hash
+    count, tails across 2^32 and past 2^64, zero-record appends with hashes,
+    match_seq_num = tail +- 2^32. Brute force = the WGL restatement = the
+    reduced search with every reduction ablation; every code regime of the
+    checker (tests/helpers.py u64_regime) gets both verdicts."""
+    import collections
+
+    from helpers import U64_REGIMES, random_history_u64, u64_regime
+    rng = random.Random(5)
+    seen = collections.Counter()
+    for i in range(1200):
+        ev = random_history_u64(rng, rng.randint(1, 9), n_clients=rng.randint(1, 4), regime=U64_REGIMES[i % 4])
+        w, _ = orc.check_wgl(ev)
+        assert orc.check_brute(ev)[0] == w, ev
+        for off in (0, 1, 2, 4, 8):
+            assert orc.check_reduced(ev, reductions_off=off)[0] == w, (off, ev)
+        seen[(u64_regime(ev).split("+")[0], w)] += 1
+        seen[("zh", w)] += "+zh" in u64_regime(ev)
+    for r in ("tail32", "nowrap", "wrap", "zh"):
+        assert seen[(r, "Ok")] >= 20 and seen[(r, "Illegal")] >= 20, seen
+
+
+def test_reduced_search_on_u64_hard_variants():
+    """H174's u64-regime variants (helpers.hard_variant) on the CPU reduced
+    search against the committed H174 fixtures: a prepended 2^32-record append
+    shifts the search by one round, exact match_seq_nums leave it unchanged, a
+    prepended zero-record append with a hash gives the P2-off search, and a
+    match_seq_num 2^32 above the true tail is Illegal."""
+    import s2_verification_amd as s2
+    from helpers import config_digest, golden, hard_variant
+
+    from s2_verification_amd import workloads as W
+    g = golden("hard_round_counts.json")["H174"]
+    assert config_digest("H174") == g["digest"]
+    ev = W.config_history("H174").events()
+    want = {"above32": ("Ok", [1] + g["0"]["counts"]), "msn_exact": ("Ok", g["0"]["counts"]),
+            "zero_hash": ("Ok", g["2"]["counts"])}
+    for v in ("above32", "msn_exact", "zero_hash", "stale_msn"):
+        hv = s2.History.from_events(hard_variant(ev, v))
+        assert hv.info()["n_chains"] == 174
+        r, st = orc.check_reduced(orc.from_s2lc_numpy(hv.events_numpy(), owner=hv), round_counts=True)
+        if v == "stale_msn":
+            assert r == "Illegal" and st["rounds"] < g["0"]["rounds"], (r, st["rounds"])
+        else:
+            assert (r, st["round_counts"]) == want[v], v
+
+
 def test_unmatched_events_are_illegal():
     """A call without a return (or a return before its call) never leaves checkSingle's list."""
     call = {"kind": "call", "op_id": 1, "input_type": 1}
