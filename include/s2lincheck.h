@@ -463,15 +463,21 @@ int s2lc_dist_frontier_load(s2lc_dist* d, void* buf, uint64_t n);
  *   s2lc_dist_x_begin   the device run state from this rank's frontier (after
  *                       s2lc_dist_keep_owned or a partitioned round)
  *   s2lc_dist_x_send    expand + close the frontier and copy the staged
- *                       children into world fixed-capacity blocks of
- *                       (cap + 1) * config_bytes bytes, owner-major, a header
- *                       in each block's first slot (count, found, staging
- *                       overflow, the sender's largest block and total)
- *   (caller)            equal-split all-to-all of send into recv (no sizes)
- *   s2lc_dist_x_recv    decide the round from the received headers and insert
- *                       this rank's configurations; *round = its number; recv
- *                       is the next frontier (kept alive by the caller for at
- *                       least 8 rounds: a re-run reads it)
+ *                       children the OTHER ranks own into world - 1
+ *                       fixed-capacity blocks of (cap + 1) * config_bytes
+ *                       bytes, in rank order without this rank, a header in
+ *                       each block's first slot (count, found, staging
+ *                       overflow, the sender's largest block and staged
+ *                       total); this rank's own share stays in its staging
+ *                       (send may be NULL with world 1: nothing travels)
+ *   (caller)            all-to-all of one block to every other rank (fixed
+ *                       split sizes, none for itself: no sizes on the host)
+ *   s2lc_dist_x_recv    decide the round from the received headers and its
+ *                       own, insert the received configurations and its own
+ *                       share; *round = its number; recv and the library's
+ *                       staging are the next frontier (recv kept alive by the
+ *                       caller for at least 8 rounds: a re-run reads it;
+ *                       NULL with world 1)
  *   s2lc_dist_x_wait    wait for a queued round and read its status; every
  *                       rank reads the same decision
  *   s2lc_dist_x_rewind  a round whose status is S2LC_DIST_X_CAPACITY inserted

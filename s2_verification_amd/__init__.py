@@ -750,7 +750,15 @@ class Checker:
         the certification of slice k also runs beside the decode of slice k+2
         on a thread of its own, instead of between the decodes. Two device
         batches alternate and are kept on the checker for the next call (a
-        long-running checker: warm buffers)."""
+        long-running checker: warm buffers).
+
+        A context is single-threaded (include/s2lincheck.h): the device stage
+        (load + run) and the certification (results_flat) of different slices
+        run on different threads, so each takes the checker's lock around its
+        context calls (they had shared the context's error slot and
+        its stream unguarded). The decode (s2lc_load_jsonl_many) needs no
+        context and runs beside either."""
+        import threading
         from concurrent.futures import ThreadPoolExecutor
         n = len(blobs)
         S = max(1, min(int(slices), n))
@@ -759,18 +767,22 @@ class Checker:
             overlap = os.environ.get("S2LC_PIPE_OVERLAP", "0") == "1"
         if not hasattr(self, "_pipe"):
             self._pipe = [None, None]
+            self._ctx_lock = threading.Lock()
+        lock = self._ctx_lock
 
         def device(slot, hs):
-            b = self._pipe[slot]
-            if b is None:
-                b = self._pipe[slot] = Batch(self, hs)
-            else:
-                b.load(hs)
-            b.run()
+            with lock:
+                b = self._pipe[slot]
+                if b is None:
+                    b = self._pipe[slot] = Batch(self, hs)
+                else:
+                    b.load(hs)
+                b.run()
             return b
 
         def certify(b):
-            o = b.results_flat(with_witness)
+            with lock:
+                o = b.results_flat(with_witness)
             # release the slice's host histories as soon as they are certified:
             # the next slice's decode then reuses their storage (the history
             # pool) instead of faulting in fresh pages. The pipe batch is not

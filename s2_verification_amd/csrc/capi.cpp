@@ -1091,12 +1091,12 @@ int s2lc_dist_x_begin(s2lc_dist* x) {
 }
 
 int s2lc_dist_x_send(s2lc_dist* x, void* send, uint32_t cap) {
-  if (!x || !send || !cap) return S2LC_EINVAL;
+  if (!x) return S2LC_EINVAL;  // (send / cap: checked by dist_x_send; NULL send with world 1)
   return dist_x_send(x->d, (uint8_t*)send, cap, x->ctx->err);
 }
 
 int s2lc_dist_x_recv(s2lc_dist* x, void* recv, uint32_t cap, uint32_t* round) {
-  if (!x || !recv || !cap) return S2LC_EINVAL;
+  if (!x) return S2LC_EINVAL;  // (recv / cap: checked by dist_x_recv; NULL recv with world 1)
   return dist_x_recv(x->d, (uint8_t*)recv, cap, round, x->ctx->err);
 }
 

@@ -634,6 +634,8 @@ int dist_create(DistLevel& d, const History* h, uint32_t rank, uint32_t world, u
 
 void dist_release(DistLevel& d) {
   if (d.xrun) (void)hipFree(d.xrun);
+  if (d.xself) (void)hipFree(d.xself);
+  d.xself = nullptr;
   if (d.xstat) (void)hipHostFree(d.xstat);
   for (hipEvent_t& e : d.xev) {
     if (e) (void)hipEventDestroy(e);
@@ -662,10 +664,11 @@ static LvParams dist_params(DistLevel& d) {
   p.trace = d.trace; p.trace_cap = d.trace_cap;
   p.ctl = reinterpret_cast<LvCtl*>(L.ctl);
   p.world = d.world; p.own_cnt = d.own_cnt; p.own_pos = d.own_pos;
-  // local staging (the closed children of this rank): the array that does not
-  // hold the current frontier
-  p.stg = d.cur == L.stg[0] ? L.stg[1] : L.stg[0];
-  p.cur = d.cur; p.cur_idx = L.idx[d.cur_sel];
+  // local staging (the closed children of this rank): the array that holds
+  // no part of the current frontier
+  p.stg = (d.cur == L.stg[0] || d.cur_loc == L.stg[0]) ? L.stg[1] : L.stg[0];
+  p.cur = d.cur; p.cur_loc = d.cur_loc; p.cur_idx = L.idx[d.cur_sel];
+  p.rank = d.rank;
   p.tgid = d.rank << 29;
   p.witness_host = 1;
   return p;
@@ -761,6 +764,7 @@ int dist_insert(DistLevel& d, uint8_t* recv, uint64_t n_recv, uint64_t* n_next, 
   LVCHK(hipEventElapsedTime(&ms, L.ev[0], L.ev[1]));
   d.ms += ms;
   d.cur = recv;
+  d.cur_loc = nullptr;
   d.cur_sel = sel;
   d.nf = hc->nnext;
   d.tnext += hc->nnext;
@@ -793,6 +797,7 @@ static const bool g_xsync = getenv("S2LC_XSYNC") != nullptr;
 static int dist_x_alloc(DistLevel& d, std::string& err) {
   if (d.xrun) return 0;
   LVCHK(hipMalloc(&d.xrun, sizeof(LvRun)));
+  LVCHK(hipMalloc(&d.xself, sizeof(LvXHdr)));
   LVCHK(hipHostMalloc(&d.xstat, LV_XRING * sizeof(LvXStat), hipHostMallocMapped));
   for (hipEvent_t& e : d.xev) LVCHK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
   return 0;
@@ -831,12 +836,27 @@ static LvParams dist_x_params(DistLevel& d, uint32_t cap) {
   p.xcap = cap;
   p.round = d.xround;
   p.ctl = reinterpret_cast<LvCtl*>(d.b.lv.ctl) + (d.xround & 1);
+  p.xself = reinterpret_cast<LvXHdr*>(d.xself);
   return p;
+}
+
+// (smallest frontier, staged count) of the latest status the host can see
+// without waiting: sizes the grids of the next queued round (any grid is
+// correct, the kernels stride)
+static void dist_x_hint(const DistLevel& d, uint32_t& hint_nf, uint64_t& hint_staged) {
+  hint_nf = UINT32_MAX;
+  hint_staged = UINT64_MAX;
+  const volatile LvXStat* xs = reinterpret_cast<const volatile LvXStat*>(d.xstat);
+  for (uint32_t back = 1; back <= 2 && back < d.xround; ++back) {
+    const uint32_t r = d.xround - back;
+    const volatile LvXStat& e = xs[r % LV_XRING];
+    if (e.round == r && !e.done) { hint_nf = back == 1 ? e.nf : UINT32_MAX; hint_staged = e.staged; break; }
+  }
 }
 
 int dist_x_send(DistLevel& d, uint8_t* send, uint32_t cap, std::string& err) {
   if (!d.xrun) { err = "dist_x_begin first"; return S2LC_EINVAL; }
-  if (cap == 0 || !send) { err = "exchange capacity 0 / null send buffer"; return S2LC_EINVAL; }
+  if (cap == 0 || (!send && d.world > 1)) { err = "exchange capacity 0 / null send buffer"; return S2LC_EINVAL; }
   hipStream_t st = d.stream;
   LvParams p = dist_x_params(d, cap);
   p.f0 = 0;
@@ -850,19 +870,13 @@ int dist_x_send(DistLevel& d, uint8_t* send, uint32_t cap, std::string& err) {
   // grids from the latest status the host can see without waiting (this
   // rank's frontier after the previous round, when published): a narrow
   // round gets small grids (any grid is correct; the kernels stride)
-  uint32_t hint_nf = UINT32_MAX;
-  uint64_t hint_staged = UINT64_MAX;
-  {
-    const volatile LvXStat* xs = reinterpret_cast<const volatile LvXStat*>(d.xstat);
-    for (uint32_t back = 1; back <= 2 && back < d.xround; ++back) {
-      const uint32_t r = d.xround - back;
-      const volatile LvXStat& e = xs[r % LV_XRING];
-      if (e.round == r && !e.done) { hint_nf = back == 1 ? e.nf : UINT32_MAX; hint_staged = e.staged; break; }
-    }
-  }
+  uint32_t hint_nf;
+  uint64_t hint_staged;
+  dist_x_hint(d, hint_nf, hint_staged);
   const uint32_t ncu = (uint32_t)n_cus(err);
   const uint32_t g_round = hint_nf <= 16 ? std::min<uint32_t>(d.b.lv.grid_round, ncu / 4) : d.b.lv.grid_round;
-  const uint32_t g_send = hint_staged <= 4096 ? std::max<uint32_t>(1, ncu / 16) : ncu;
+  // (one rank: lv_xsend copies nothing, it only writes the own header)
+  const uint32_t g_send = d.world == 1 ? 1u : hint_staged <= 4096 ? std::max<uint32_t>(1, ncu / 16) : ncu;
   p.ctl_next = reinterpret_cast<LvCtl*>(d.b.lv.ctl) + ((d.xround + 1) & 1);
   LVCHK(lv_dispatch(d.nq, LK_ROUND, g_round, p, st));
   p.ctl_next = nullptr;
@@ -876,30 +890,41 @@ int dist_x_send(DistLevel& d, uint8_t* send, uint32_t cap, std::string& err) {
 
 int dist_x_recv(DistLevel& d, uint8_t* recv, uint32_t cap, uint32_t* round, std::string& err) {
   if (!d.xrun) { err = "dist_x_begin first"; return S2LC_EINVAL; }
-  if (cap == 0 || !recv) { err = "exchange capacity 0 / null receive buffer"; return S2LC_EINVAL; }
-  const uint64_t slots = (uint64_t)d.world * (cap + 1);
-  // (what one round inserts stays within the next frontier's index list, and
-  // the device stops recording the trace before the pool fills)
-  if ((uint64_t)d.world * cap > d.b.lv.scap) { err = "exchange blocks exceed the frontier capacity"; return S2LC_ENOMEM; }
+  if (cap == 0 || (!recv && d.world > 1)) { err = "exchange capacity 0 / null receive buffer"; return S2LC_EINVAL; }
+  // the other ranks' blocks (the own share stays in the local staging)
+  const uint64_t slots = (uint64_t)(d.world - 1) * (cap + 1);
+  // (what one round inserts: at most the local staging plus the received
+  // blocks, which the table holds at under 3/4 load; the close stops the run
+  // if the next frontier's index list overflows, and the device stops
+  // recording the trace before the pool fills)
+  if ((uint64_t)(d.world - 1) * cap > d.b.lv.scap / 2) { err = "exchange blocks exceed the frontier capacity"; return S2LC_ENOMEM; }
   hipStream_t st = d.stream;
   const uint32_t r = d.xround % LV_XRING;
   d.xcur[r] = d.cur;
+  d.xcur_loc[r] = d.cur_loc;
   d.xsel[r] = d.cur_sel;
   const int sel = d.cur_sel ^ 1;
   LvParams p = dist_x_params(d, cap);
+  uint8_t* const loc = p.stg;  // this round's local staging (lv_round of dist_x_send staged there)
   p.stg = recv;
+  p.stg_loc = loc;
   p.nxt_idx = d.b.lv.idx[sel];
   p.dense = (uint32_t)slots;
   p.close_round = 1;
   void* xs = nullptr;
   LVCHK(hipHostGetDevicePointer(&xs, d.xstat, 0));
   p.xstat = reinterpret_cast<LvXStat*>(xs);
+  uint32_t hint_nf;
+  uint64_t hint_staged;
+  dist_x_hint(d, hint_nf, hint_staged);
   const uint32_t max_grid = (uint32_t)n_cus(err) * 8;
-  LVCHK(lv_dispatch(d.nq, LK_INSERT, (uint32_t)std::min<uint64_t>(max_grid, (slots + LV_BLOCK - 1) / LV_BLOCK), p, st));
+  const uint64_t want = slots + std::min<uint64_t>(hint_staged, (uint64_t)max_grid * LV_BLOCK);
+  LVCHK(lv_dispatch(d.nq, LK_INSERT, (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>(max_grid, (want + LV_BLOCK - 1) / LV_BLOCK)), p, st));
   LVCHK(hipEventRecord(d.xev[r], st));
   if (g_xsync) LVCHK(hipStreamSynchronize(st));
   if (round) *round = d.xround;
   d.cur = recv;
+  d.cur_loc = loc;
   d.cur_sel = sel;
   d.xround++;
   return 0;
@@ -928,6 +953,7 @@ int dist_x_rewind(DistLevel& d, uint32_t round, std::string& err) {
   }
   LVCHK(hipStreamSynchronize(d.stream));
   d.cur = d.xcur[round % LV_XRING];
+  d.cur_loc = d.xcur_loc[round % LV_XRING];
   d.cur_sel = d.xsel[round % LV_XRING];
   d.xround = round;
   d.xfresh = true;
@@ -958,6 +984,7 @@ int dist_x_end(DistLevel& d, uint32_t* done, uint64_t* configs, std::string& err
 // every decision, is the same on all ranks.
 int dist_local_round(DistLevel& d, uint64_t* n_next, int* found, std::string& err) {
   LevelBufs& L = d.b.lv;
+  if (d.cur_loc) { err = "the frontier is partitioned: gather it (frontier_pack / frontier_load) first"; return S2LC_EINVAL; }
   LvCtl* hc = reinterpret_cast<LvCtl*>(L.h_ctl);
   const uint32_t max_grid = (uint32_t)n_cus(err) * 8;
   hipStream_t st = d.stream;
@@ -989,6 +1016,7 @@ int dist_local_round(DistLevel& d, uint64_t* n_next, int* found, std::string& er
     return 0;
   }
   d.cur = p.stg;
+  d.cur_loc = nullptr;
   d.cur_sel ^= 1;
   d.nf = hc->nnext;
   d.tnext += hc->nnext;
@@ -1015,6 +1043,7 @@ int dist_local_run(DistLevel& d, uint32_t wide, uint64_t* n_next, int* found, ui
   LevelBufs& L = d.b.lv;
   *rounds = 0;
   *found = 0;
+  if (d.cur_loc) { err = "the frontier is partitioned: gather it (frontier_pack / frontier_load) first"; return S2LC_EINVAL; }
   if (!L.grid_persist || L.persist_refused || d.round == 0 || wide < 2) {
     err = "persistent replicated rounds unavailable";
     return S2LC_EUNSUPPORTED;
@@ -1103,6 +1132,7 @@ int dist_local_run(DistLevel& d, uint32_t wide, uint64_t* n_next, int* found, ui
     }
     LVCHK(hipStreamSynchronize(st));
     d.cur = d.snap;
+    d.cur_loc = nullptr;
     d.cur_sel = 0;
     err = "persistent replicated rounds refused or timed out: host-driven rounds";
     return S2LC_EUNSUPPORTED;
@@ -1124,6 +1154,7 @@ int dist_local_run(DistLevel& d, uint32_t wide, uint64_t* n_next, int* found, ui
   if (fin.done == LVR_EMPTY) { d.nf = 0; *n_next = 0; return 0; }
   d.cur_sel = (int)(fin.round & 1);  // the last closed round's staging and index list
   d.cur = L.stg[d.cur_sel];
+  d.cur_loc = nullptr;
   d.nf = fin.nf;
   *n_next = fin.nf;
   return 0;
@@ -1176,6 +1207,7 @@ int dist_frontier_load(DistLevel& d, uint8_t* buf, uint64_t n, std::string& err)
   LVCHK(hipMemsetAsync(L.ht[0], 0xFF, ((size_t)L.ht_mask + 1) * 8, st));
   LVCHK(hipStreamSynchronize(st));
   d.cur = buf;
+  d.cur_loc = nullptr;
   d.cur_sel = sel;
   d.nf = (uint32_t)n;
   return 0;

@@ -39,6 +39,10 @@ constexpr uint32_t LV_HOLE = 0xFFFFFFFEu;  // LCfg::move of a reserved, unused s
 constexpr int LV_BLOCK = 256;
 constexpr uint32_t LV_RESERVE = 8;          // staging slots a wave reserves per atomic
 constexpr unsigned long long LV_PENDING = 1ull << 31;  // table entry whose configuration is still landing (lv_persist)
+// Index bit of a frontier / table entry in a partitioned round (distributed
+// search): the configuration lives in the rank's local staging (its own share
+// of what it expanded, never sent), not in the received exchange blocks.
+constexpr uint32_t LV_LOCAL = 1u << 30;
 
 // A staged / frontier configuration: 128 + 128 * NQ bytes. The header fills
 // one 128-byte line and every 64-counter block another, so no two
@@ -79,7 +83,8 @@ struct LvCtl {
   unsigned long long prof_end;  // S2LC_PROF: latest expansion end of the round (wall clock)
   uint32_t stop;      // lv_persist: the run's deadline passed (set by workgroup 0 before the round's barrier)
   uint32_t xblocks;   // lv_xsend blocks finished (the last one writes the exchange headers)
-  uint32_t _pad[2];
+  uint32_t staged;    // closed children staged this round (lv_round, grid rounds)
+  uint32_t _pad;
   uint32_t lo[LV_STRIPES];        // lv_insert: first slot of each stripe not inserted yet (chunked rounds)
   uint32_t cnt[LV_STRIPES * 16];  // stripe s reserves slots at cnt[16 s] (holes included)
 };
@@ -168,12 +173,25 @@ struct LvParams {
   // variable-size buckets above) and the host-mapped status ring
   uint32_t xcap;
   struct LvXStat* xstat;
+  // partitioned rounds: the rank keeps its own share of what it staged
+  // (LV_LOCAL): cur_loc holds the current frontier's local part, stg_loc this
+  // round's local staging (lv_insert), xself the rank's own exchange header
+  uint32_t rank;
+  const uint8_t* cur_loc;
+  uint8_t* stg_loc;
+  struct LvXHdr* xself;
   unsigned long long* prof;  // S2LC_PROF builds: lv_round phase cycles (nullable)
   // per-op longest partial linearizations (s2lc_check_partials): for every
   // inserted configuration c and chain j, pmax[cs[j] + cnt_c[j]] = max of
   // (|c| << 32 | c's trace id), |c| = its linearized ops (nullable)
   unsigned long long* pmax;
 };
+
+// ---- distributed: owner of a configuration ---------------------------------
+// Independent of the table slot (low fingerprint bits) and tag (high bits).
+__host__ __device__ __forceinline__ uint32_t lv_owner(uint64_t fp, uint32_t world) {
+  return (uint32_t)(((fp * 0xD6E8FEB86659FD93ull) >> 40) % world);
+}
 
 template <int NQ>
 __device__ __forceinline__ const LCfg<NQ>* lv_cfg(const uint8_t* base, uint32_t i) {
@@ -740,6 +758,7 @@ __device__ __forceinline__ bool lv_expand(const LvParams& p, const LvRoundIn& in
   }
   unsigned long long kids = 0;
   uint32_t closed = 0;  // children closed by this wave (wave-uniform)
+  uint32_t staged = 0;  // children it staged (grid rounds)
 #ifdef S2LC_PROF
   unsigned long long lv_acc[10] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0}, lv_t = 0;
 #endif
@@ -749,7 +768,12 @@ __device__ __forceinline__ bool lv_expand(const LvParams& p, const LvRoundIn& in
     const uint32_t f = f0 + it / S;
     const uint32_t slice = it % S;
     // parent configuration (round 0: the all-zero initial one)
-    const LCfg<NQ>* pc = p.init ? nullptr : lv_cfg<NQ>(p.cur, p.cur_idx[f]);
+    const LCfg<NQ>* pc = nullptr;
+    if (!p.init) {
+      const uint32_t ci = p.cur_idx[f];
+      // (a partitioned round's frontier: its local part in cur_loc; lv_round only)
+      pc = (!FUSED && (ci & LV_LOCAL)) ? lv_cfg<NQ>(p.cur_loc, ci & ~LV_LOCAL) : lv_cfg<NQ>(p.cur, ci);
+    }
     const bool has_parent = pc != nullptr;
     State ps{0, 0, 0};
     uint32_t pmin = 0, ptrace = TRACE_NONE;
@@ -1022,6 +1046,7 @@ __device__ __forceinline__ bool lv_expand(const LvParams& p, const LvRoundIn& in
             lv_stage_insert<NQ>(p, in, stripe, rk, rleft, cs_, fp_of(), cdx, mr, ptrace, mv, cnt, d);
           } else {
             lv_stage<NQ>(p, stripe, rk, rleft, cs_, fp_of(), cdx, mr, ptrace, mv, cnt, d);
+            ++staged;
           }
         }
         // back to the parent's heads on the chains this child advanced
@@ -1041,6 +1066,7 @@ __device__ __forceinline__ bool lv_expand(const LvParams& p, const LvRoundIn& in
   if (MODE == 0 && rleft) lv_release<NQ>(p, stripe, rk, rleft);
   if (lane == 0 && kids) atomicAdd(&p.ctl->children, kids);
   if (lane == 0 && closed) atomicAdd(&p.ctl->closed, closed);
+  if (!FUSED && lane == 0 && staged) atomicAdd(&p.ctl->staged, staged);
   return wave_id < items;
 }
 
@@ -1235,42 +1261,53 @@ __global__ __launch_bounds__(LV_BLOCK) void lv_insert(LvParams p) {
   const int lane = (int)(threadIdx.x & 63), wv = (int)(threadIdx.x >> 6);
   const bool wit = p.run ? p.run->witness != 0 : p.witness_host != 0;
   const uint32_t tbase = p.run ? (uint32_t)p.run->tnext : p.tbase_host;
-  uint32_t lo = 0, hi = 0;  // this lane's stripe range (striped mode)
+  // an exchanged round (p.xcap) inserts two sources: the exchange blocks it
+  // received (p.stg, p.dense slots: the other ranks' children this rank
+  // owns) and its own share of what it staged itself (p.stg_loc, striped,
+  // never sent: entries marked LV_LOCAL)
+  const bool xm = p.xcap != 0;
+  uint32_t lo = 0, hi = 0;  // this lane's stripe range (striped mode; exchanged rounds: the local staging)
   if (p.fused) {
     // lv_round inserted the children itself: only the round's close is left
-  } else if (p.dense) {
+  } else if (p.dense && !xm) {
     hi = p.dense;
   } else if (!ld_agent(&p.ctl->overflow)) {
     lo = p.ctl->lo[lane];
     hi = min(ld_agent(&p.ctl->cnt[16 * lane]), p.scs);
   }
-  // iterations: the longest stripe (striped) / the dense range, block-uniform
-  uint32_t n_it;
-  if (p.dense) {
-    n_it = (p.dense + LV_BLOCK - 1) / LV_BLOCK;
-  } else {
-    const uint32_t m = wave_max_u32(hi);
-    n_it = (m + LV_BLOCK / 64 - 1) / (LV_BLOCK / 64);  // rows of 4 slots per stripe per block iteration
-  }
+  // iterations, block-uniform: the dense range, then the longest stripe (rows
+  // of 4 slots per stripe per block iteration)
+  const uint32_t n_dense = p.dense ? (p.dense + LV_BLOCK - 1) / LV_BLOCK : 0u;
+  const uint32_t n_str = (p.dense && !xm) ? 0u : (wave_max_u32(hi) + LV_BLOCK / 64 - 1) / (LV_BLOCK / 64);
+  const uint32_t n_it = n_dense + n_str;
+  uint8_t* const loc = xm ? p.stg_loc : p.stg;  // the striped source
   for (uint32_t itb = blockIdx.x; itb < n_it; itb += gridDim.x) {
     bool win = false;
     uint32_t slot = 0, k = 0;
     LCfg<NQ>* c = nullptr;
     bool valid;
-    if (p.dense) {
+    if (itb < n_dense) {
       k = itb * LV_BLOCK + threadIdx.x;
       valid = k < p.dense;
-      if (valid && p.xcap) {  // exchange blocks: slot 0 is the header, then the block's count
+      if (valid && xm) {  // exchange blocks: slot 0 is the header, then the block's count
         const uint32_t b = k / (p.xcap + 1), i = k - b * (p.xcap + 1);
         valid = i >= 1 && i - 1 < min(lv_xhdr<NQ>(p.stg, b, p.xcap)->count, p.xcap);
       }
+      if (valid) c = lv_cfg<NQ>(p.stg, k);
     } else {
-      const uint32_t i = itb * (LV_BLOCK / 64) + (uint32_t)wv;
+      const uint32_t i = (itb - n_dense) * (LV_BLOCK / 64) + (uint32_t)wv;
       valid = i >= lo && i < hi;
       k = (uint32_t)lane * p.scs + i;
+      if (valid) {
+        c = lv_cfg<NQ>(loc, k);
+        // exchanged rounds: only the configurations this rank owns (lv_xsend sent the rest)
+        if (xm) {
+          valid = c->move == LV_HOLE || lv_owner(c->fp, p.world) == p.rank;
+          k |= LV_LOCAL;
+        }
+      }
     }
     if (valid) {
-      c = lv_cfg<NQ>(p.stg, k);
       if (c->move != LV_HOLE) {
         const uint64_t fp = c->fp;
         const uint32_t tag = (uint32_t)(fp >> 32);
@@ -1279,7 +1316,11 @@ __global__ __launch_bounds__(LV_BLOCK) void lv_insert(LvParams p) {
         for (;;) {
           const unsigned long long prev = atomicCAS(&p.ht[slot], HT_EMPTY, mine);
           if (prev == HT_EMPTY) { win = true; break; }
-          if ((uint32_t)(prev >> 32) == tag && lv_eq<NQ>(lv_cfg<NQ>(p.stg, (uint32_t)prev), c, p.K)) break;
+          if ((uint32_t)(prev >> 32) == tag) {
+            const uint32_t pk = (uint32_t)prev;
+            const LCfg<NQ>* o = (pk & LV_LOCAL) ? lv_cfg<NQ>(loc, pk & ~LV_LOCAL) : lv_cfg<NQ>(p.stg, pk);
+            if (lv_eq<NQ>(o, c, p.K)) break;
+          }
           slot = (slot + 1) & p.ht_mask;
         }
       }
@@ -1299,7 +1340,7 @@ __global__ __launch_bounds__(LV_BLOCK) void lv_insert(LvParams p) {
     n += (uint32_t)__popcll(bw & ((1ull << lane) - 1));
     __syncthreads();  // s_wcnt / s_base are rewritten next iteration
     if (win) {
-      p.nxt_idx[n] = k;
+      if (n < p.scap) p.nxt_idx[n] = k;  // (beyond: the close stops the run, lv_xclose)
       c->slot = slot;
       if (wit) {
         c->trace = p.tgid + tbase + n;
@@ -1535,11 +1576,6 @@ __global__ __attribute__((unused)) void lv_run_init(LvRun* R, unsigned long long
   R->t_last = wall_clock64(); R->narrow_ticks = 0; R->wide_ticks = 0; R->solo_ticks = 0;
 }
 
-// ---- distributed: owner of a configuration ---------------------------------
-// Independent of the table slot (low fingerprint bits) and tag (high bits).
-__host__ __device__ __forceinline__ uint32_t lv_owner(uint64_t fp, uint32_t world) {
-  return (uint32_t)(((fp * 0xD6E8FEB86659FD93ull) >> 40) % world);
-}
 
 // Distributed staging walk: k -> stripe k & 63, index k >> 6, for k below
 // p.dense = 64 * (the longest stripe) (set by the host from the round's counters).
@@ -1592,16 +1628,19 @@ __device__ __forceinline__ uint32_t lv_stage_dense(const LvParams& p) {
   return 64u * wave_max_u32(min(ld_agent(&p.ctl->cnt[16 * lane]), p.scs));
 }
 
+// Block of owner / sender o in a rank's send / receive buffer: the world - 1
+// other ranks in rank order (the rank's own share never travels)
+__host__ __device__ __forceinline__ uint32_t lv_xblk(uint32_t o, uint32_t rank) { return o < rank ? o : o - 1; }
+
 // the exchange headers (one wave): block o's count, the sender's largest
-// block and total, the round's found / staging-overflow flags; clears the
-// owner counters for the next round
+// block and staged total, the round's found / staging-overflow flags; clears
+// the owner counters for the next round. The rank's own header goes to
+// p.xself (its share stays in its local staging)
 template <int NQ>
 __device__ __forceinline__ void lv_xhdr_wave(const LvParams& p) {
   const uint32_t lane = threadIdx.x & 63;
-  const uint32_t c = lane < p.world ? atomicExch(&p.own_cnt[lane], 0u) : 0u;
+  const uint32_t c = (lane < p.world && lane != p.rank) ? atomicExch(&p.own_cnt[lane], 0u) : 0u;
   const uint32_t mb = wave_max_u32(c);
-  unsigned long long tot = c;
-  for (int d = 32; d >= 1; d >>= 1) tot += __shfl_xor(tot, d, 64);
   if (lane < p.world) {
     LvXHdr h;
     h.count = c; h.maxblk = mb;
@@ -1610,46 +1649,70 @@ __device__ __forceinline__ void lv_xhdr_wave(const LvParams& p) {
     h.fp4 = ld_agent(&p.ctl->found_p4);
     h.sovf = ld_agent(&p.ctl->overflow);
     h.nf = p.run->nf;
-    h.staged = tot;
-    *lv_xhdr<NQ>(p.send, lane, p.xcap) = h;
+    h.staged = ld_agent(&p.ctl->staged);
+    *(lane == p.rank ? p.xself : lv_xhdr<NQ>(p.send, lv_xblk(lane, p.rank), p.xcap)) = h;
   }
 }
 
-// stage -> fixed-capacity blocks: one wave per 64 staging slots (lane = stripe)
-// takes owner positions with atomics, then copies each of its configurations
-// cooperatively (16 bytes per lane); the last block to finish writes the
-// headers. It reads only the owner counters (device-scope atomics, complete
-// before each block's arrival) and values earlier kernels wrote, so the
-// hand-off needs no fence (an agent-scope __threadfence per block cost ~60 us
-// per round at 4 blocks per CU: MI355X_MICROARCH.md).
+// stage -> fixed-capacity blocks of the OTHER ranks: one wave per 64
+// staging slots (lane = stripe) takes owner positions (one atomic per owner
+// per wave), then the wave copies its configurations as one flat stream of
+// 16-byte pieces, every lane's loads in flight together; the rank's own
+// share stays in its staging (lv_insert reads it there). With one rank
+// nothing is copied: only the own header is written. The last block to
+// finish writes the headers. It reads only the owner counters (device-scope
+// atomics, complete before each block's arrival) and values earlier kernels
+// wrote, so the hand-off needs no fence (an agent-scope __threadfence per
+// block cost ~60 us per round at 4 blocks per CU: MI355X_MICROARCH.md).
 template <int NQ>
 __global__ __launch_bounds__(LV_BLOCK) void lv_xsend(LvParams p) {
   if (p.run->done) return;
   __shared__ uint32_t s_last;
+  __shared__ uint32_t s_to[LV_BLOCK], s_sl[LV_BLOCK];  // per wave: destination / source of its kept configurations
   constexpr uint32_t PER = sizeof(LCfg<NQ>) / 16;
   const uint32_t lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
-  const uint32_t dense = lv_stage_dense(p), cap = p.xcap;
+  const uint32_t dense = p.world > 1 ? lv_stage_dense(p) : 0u, cap = p.xcap;
   const uint4* src = reinterpret_cast<const uint4*>(p.stg);
   uint4* dst = reinterpret_cast<uint4*>(p.send);
   for (uint32_t k0 = (blockIdx.x * (LV_BLOCK / 64) + wv) * 64; k0 < dense; k0 += gridDim.x * LV_BLOCK) {
     const uint32_t i = k0 / 64, slot = lane * p.scs + i;
     bool v = i < min(ld_agent(&p.ctl->cnt[16 * lane]), p.scs);
-    uint32_t to = 0;
+    uint32_t o = p.rank;
     if (v) {
       const LCfg<NQ>* c = lv_cfg<NQ>(p.stg, slot);
       v = c->move != LV_HOLE;
-      if (v) {
-        const uint32_t o = lv_owner(c->fp, p.world);
-        const uint32_t pos = atomicAdd(&p.own_cnt[o], 1u);
-        v = pos < cap;
-        to = o * (cap + 1) + 1 + pos;
+      if (v) o = lv_owner(c->fp, p.world);
+    }
+    v = v && o != p.rank;
+    // positions: one atomic per owner present in the wave
+    uint32_t to = 0;
+    bool keep = false;
+    for (uint32_t w = 0; w < p.world; ++w) {
+      const uint64_t bw = __ballot(v && o == w);
+      if (!bw) continue;
+      uint32_t base = 0;
+      if (lane == (uint32_t)(__ffsll((unsigned long long)bw) - 1)) base = atomicAdd(&p.own_cnt[w], (uint32_t)__popcll(bw));
+      base = (uint32_t)__shfl((int)base, __ffsll((unsigned long long)bw) - 1, 64);
+      if (v && o == w) {
+        const uint32_t pos = base + (uint32_t)__popcll(bw & ((1ull << lane) - 1));
+        keep = pos < cap;
+        to = lv_xblk(w, p.rank) * (cap + 1) + 1 + pos;
       }
     }
-    for (uint64_t m = __ballot(v); m; m &= m - 1) {
-      const int l = __ffsll((unsigned long long)m) - 1;
-      const uint32_t d = (uint32_t)__shfl((int)to, l, 64), sl = (uint32_t)__shfl((int)slot, l, 64);
-      for (uint32_t c = lane; c < PER; c += 64) dst[(size_t)d * PER + c] = src[(size_t)sl * PER + c];
+    // the wave's kept configurations, as one stream of pieces: piece x of the
+    // n kept ones is piece x % PER of configuration x / PER
+    const uint64_t km = __ballot(keep);
+    const uint32_t nk = (uint32_t)__popcll(km);
+    const uint32_t my = (uint32_t)__popcll(km & ((1ull << lane) - 1));  // my rank among the kept lanes
+    if (keep) { s_to[wv * 64 + my] = to; s_sl[wv * 64 + my] = slot; }
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+#pragma unroll 4
+    for (uint32_t x = lane; x < nk * PER; x += 64) {
+      const uint32_t e = x / PER, c = x - e * PER;
+      dst[(size_t)s_to[wv * 64 + e] * PER + c] = src[(size_t)s_sl[wv * 64 + e] * PER + c];
     }
+    __builtin_amdgcn_wave_barrier();
   }
   __syncthreads();  // (every wave's owner atomics have returned)
   if (threadIdx.x == 0) s_last = atomicAdd(&p.ctl->xblocks, 1u) == gridDim.x - 1;
@@ -1664,8 +1727,8 @@ __device__ __forceinline__ LvXDecision lv_xdecide(const LvParams& p) {
   LvXDecision d;
   d.halt = 0; d.maxblk = 0; d.fpar = TRACE_NONE; d.fmov = LV_NONE; d.fp4 = 0; d.nf_global = 0; d.staged = 0;
   bool found = false, sovf = false;
-  for (uint32_t s = 0; s < p.world; ++s) {
-    const LvXHdr* h = lv_xhdr<NQ>(const_cast<uint8_t*>(p.stg), s, p.xcap);
+  for (uint32_t s = 0; s < p.world; ++s) {  // (in rank order: every rank takes the same found child)
+    const LvXHdr* h = s == p.rank ? p.xself : lv_xhdr<NQ>(const_cast<uint8_t*>(p.stg), lv_xblk(s, p.rank), p.xcap);
     d.maxblk = max(d.maxblk, h->maxblk);
     d.nf_global += h->nf;
     d.staged += h->staged;
@@ -1715,6 +1778,7 @@ __device__ __forceinline__ void lv_xclose(const LvParams& p, const LvXDecision& 
   R.round = p.round;
   R.configs += k.nn;
   R.max_frontier = max(R.max_frontier, k.nn);
+  if (k.nn > p.scap) R.done = LVR_ABORT;  // (the next frontier's index list is full)
   if (R.witness) {
     R.last_tbase = (uint32_t)R.tnext;
     R.tnext += k.nn;
@@ -1733,7 +1797,8 @@ __global__ __launch_bounds__(LV_BLOCK) void lv_keep(LvParams p, uint32_t rank) {
     bool mine = false;
     if (i < nf) {
       k = p.cur_idx[i];
-      mine = lv_owner(lv_cfg<NQ>(p.cur, k)->fp, p.world) == rank;
+      const uint8_t* base = (k & LV_LOCAL) ? p.cur_loc : p.cur;
+      mine = lv_owner(lv_cfg<NQ>(base, k & ~LV_LOCAL)->fp, p.world) == rank;
     }
     const uint32_t n = wave_alloc(&p.ctl->nnext, mine ? 1u : 0u);
     if (mine) p.nxt_idx[n] = k;
@@ -1747,7 +1812,8 @@ __global__ __launch_bounds__(LV_BLOCK) void lv_gather_frontier(LvParams p) {
   const uint64_t total = (uint64_t)p.f1 * PER;
   for (uint64_t i = (uint64_t)blockIdx.x * LV_BLOCK + threadIdx.x; i < total; i += (uint64_t)gridDim.x * LV_BLOCK) {
     const uint32_t f = (uint32_t)(i / PER), c = (uint32_t)(i % PER);
-    const uint4* src = reinterpret_cast<const uint4*>(lv_cfg<NQ>(p.cur, p.cur_idx[f]));
+    const uint32_t k = p.cur_idx[f];
+    const uint4* src = reinterpret_cast<const uint4*>(lv_cfg<NQ>((k & LV_LOCAL) ? p.cur_loc : p.cur, k & ~LV_LOCAL));
     reinterpret_cast<uint4*>(p.send + (uint64_t)f * sizeof(LCfg<NQ>))[c] = src[c];
   }
 }

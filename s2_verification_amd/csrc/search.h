@@ -250,6 +250,7 @@ struct DistLevel {
   hipStream_t stream = nullptr;
   bool own_stream = true;        // false: the context's (caller's) stream
   const uint8_t* cur = nullptr;  // current frontier: received buffer (caller-owned)
+  const uint8_t* cur_loc = nullptr;  // partitioned rounds: its local part (LV_LOCAL entries, a staging array)
   int cur_sel = 0;               // index list of the current frontier: b.lv.idx[cur_sel]
   uint32_t nf = 0, slot_hi = 0, round = 0;  // slot_hi: staging walk bound (64 x longest stripe)
   uint32_t found_parent = TRACE_NONE, found_move = TRACE_NONE, found_p4 = 0;
@@ -264,7 +265,9 @@ struct DistLevel {
   void* xstat = nullptr;
   hipEvent_t xev[8] = {};
   const uint8_t* xcur[8] = {};
+  const uint8_t* xcur_loc[8] = {};
   int xsel[8] = {};
+  void* xself = nullptr;         // this rank's own exchange header (its share is never sent)
   uint32_t xround = 0;           // the next round to queue
   bool xfresh = true;            // the next queued round zeroes its counters on the host
 };

@@ -134,13 +134,14 @@ class DistSearch:
     def x_begin(self):
         self._chk(lib().s2lc_dist_x_begin(self._d), "dist_x_begin")
 
-    def x_send(self, send: torch.Tensor, cap: int):
-        self._chk(lib().s2lc_dist_x_send(self._d, ctypes.c_void_p(send.data_ptr()), cap), "dist_x_send")
+    def x_send(self, send: Optional[torch.Tensor], cap: int):
+        ptr = ctypes.c_void_p(send.data_ptr() if send is not None else 0)
+        self._chk(lib().s2lc_dist_x_send(self._d, ptr, cap), "dist_x_send")
 
-    def x_recv(self, recv: torch.Tensor, cap: int) -> int:
+    def x_recv(self, recv: Optional[torch.Tensor], cap: int) -> int:
         r = ctypes.c_uint32(0)
-        self._chk(lib().s2lc_dist_x_recv(self._d, ctypes.c_void_p(recv.data_ptr()), cap, ctypes.byref(r)),
-                  "dist_x_recv")
+        ptr = ctypes.c_void_p(recv.data_ptr() if recv is not None else 0)
+        self._chk(lib().s2lc_dist_x_recv(self._d, ptr, cap, ctypes.byref(r)), "dist_x_recv")
         return r.value
 
     def x_wait(self, round_: int) -> c_dist_xstat:
@@ -176,13 +177,30 @@ class _Exchange:
         self.on_gpu = dist.get_backend(group) == "nccl"
         self.tdev = device if self.on_gpu else torch.device("cpu")
         self.world = dist.get_world_size(group)
+        self.rank = dist.get_rank(group)
         # the library launches on torch's current stream (Checker(stream=...)):
         # its kernels are ordered after the collectives on the device, with no
         # host synchronization in between
         self.same_stream = lib_stream != 0 and lib_stream == torch.cuda.current_stream(device).cuda_stream
+        # a caller stream that is not torch's current one: the
+        # collectives wait for the library's queued kernels, and the
+        # library's next kernels for the collectives, as stream waits on the
+        # device (the library skips its host wait on a caller's stream)
+        self.lib_ext = (torch.cuda.ExternalStream(lib_stream, device=device)
+                        if lib_stream != 0 and not self.same_stream and device.type == "cuda" else None)
+
+    def _pre(self):
+        """Before a collective (or a host copy) reads what the library wrote."""
+        if self.lib_ext is not None:
+            torch.cuda.current_stream(self.device).wait_stream(self.lib_ext)
 
     def _lib_sync(self):
-        if not self.same_stream and self.device.type == "cuda":
+        """After a collective, before the library reads what it received."""
+        if self.same_stream or self.device.type != "cuda":
+            return
+        if self.lib_ext is not None:
+            self.lib_ext.wait_stream(torch.cuda.current_stream(self.device))
+        else:
             torch.cuda.current_stream(self.device).synchronize()  # the library reads on its own stream
 
     def counts(self, counts, found: bool, staged: int, frontier: int = 0):
@@ -199,6 +217,7 @@ class _Exchange:
 
     def payload(self, send: torch.Tensor, in_bytes, out_bytes) -> torch.Tensor:
         total = int(sum(out_bytes))
+        self._pre()
         if self.on_gpu:
             recv = torch.empty(max(total, 1), dtype=torch.uint8, device=self.device)
             dist.all_to_all_single(recv[:total] if total else recv[:0], send, out_bytes, in_bytes, group=self.group)
@@ -210,17 +229,24 @@ class _Exchange:
         self._lib_sync()
         return recv
 
-    def payload_fixed(self, send: torch.Tensor) -> torch.Tensor:
-        """Equal-split all-to-all of `world` fixed-capacity blocks: no sizes
-        on the host. On CUDA tensors (RCCL) it is queued behind the library's
-        kernels on the same stream with no host synchronization."""
+    def payload_blocks(self, send: Optional[torch.Tensor], blk: int) -> Optional[torch.Tensor]:
+        """All-to-all of one fixed-capacity block of `blk` bytes to every OTHER
+        rank: `send` holds the world - 1 blocks in rank order without this
+        rank's (its own share never travels), and so does the result, by
+        sender. The split sizes are fixed, so no size goes to the host; on
+        CUDA tensors (RCCL) the collective is queued behind the library's
+        kernels with no host synchronization. One rank: nothing to send."""
+        if self.world == 1:
+            return None
+        splits = [0 if r == self.rank else blk for r in range(self.world)]
+        self._pre()
         if self.on_gpu:
             recv = torch.empty_like(send)
-            dist.all_to_all_single(recv, send, group=self.group)
+            dist.all_to_all_single(recv, send, splits, splits, group=self.group)
             self._lib_sync()
             return recv
         recv_h = torch.empty(send.numel(), dtype=torch.uint8)
-        dist.all_to_all_single(recv_h, send.cpu(), group=self.group)
+        dist.all_to_all_single(recv_h, send.cpu(), splits, splits, group=self.group)
         recv = recv_h.to(self.device)
         self._lib_sync()
         return recv
@@ -232,6 +258,7 @@ class _Exchange:
 
     def gather_frontier(self, mine: torch.Tensor, n_bytes: List[int]) -> torch.Tensor:
         """All-gather of variable-size byte buffers (every rank's frontier)."""
+        self._pre()
         m = max(n_bytes)
         src = torch.zeros(max(m, 1), dtype=torch.uint8, device=self.tdev)
         if n_bytes[dist.get_rank(self.group)]:
@@ -331,7 +358,8 @@ def _partitioned_rounds(ds: "DistSearch", ex: "_Exchange", device, cb: int, worl
     when the global frontier narrows below wide / 4."""
     from collections import deque
     info = ds.info()
-    limit = max(1, int(info.frontier_cap) // world)
+    nb = world - 1  # exchange blocks: one per other rank
+    limit = max(1, int(info.frontier_cap) // (2 * max(1, nb)))
     round0 = info.round
     ph = _XPhase(cap=min(cap, limit))
     ds.x_begin()
@@ -345,15 +373,15 @@ def _partitioned_rounds(ds: "DistSearch", ex: "_Exchange", device, cb: int, worl
     while True:
         if tm:
             t0 = time.perf_counter()
-        send = torch.empty(world * (ph.cap + 1) * cb, dtype=torch.uint8, device=device)
-        if _XDEBUG:
+        send = torch.empty(nb * (ph.cap + 1) * cb, dtype=torch.uint8, device=device) if nb else None
+        if _XDEBUG and send is not None:
             print(f"[x] rank {ds.rank} queue cap {ph.cap} send {send.data_ptr():#x}+{send.numel()}", flush=True)
         if tm:
             t1 = time.perf_counter()
         ds.x_send(send, ph.cap)
         if tm:
             t2 = time.perf_counter()
-        recv = ex.payload_fixed(send)
+        recv = ex.payload_blocks(send, (ph.cap + 1) * cb)
         if tm:
             t3 = time.perf_counter()
         r = ds.x_recv(recv, ph.cap)
@@ -361,11 +389,11 @@ def _partitioned_rounds(ds: "DistSearch", ex: "_Exchange", device, cb: int, worl
             t4 = time.perf_counter()
             for i, (a, b) in enumerate(((t0, t1), (t1, t2), (t2, t3), (t3, t4))):
                 tm[i] += b - a
-        if _XDEBUG:
+        if _XDEBUG and recv is not None:
             print(f"[x] rank {ds.rank} queued round {r} recv {recv.data_ptr():#x}+{recv.numel()}", flush=True)
         queued.append(r)
         keep.append(recv)
-        ph.sent_bytes += (world - 1) * (ph.cap + 1) * cb
+        ph.sent_bytes += nb * (ph.cap + 1) * cb
         if len(queued) <= _XDEPTH:
             continue
         r0 = queued.popleft()

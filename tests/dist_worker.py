@@ -29,23 +29,29 @@ def exchange_worker(rank, world, port, q):
         assert front == sum(100 + r for r in range(world))
         tr = np.array([[0xFFFFFFFF, 0xFFFFFFFF], [(rank << 29) | 0, rank + 1]], dtype=np.uint32)
         traces = ex.gather_traces(tr)
-        # fixed-capacity blocks (equal split, no sizes): block w of rank r's
-        # send buffer holds bytes (r, w, 0, 1, ...); block s of what rank r
-        # receives is what rank s sent to r
+        # fixed-capacity blocks to the other ranks (no sizes, no own block):
+        # the block for rank w of rank r's send buffer holds bytes (r, w, 0, 1,
+        # ...); the block from rank s of what rank r receives is what s sent to r
         blk = 24
-        send = torch.zeros(world * blk, dtype=torch.uint8)
-        for w in range(world):
-            send[w * blk:(w + 1) * blk] = torch.tensor([rank, w] + list(range(blk - 2)), dtype=torch.uint8)
-        got = ex.payload_fixed(send)
-        blocks = [got[s_ * blk:(s_ + 1) * blk].tolist()[:2] for s_ in range(world)]
+        others = [w for w in range(world) if w != rank]
+        send = torch.zeros(len(others) * blk, dtype=torch.uint8)
+        for b, w in enumerate(others):
+            send[b * blk:(b + 1) * blk] = torch.tensor([rank, w] + list(range(blk - 2)), dtype=torch.uint8)
+        got = ex.payload_blocks(send, blk)
+        blocks = [got[b * blk:(b + 1) * blk].tolist()[:2] for b in range(len(others))]
         q.put((rank, recv, found_any, staged, [t.tolist() for t in traces], blocks))
         dist.destroy_process_group()
     except Exception:
         q.put((rank, "error", traceback.format_exc()))
 
 
-def search_worker(rank, world, port, backend, names, wide, persistent, self_exchange, q, sized=False, xcap0=None):
-    """GPU: every rank checks the named histories with check_distributed."""
+def search_worker(rank, world, port, backend, names, wide, persistent, self_exchange, q, sized=False, xcap0=None,
+                  stream_mode=None):
+    """GPU: every rank checks the named histories with check_distributed.
+    stream_mode: "bound" (the library on torch's current stream: nccl's
+    default), "own" (the library's own stream: gloo's default) or "side" (a
+    caller stream that is NOT torch's current one: the collectives and the
+    library's kernels are ordered by stream waits)."""
     try:
         import torch
         import s2_verification_amd as s2
@@ -54,8 +60,10 @@ def search_worker(rank, world, port, backend, names, wide, persistent, self_exch
         torch.cuda.set_device(0 if backend == "gloo" else rank)
         dist = _init(rank, world, port, backend)
         # nccl: the library on torch's stream (no host syncs around the collectives)
-        checker = s2.Checker(device=torch.cuda.current_device(),
-                             stream=bind_stream() if backend == "nccl" else 0)
+        mode = stream_mode or ("bound" if backend == "nccl" else "own")
+        side = torch.cuda.Stream() if mode == "side" else None
+        stream = bind_stream() if mode == "bound" else side.cuda_stream if side is not None else 0
+        checker = s2.Checker(device=torch.cuda.current_device(), stream=stream)
         out = []
         for name in names:
             h = W.config_history(name)

@@ -35,7 +35,7 @@ def test_exchange_gloo_world2():
     out = _spawn(dist_worker.exchange_worker, [(r, 2, port) for r in range(2)], timeout=120)
     for rank, recv, found_any, staged, traces, blocks in out:
         assert recv == [10 * s + rank for s in range(2)]  # what each source sent to me
-        assert blocks == [[s, rank] for s in range(2)]  # fixed-capacity blocks: block s came from rank s
+        assert blocks == [[s, rank] for s in range(2) if s != rank]  # fixed-capacity blocks: one from each other rank
         assert found_any is True
         assert staged == sum(10 * s + w for s in range(2) for w in range(2))
         assert traces == [[[0xFFFFFFFF, 0xFFFFFFFF], [(s << 29), s + 1]] for s in range(2)]
@@ -118,8 +118,9 @@ def test_distributed_wide_history(world, wide, backend):
 def test_partitioned_exchange_modes(world, wide, backend, sized, xcap0):
     """Partitioned rounds the round-3 way (sized: host-read counts and a
     variable-split all-to-all) and host-free with exchange blocks of capacity
-    1 at every switch (every first partitioned round overflows its blocks on
-    all ranks, inserts nothing and is re-run with larger ones): H212 and C5bad
+    1 at every switch (with 2 ranks every first partitioned round overflows
+    its blocks on all ranks, inserts nothing and is re-run with larger ones;
+    one rank sends no block at all, its share stays local): H212 and C5bad
     give the committed verdicts and round counts, and C5wide's unique
     configurations sum to the committed total."""
     import dist_worker
@@ -138,8 +139,33 @@ def test_partitioned_exchange_modes(world, wide, backend, sized, xcap0):
             if verdict == "Ok":
                 assert wvalid and wlen == n_ops, (rank, name, wvalid, wlen)
             assert part > 0, (rank, name)
-            if xcap0 == 1:
+            if xcap0 == 1 and world > 1:
                 assert xreruns >= 1, (rank, name, xreruns)
+            if world == 1 and not sized:  # (the own share never travels: no block to outgrow)
+                assert xreruns == 0, (rank, name, xreruns)
             if sized:
                 assert xreruns == 0
     assert len({tuple(r) for _, res in out for r in res}) == len(names)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("world,wide,backend,selfx", [(1, 256, "nccl", True), (2, 256, "gloo", False)])
+def test_distributed_search_on_a_side_stream(world, wide, backend, selfx):
+    """Checker(stream=X) with X a caller stream that is not torch's
+    current one. The library then skips its host waits, so the collectives
+    must wait for its queued kernels (and its next kernels for the
+    collectives) on the device: verdicts, round counts and certified
+    witnesses as committed."""
+    import dist_worker
+    ref = golden("hard_reduced.json")
+    rc = golden("hard_round_counts.json")
+    names = ["H212", "C5bad"]
+    port = random.randint(20000, 40000)
+    out = _spawn(dist_worker.search_worker, [(r, world, port, backend, names, wide, None, selfx)
+                                             for r in range(world)], extra=(False, None, "side"))
+    for rank, res in out:
+        for name, verdict, rounds, configs, wvalid, wlen, n_ops, xreruns, part in res:
+            assert verdict == ref[name]["verdict"] and rounds == rc[name]["0"]["rounds"], (rank, name, verdict, rounds)
+            assert part > 0, (rank, name)
+            if verdict == "Ok":
+                assert wvalid and wlen == n_ops, (rank, name, wvalid, wlen)
