@@ -38,7 +38,7 @@ namespace {
     }                                                                    \
   } while (0)
 
-enum LvKernel { LK_ROUND = 0, LK_INSERT, LK_BUCKET, LK_SCATTER, LK_KEEP, LK_GATHER, LK_CLOSE, LK_XSEND };
+enum LvKernel { LK_ROUND = 0, LK_INSERT, LK_BUCKET, LK_SCATTER, LK_KEEP, LK_GATHER, LK_CLOSE, LK_XSEND, LK_CLEAR };
 
 size_t lv_cfg_bytes(uint32_t nq) { return 128 + 128 * (size_t)nq; }
 
@@ -55,6 +55,7 @@ hipError_t lv_launch(int which, uint32_t grid, const LvParams& p, hipStream_t st
     case LK_KEEP: hipLaunchKernelGGL(lv_keep<NQ>, dim3(grid), dim3(LV_BLOCK), 0, st, p, (uint32_t)(p.tgid >> 29)); break;
     case LK_GATHER: hipLaunchKernelGGL(lv_gather_frontier<NQ>, dim3(grid), dim3(LV_BLOCK), 0, st, p); break;
     case LK_XSEND: hipLaunchKernelGGL(lv_xsend<NQ>, dim3(grid), dim3(LV_BLOCK), 0, st, p); break;
+    case LK_CLEAR: hipLaunchKernelGGL(lv_clear_slots<NQ>, dim3(grid), dim3(LV_BLOCK), 0, st, p); break;
     default: hipLaunchKernelGGL(lv_close_kernel, dim3(1), dim3(1), 0, st, p); break;
   }
   return hipGetLastError();
@@ -674,6 +675,23 @@ static LvParams dist_params(DistLevel& d) {
   return p;
 }
 
+// Phase switches of the distributed search (replicated <-> partitioned) clean
+// the two tables by clearing the current frontier's slots (lv_clear_slots),
+// not by resetting them: every round inserts its winners and clears its
+// parents' slots, so at a switch the frontier's entries are all the tables
+// hold (a reset of both tables cost ~90 us each at their full size, six per
+// switch; C5wide switches 11 times)
+static int dist_clear_frontier_slots(DistLevel& d, std::string& err) {
+  if (!d.nf) return 0;
+  LevelBufs& L = d.b.lv;
+  LvParams p = dist_params(d);
+  p.f1 = d.nf;
+  p.ht = L.ht[0];
+  p.ht_clear = L.ht[1];
+  LVCHK(lv_dispatch(d.nq, LK_CLEAR, (uint32_t)std::min<uint64_t>(1024, (d.nf + LV_BLOCK - 1) / LV_BLOCK), p, d.stream));
+  return 0;
+}
+
 // expand + close this rank's frontier (round 0: the initial configuration, on
 // rank 0 only) into local staging; host-driven, control block 0
 static int dist_stage(DistLevel& d, LvParams& p, std::string& err) {
@@ -1072,7 +1090,9 @@ int dist_local_run(DistLevel& d, uint32_t wide, uint64_t* n_next, int* found, ui
     hipLaunchKernelGGL(lv_iota, dim3((uint32_t)std::min<uint64_t>(1024, (d.nf + 255) / 256)), dim3(256), 0, st, L.idx[x], d.nf);
     LVCHK(hipGetLastError());
   }
-  for (int i = 0; i < 2; ++i) LVCHK(hipMemsetAsync(L.ht[i], 0xFF, ht_bytes, st));
+  // clean tables for the persistent rounds (the frontier's entries are all
+  // they hold; its configurations are still in place in d.cur)
+  if (dist_clear_frontier_slots(d, err)) return S2LC_EHIP;
   LvRun* hr = reinterpret_cast<LvRun*>(L.h_run);
   LvRun* d_pub = nullptr;
   LVCHK(hipHostGetDevicePointer((void**)&d_pub, hr, 0));
@@ -1116,7 +1136,11 @@ int dist_local_run(DistLevel& d, uint32_t wide, uint64_t* n_next, int* found, ui
     if (hr->done != LVR_RUNNING || hr->nf >= wide) break;
   }
   LVCHK(hipEventRecord(L.ev[1], st));
-  for (int i = 0; i < 2; ++i) LVCHK(hipMemsetAsync(L.ht[i], 0xFF, ht_bytes, st));  // the dist rounds insert into ht[0]
+  // (the last round's winners stay in its table, every other slot is clear:
+  // the next switch clears the frontier's slots. An aborted launch left
+  // entries anywhere: reset both tables for the host-driven rounds)
+  if (aborted)
+    for (int i = 0; i < 2; ++i) LVCHK(hipMemsetAsync(L.ht[i], 0xFF, ht_bytes, st));
   LVCHK(hipStreamSynchronize(st));
   float ms = 0;
   LVCHK(hipEventElapsedTime(&ms, L.ev[0], L.ev[1]));
@@ -1170,9 +1194,10 @@ int dist_keep_owned(DistLevel& d, uint64_t* n_kept, std::string& err) {
   p.nxt_idx = L.idx[d.cur_sel ^ 1];
   memset(hc, 0, sizeof(LvCtl));
   LVCHK(hipMemcpyAsync(L.ctl, hc, sizeof(LvCtl), hipMemcpyHostToDevice, st));
+  // the tables hold the whole replicated frontier's entries (the dropped
+  // configurations' too): clear them before the partitioned rounds
+  if (dist_clear_frontier_slots(d, err)) return S2LC_EHIP;
   if (d.nf) LVCHK(lv_dispatch(d.nq, LK_KEEP, (uint32_t)std::min<uint64_t>(2048, (d.nf + LV_BLOCK - 1) / LV_BLOCK), p, st));
-  // the table still holds the dropped configurations' slots: reset it
-  LVCHK(hipMemsetAsync(L.ht[0], 0xFF, ((size_t)L.ht_mask + 1) * 8, st));
   LVCHK(hipMemcpyAsync(hc, L.ctl, sizeof(LvCtl), hipMemcpyDeviceToHost, st));
   LVCHK(hipStreamSynchronize(st));
   d.cur_sel ^= 1;
@@ -1204,7 +1229,9 @@ int dist_frontier_load(DistLevel& d, uint8_t* buf, uint64_t n, std::string& err)
   const int sel = d.cur_sel ^ 1;
   if (n) hipLaunchKernelGGL(lv_iota, dim3((uint32_t)std::min<uint64_t>(1024, (n + 255) / 256)), dim3(256), 0, st, L.idx[sel], (uint32_t)n);
   LVCHK(hipGetLastError());
-  LVCHK(hipMemsetAsync(L.ht[0], 0xFF, ((size_t)L.ht_mask + 1) * 8, st));
+  // (ht[0] holds this rank's share of the gathered frontier, which is in the
+  // new frontier with its slots: the next round's expansion, or the next
+  // switch, clears them; ht[1] is clear)
   LVCHK(hipStreamSynchronize(st));
   d.cur = buf;
   d.cur_loc = nullptr;

@@ -1818,6 +1818,24 @@ __global__ __launch_bounds__(LV_BLOCK) void lv_gather_frontier(LvParams p) {
   }
 }
 
+// clear the table slots of the frontier's configurations in both tables (a
+// phase switch of the distributed search: the tables then hold no entry at
+// all, since at a switch their only entries are the current frontier's,
+// each at its configuration's slot; a slot another rank's configuration
+// names is empty here or this rank's frontier entry, cleared either way)
+template <int NQ>
+__global__ __launch_bounds__(LV_BLOCK) void lv_clear_slots(LvParams p) {
+  const uint32_t nf = p.f1;
+  for (uint32_t i = blockIdx.x * LV_BLOCK + threadIdx.x; i < nf; i += gridDim.x * LV_BLOCK) {
+    const uint32_t k = p.cur_idx[i];
+    const uint32_t s = lv_cfg<NQ>((k & LV_LOCAL) ? p.cur_loc : p.cur, k & ~LV_LOCAL)->slot;
+    if (s <= p.ht_mask) {
+      p.ht[s] = HT_EMPTY;
+      p.ht_clear[s] = HT_EMPTY;
+    }
+  }
+}
+
 __global__ __attribute__((unused)) void lv_iota(uint32_t* out, uint32_t n) {
   for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) out[i] = i;
 }

@@ -251,13 +251,19 @@ class _Exchange:
         self._lib_sync()
         return recv
 
+    # (one rank: every collective below is the identity, taken on the host
+    # without a device round trip)
     def sum(self, v: int) -> int:
+        if self.world == 1:
+            return int(v)
         t = torch.tensor([v], dtype=torch.int64, device=self.tdev)
         dist.all_reduce(t, group=self.group)
         return int(t.item())
 
     def gather_frontier(self, mine: torch.Tensor, n_bytes: List[int]) -> torch.Tensor:
         """All-gather of variable-size byte buffers (every rank's frontier)."""
+        if self.world == 1:
+            return mine  # (frontier_pack waited for the library's copy)
         self._pre()
         m = max(n_bytes)
         src = torch.zeros(max(m, 1), dtype=torch.uint8, device=self.tdev)
@@ -271,12 +277,16 @@ class _Exchange:
         return full
 
     def gather_small(self, vals: List[int]) -> List[List[int]]:
+        if self.world == 1:
+            return [[int(v) for v in vals]]
         t = torch.tensor(vals, dtype=torch.int64, device=self.tdev)
         out = [torch.empty_like(t) for _ in range(self.world)]
         dist.all_gather(out, t, group=self.group)
         return [o.cpu().tolist() for o in out]
 
     def gather_traces(self, tr: np.ndarray) -> List[np.ndarray]:
+        if self.world == 1:
+            return [tr.astype(np.uint32)]
         n = self.gather_small([len(tr)])
         m = max(x[0] for x in n)
         buf = torch.zeros((max(m, 1), 2), dtype=torch.int64, device=self.tdev)

@@ -69,3 +69,9 @@ def test_bench_two_gloo_ranks_on_one_gpu():
     assert c5["replicated_only"]["verdict"] == c5["verdict"]
     w = c5["c5wide"]
     assert w["verdict"] == hard["C5wide"]["verdict"] and w["witness_replayed"], w
+    # the N-GPU legs carry the single-GPU engine's time and the
+    # speed-up against it (not against the replicated-only distributed path)
+    for leg, name in ((c5, "C5"), (w, "C5wide")):
+        assert leg["single_gpu_verdict"] == hard[name]["verdict"], (name, leg)
+        assert leg["single_gpu_seconds"] > 0 and leg["speedup"] > 0, (name, leg)
+        assert abs(leg["speedup"] - leg["single_gpu_seconds"] / leg["seconds"]) < 0.01 * leg["speedup"] + 1e-3
