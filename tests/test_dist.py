@@ -114,7 +114,7 @@ def test_distributed_wide_history(world, wide, backend):
 @pytest.mark.gpu
 @pytest.mark.parametrize("world,wide,backend,sized,xcap0", [
     (2, 256, "gloo", True, None), (1, 0, "nccl", True, None),
-    (2, 256, "gloo", False, 1), (1, 256, "nccl", False, 1)])
+    (2, 256, "gloo", False, 1), (1, 256, "nccl", False, 1), (2, 256, "nccl", False, 1)])
 def test_partitioned_exchange_modes(world, wide, backend, sized, xcap0):
     """Partitioned rounds the round-3 way (sized: host-read counts and a
     variable-split all-to-all) and host-free with exchange blocks of capacity
@@ -124,6 +124,11 @@ def test_partitioned_exchange_modes(world, wide, backend, sized, xcap0):
     give the committed verdicts and round counts, and C5wide's unique
     configurations sum to the committed total."""
     import dist_worker
+    import torch
+    if backend == "nccl" and world > torch.cuda.device_count():
+        # (ADVICE r4: the host-free rounds over RCCL with two ranks, one GPU
+        # each, forced re-runs included; runs where the box has the GPUs)
+        pytest.skip(f"{world} ranks over RCCL need {world} GPUs")
     ref = golden("hard_reduced.json")
     rc = golden("hard_round_counts.json")
     names = ["H212", "C5bad", "C5wide"]
