@@ -898,7 +898,8 @@ int dist_x_send(DistLevel& d, uint8_t* send, uint32_t cap, std::string& err) {
   p.ctl_next = reinterpret_cast<LvCtl*>(d.b.lv.ctl) + ((d.xround + 1) & 1);
   LVCHK(lv_dispatch(d.nq, LK_ROUND, g_round, p, st));
   p.ctl_next = nullptr;
-  LVCHK(lv_dispatch(d.nq, LK_XSEND, g_send, p, st));
+  // (one rank sends nothing: lv_insert takes its header from the counters)
+  if (d.world > 1) LVCHK(lv_dispatch(d.nq, LK_XSEND, g_send, p, st));
   // on a stream of its own the caller's collective is not ordered after these
   // kernels on the device: the host waits (the gloo tests; one process per
   // GPU passes its stream and queues with no wait)
@@ -935,8 +936,12 @@ int dist_x_recv(DistLevel& d, uint8_t* recv, uint32_t cap, uint32_t* round, std:
   uint32_t hint_nf;
   uint64_t hint_staged;
   dist_x_hint(d, hint_nf, hint_staged);
-  const uint32_t max_grid = (uint32_t)n_cus(err) * 8;
-  const uint64_t want = slots + std::min<uint64_t>(hint_staged, (uint64_t)max_grid * LV_BLOCK);
+  // grid: from the latest visible status; with none visible (rounds queued
+  // ahead) two blocks per CU: the close is the last block's, and its
+  // done-counter atomics grow with the grid (~11 ns each: 2,048 blocks cost a
+  // narrow round ~40 us)
+  const uint32_t ncu = (uint32_t)n_cus(err), max_grid = ncu * 8;
+  const uint64_t want = slots + (hint_staged == UINT64_MAX ? (uint64_t)2 * ncu * LV_BLOCK : hint_staged);
   LVCHK(lv_dispatch(d.nq, LK_INSERT, (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>(max_grid, (want + LV_BLOCK - 1) / LV_BLOCK)), p, st));
   LVCHK(hipEventRecord(d.xev[r], st));
   if (g_xsync) LVCHK(hipStreamSynchronize(st));

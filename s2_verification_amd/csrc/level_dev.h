@@ -1727,8 +1727,19 @@ __device__ __forceinline__ LvXDecision lv_xdecide(const LvParams& p) {
   LvXDecision d;
   d.halt = 0; d.maxblk = 0; d.fpar = TRACE_NONE; d.fmov = LV_NONE; d.fp4 = 0; d.nf_global = 0; d.staged = 0;
   bool found = false, sovf = false;
+  LvXHdr own;  // one rank: its header from its counters (no lv_xsend ran; nothing was sent)
+  if (p.world == 1) {
+    own.count = 0; own.maxblk = 0;
+    own.found = ld_agent(&p.ctl->found);
+    own.fpar = ld_agent(&p.ctl->found_parent); own.fmov = ld_agent(&p.ctl->found_move);
+    own.fp4 = ld_agent(&p.ctl->found_p4);
+    own.sovf = ld_agent(&p.ctl->overflow);
+    own.nf = p.run->nf;
+    own.staged = ld_agent(&p.ctl->staged);
+  }
   for (uint32_t s = 0; s < p.world; ++s) {  // (in rank order: every rank takes the same found child)
-    const LvXHdr* h = s == p.rank ? p.xself : lv_xhdr<NQ>(const_cast<uint8_t*>(p.stg), lv_xblk(s, p.rank), p.xcap);
+    const LvXHdr* h = s != p.rank ? lv_xhdr<NQ>(const_cast<uint8_t*>(p.stg), lv_xblk(s, p.rank), p.xcap)
+                      : p.world == 1 ? &own : p.xself;
     d.maxblk = max(d.maxblk, h->maxblk);
     d.nf_global += h->nf;
     d.staged += h->staged;
