@@ -456,8 +456,30 @@ def _partitioned_rounds(ds: "DistSearch", ex: "_Exchange", device, cb: int, worl
     return ph
 
 
+# Cost model of a partitioned round ("N-GPU model"; constants
+# measured on one MI355X, profiles/r05/dist/): a round of a frontier of nf
+# configurations costs the single-GPU engine ~X_FIX + X_PER * nf us; split
+# over N ranks it costs X_OVER (the partitioned round's own overhead on one
+# GPU) + X_RCCL (the all-to-all's latency over xGMI: a parameter, not
+# measurable on one GPU) + that work / N. Partitioning pays from the frontier
+# where the saving (1 - 1/N) of the work exceeds the overhead.
+X_FIX, X_PER, X_OVER, X_RCCL = 10.0, 0.0082, 22.0, 30.0
+
+
+def default_wide(world: int) -> int:
+    """The frontier width from which rounds run partitioned on `world` ranks
+    (a power of two, 4,096 .. 65,536; one rank: 4,096, the rehearsal's)."""
+    if world <= 1:
+        return 4096
+    nf = ((X_OVER + X_RCCL) / (1.0 - 1.0 / world) - X_FIX) / X_PER
+    w = 4096
+    while w < nf and w < 65536:
+        w *= 2
+    return w
+
+
 def check_distributed(checker, history: History, group=None, witness: bool = True,
-                      wide: int = 4096, persistent: Optional[bool] = None,
+                      wide: Optional[int] = None, persistent: Optional[bool] = None,
                       self_exchange: bool = False, sized_exchange: bool = False,
                       xcap0: Optional[int] = None) -> DistResult:
     """Check one history with every rank of `group` (default: the world).
@@ -468,7 +490,7 @@ def check_distributed(checker, history: History, group=None, witness: bool = Tru
     (s2lc_dist_local_run: solo and persistent rounds, one host sync per
     launch) unless persistent=False (one host-driven round per call). Wider
     rounds run partitioned by owner with one all-to-all per round. wide=0
-    partitions every round.
+    partitions every round; None: default_wide(world), from the cost model.
 
     persistent=None: on with nccl (one process per GPU) and for one rank; off
     for several gloo ranks, which are the tests' ranks sharing one GPU: the
@@ -491,6 +513,8 @@ def check_distributed(checker, history: History, group=None, witness: bool = Tru
     is grown by re-running the rounds that overflow it)."""
     rank = dist.get_rank(group)
     world = dist.get_world_size(group)
+    if wide is None:
+        wide = default_wide(world)
     device = torch.device("cuda", torch.cuda.current_device())
     ex = _Exchange(group, device, getattr(checker, "stream", 0))
     if persistent is None:
