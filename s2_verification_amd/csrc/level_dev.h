@@ -1236,7 +1236,7 @@ __device__ __forceinline__ void lv_xclose(const LvParams& p, const LvXDecision& 
 template <int NQ>
 __global__ __launch_bounds__(LV_BLOCK) void lv_insert(LvParams p) {
   __shared__ uint32_t s_wcnt[LV_BLOCK / 64], s_base, s_hi, s_last;
-  LvXDecision xd;  // (thread 0: the exchanged round's decision, reused by the close)
+  __shared__ LvXDecision xd;  // (thread 0: the exchanged round's decision, reused by the close; in LDS, not a private frame)
   if (p.xcap) {
     // exchanged round: every block takes the round's decision from the
     // received headers; a halting round inserts nothing (block 0 records it).
@@ -1727,24 +1727,23 @@ __device__ __forceinline__ LvXDecision lv_xdecide(const LvParams& p) {
   LvXDecision d;
   d.halt = 0; d.maxblk = 0; d.fpar = TRACE_NONE; d.fmov = LV_NONE; d.fp4 = 0; d.nf_global = 0; d.staged = 0;
   bool found = false, sovf = false;
-  LvXHdr own;  // one rank: its header from its counters (no lv_xsend ran; nothing was sent)
-  if (p.world == 1) {
-    own.count = 0; own.maxblk = 0;
-    own.found = ld_agent(&p.ctl->found);
-    own.fpar = ld_agent(&p.ctl->found_parent); own.fmov = ld_agent(&p.ctl->found_move);
-    own.fp4 = ld_agent(&p.ctl->found_p4);
-    own.sovf = ld_agent(&p.ctl->overflow);
-    own.nf = p.run->nf;
-    own.staged = ld_agent(&p.ctl->staged);
-  }
   for (uint32_t s = 0; s < p.world; ++s) {  // (in rank order: every rank takes the same found child)
-    const LvXHdr* h = s != p.rank ? lv_xhdr<NQ>(const_cast<uint8_t*>(p.stg), lv_xblk(s, p.rank), p.xcap)
-                      : p.world == 1 ? &own : p.xself;
-    d.maxblk = max(d.maxblk, h->maxblk);
-    d.nf_global += h->nf;
-    d.staged += h->staged;
-    sovf |= h->sovf != 0;
-    if (h->found && !found) { found = true; d.fpar = h->fpar; d.fmov = h->fmov; d.fp4 = h->fp4; }
+    uint32_t mb, nf, sv, fnd, fpar, fmov, fp4;
+    unsigned long long stg;
+    if (p.world == 1) {  // one rank: its header from its counters (no lv_xsend ran; nothing was sent)
+      mb = 0; nf = p.run->nf; stg = ld_agent(&p.ctl->staged); sv = ld_agent(&p.ctl->overflow);
+      fnd = ld_agent(&p.ctl->found); fpar = ld_agent(&p.ctl->found_parent); fmov = ld_agent(&p.ctl->found_move);
+      fp4 = ld_agent(&p.ctl->found_p4);
+    } else {
+      const LvXHdr* h = s != p.rank ? lv_xhdr<NQ>(const_cast<uint8_t*>(p.stg), lv_xblk(s, p.rank), p.xcap) : p.xself;
+      mb = h->maxblk; nf = h->nf; stg = h->staged; sv = h->sovf;
+      fnd = h->found; fpar = h->fpar; fmov = h->fmov; fp4 = h->fp4;
+    }
+    d.maxblk = max(d.maxblk, mb);
+    d.nf_global += nf;
+    d.staged += stg;
+    sovf |= sv != 0;
+    if (fnd && !found) { found = true; d.fpar = fpar; d.fmov = fmov; d.fp4 = fp4; }
   }
   d.halt = found ? LVR_FOUND : sovf ? LVR_ABORT : d.maxblk > p.xcap ? LVR_OVERFLOW : d.staged == 0 ? LVR_EMPTY : 0u;
   return d;
