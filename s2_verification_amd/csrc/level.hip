@@ -134,10 +134,13 @@ int lv_grids_t(LevelBufs& L, std::string& err) {
   LVCHK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&bp, lv_persist<NQ>, LV_BLOCK, 0));
   L.grid_round = (uint32_t)(std::max(1, br) * n_cu);
   L.grid_insert = (uint32_t)(std::max(1, bi) * n_cu);
-  // lv_persist's grid barrier needs every block resident: one per CU, and
-  // only where the occupancy answer leaves a margin of one (MI355X guide:
-  // the API can over-report by one block per CU)
-  L.grid_persist = bp >= 2 ? (uint32_t)n_cu : 0u;
+  // lv_persist's grid barrier needs every block resident: one per CU (its
+  // launch bound: one workgroup per CU, the whole register file). A
+  // cooperative launch is refused when its grid cannot be co-resident; a
+  // plain launch whose workgroup never becomes resident (another process
+  // holding the CUs) times out at the barrier: either way the search goes on
+  // host-driven (LVR_ABORT / persist_refused)
+  L.grid_persist = bp >= 1 ? (uint32_t)n_cu : 0u;
   // (S2LC_PERSIST_GRID: fewer persistent workgroups; diagnostics: with 1,
   // the SQ counters of lv_persist are those of the solo rounds' workgroup)
   if (const char* e = getenv("S2LC_PERSIST_GRID"))

@@ -736,6 +736,9 @@ __device__ __forceinline__ uint64_t ld_suf(const OpRec* r) {
 // ---- expansion: one wave per (frontier configuration, slice of its candidates)
 // MODE 0: stage into the striped staging array (lv_insert deduplicates);
 // MODE 1: the persistent kernel's stage-and-insert.
+#ifndef S2LC_FUSED_PRE_NQ
+#define S2LC_FUSED_PRE_NQ 6  // the widest layout whose persistent rounds precheck every move at once
+#endif
 // (A frontier of one configuration runs as solo rounds: solo_dev.h.)
 template <int NQ, int MODE>
 __device__ __forceinline__ bool lv_expand(const LvParams& p, const LvRoundIn& in, LvHeadsLds<NQ>& PL,
@@ -855,7 +858,7 @@ __device__ __forceinline__ bool lv_expand(const LvParams& p, const LvRoundIn& in
     // outcome and hash fold, for those moves in parallel, so a move in the
     // loop below costs only its next head's load. Registers: 5 per slot
     // (NQ <= 6).
-    constexpr bool PRE = NQ <= 6;
+    constexpr bool PRE = FUSED ? NQ <= S2LC_FUSED_PRE_NQ : NQ <= 6;
     constexpr int NP = PRE ? NQ : 1;
     uint64_t mv_tail[NP], mv_hash[NP];
     uint32_t mv_pk[NP];  // take_opt | take_id << 1 | P1-dead opt child << 2 | token << 16
@@ -1445,7 +1448,11 @@ __device__ __forceinline__ bool lv_grid_sync(LvBar* B, uint32_t e, unsigned long
 #include "solo_dev.h"
 
 template <int NQ>
-__global__ __launch_bounds__(LV_BLOCK, 2) void lv_persist(LvParams p, LvPersist q) {
+// (one workgroup per CU: the launch is one per CU anyway, and the whole
+// 512-register file of a SIMD lane goes to its one wave: the grid rounds'
+// pressure spills to AGPRs, not to scratch; round 4's two-per-CU bound left
+// lv_persist<5> ~300 scratch accesses in its grid rounds)
+__global__ __launch_bounds__(LV_BLOCK, 1) void lv_persist(LvParams p, LvPersist q) {
   // solo rounds use s_heads[0] (the configuration's heads), s_heads[1] (the
   // moves' next heads) and s_heads[2..3] as the move records (LvSoloExt)
   __shared__ __attribute__((aligned(16))) LvHeadsLds<NQ> s_heads[LV_BLOCK / 64];
