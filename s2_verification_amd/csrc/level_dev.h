@@ -564,11 +564,18 @@ struct LvRoundIn {
 // over several waves (down to about one child per wave), wide ones give a wave
 // whole configurations. The expected moves per configuration come from the
 // previous round.
+#ifndef S2LC_SLICE_WAVES
+#define S2LC_SLICE_WAVES 2  // items per wave a round may make (x the waves)
+#endif
+#ifndef S2LC_SLICE_KIDS
+#define S2LC_SLICE_KIDS 1   // expected closed children per item
+#endif
 __device__ __forceinline__ uint32_t lv_slices(uint32_t K, uint32_t nf, uint32_t nwaves, uint32_t last_nf,
                                               unsigned long long last_closed) {
   uint32_t c_est = K;
   if (last_nf) c_est = (uint32_t)min<unsigned long long>(K, last_closed / last_nf + 1);
-  return max(1u, min(c_est + (c_est >> 2) + 1, (2u * nwaves + nf - 1) / max(nf, 1u)));
+  c_est = (c_est + S2LC_SLICE_KIDS - 1) / S2LC_SLICE_KIDS;
+  return max(1u, min(c_est + (c_est >> 2) + 1, (S2LC_SLICE_WAVES * nwaves + nf - 1) / max(nf, 1u)));
 }
 
 // A configuration's counters (lane l holds chains l + 64 q) with 8-byte
@@ -878,12 +885,15 @@ __device__ __forceinline__ bool lv_expand(const LvParams& p, const LvRoundIn& in
 #ifndef S2LC_PRE_GROUP
 #define S2LC_PRE_GROUP 1
 #endif
+#ifndef S2LC_PRE_GROUP_NQ
+#define S2LC_PRE_GROUP_NQ 4
+#endif
     // grid rounds: the rest of every candidate's record and its next record's
     // P1 bound loaded for all slots before the precheck uses any (one latency
     // instead of one per slot with a candidate). NQ <= 4: C5wide (NQ = 4)
     // 0.0394 -> 0.0361 s; at NQ = 5 the 50 more live VGPRs cost C5 0.6 %
     // (profiles/r04/pre_group_ab.txt)
-    constexpr bool PG = NQ <= 4 && S2LC_PRE_GROUP;
+    constexpr bool PG = NQ <= S2LC_PRE_GROUP_NQ && S2LC_PRE_GROUP;
     uint4 pm0[PG ? NP : 1], pm3[PG ? NP : 1];
     uint64_t pns[PG ? NP : 1];
     if (PG) {
