@@ -133,6 +133,27 @@ __device__ __forceinline__ uint64_t bcast_u64(uint64_t v, int src) {
 #define S2LC_PACK_W 2
 #endif
 constexpr int PACK_W = S2LC_PACK_W;
+// Read-ahead: a window refill at count c also loads one dword of records
+// c+PD .. c+PD+PN-1 (the lines of the chain's next window), so that the next
+// refill finds them in L2 instead of HBM. The dwords are consumed (folded into
+// sink) only at the refill after, by when they have long arrived, and sink is
+// consumed by an empty asm at the history's end. C4 10k launch
+// (tools/pack_ab.sh, profiles/r05/pack_readahead.txt): 1.363 -> 1.287 ms at
+// PD = 2, PN = 2; PN = 4 / 8 and PD = 3 / 4 are no better, and touching the
+// next record's hashes as well (PH = 1) is slower (1.455 ms): vmcnt retires
+// in order, so a later load that misses to HBM delays every wait behind it.
+#ifndef S2LC_PACK_PD
+#define S2LC_PACK_PD 2
+#endif
+constexpr int PACK_PD = S2LC_PACK_PD;  // read-ahead distance (records); 0 = off
+#ifndef S2LC_PACK_PN
+#define S2LC_PACK_PN 2
+#endif
+constexpr int PACK_PN = S2LC_PACK_PN;  // read-ahead records per refill
+#ifndef S2LC_PACK_PH
+#define S2LC_PACK_PH 0
+#endif
+constexpr int PACK_PH = S2LC_PACK_PH;  // 1: a refill also touches the window's second record's hashes
 struct ChainLane {
   const OpRec* __restrict__ base;  // first record of chain l (valid iff on)
   bool on;                         // l < K
@@ -141,6 +162,10 @@ struct ChainLane {
   uint32_t cc;                     // count of r
   uint4 w[PACK_W][4];              // window: records at counts w0 .. w0+PACK_W-1
   OpRec r;                         // record at count cc (null record when !on)
+  uint32_t pfx[PACK_PN];           // read-ahead dwords of the last refill (PACK_PD)
+  uint32_t sink;                   // read-ahead dwords consumed
+  uint32_t phx;                    // PACK_PH read-ahead dword
+  const uint32_t* pool32;          // the hash pool (PACK_PH)
 #ifdef S2LC_PROF
   bool refilled;                   // the last at() reloaded the window
 #endif
@@ -150,6 +175,10 @@ struct ChainLane {
     len = len_;
     w0 = 0xFFFF0000u;
     cc = 0xFFFFFFFFu;
+#pragma unroll
+    for (int i = 0; i < PACK_PN; ++i) pfx[i] = 0;
+    sink = 0;
+    phx = 0;
     r.num_records = 0; r.msn = 0; r.out_tail = 0; r.out_hash = 0;
     r.sufmin = REQ_NONE; r.call_ev = EV_INF; r.ret_ev = EV_INF;
     r.hash_off = 0; r.hash_cnt = 0; r.batch_tok = 0; r.set_tok = 0;
@@ -173,6 +202,17 @@ struct ChainLane {
         const uint4* qi = reinterpret_cast<const uint4*>(q + min((uint32_t)i, last));
 #pragma unroll
         for (int k = 0; k < 4; ++k) w[i][k] = qi[k];
+      }
+      if (PACK_PD > 0) {
+#pragma unroll
+        for (int i = 0; i < PACK_PN; ++i) sink ^= pfx[i];
+#pragma unroll
+        for (int i = 0; i < PACK_PN; ++i)
+          pfx[i] = *reinterpret_cast<const uint32_t*>(q + min((uint32_t)(PACK_PD + i), last));
+      }
+      if (PACK_PH) {
+        sink ^= phx;
+        phx = w[1][3].y ? pool32[2 * w[1][3].x] : 0u;  // hash_cnt, hash_off of record c+1
       }
       w0 = c;
       o = 0;
@@ -307,6 +347,7 @@ __global__ __launch_bounds__(PACK_BLOCK, S2LC_PACK_MINW) void pack_kernel(Params
     const uint32_t ce = on ? p.chain_start[hd.cs_base + gl + 1] : 0u;
     ChainLane ch;
     ch.reset(p.recs + cs, on, ce - cs);
+    ch.pool32 = reinterpret_cast<const uint32_t*>(p.pool);
     bool witness_ok = p.witness != 0;
     // the first record hashes of this lane's head in the next round's first
     // configuration, loaded right after that configuration's closure so the
@@ -514,6 +555,11 @@ __global__ __launch_bounds__(PACK_BLOCK, S2LC_PACK_MINW) void pack_kernel(Params
       if (p.max_configs && configs > p.max_configs) { verdict = V_UNKNOWN; reason = S2LC_R_BUDGET; break; }
       cur = 1 - cur;
       nf = nn;
+    }
+    if (PACK_PD > 0) {  // the read-ahead's last loads
+#pragma unroll
+      for (int i = 0; i < PACK_PN; ++i) ch.sink ^= ch.pfx[i];
+      asm volatile("" ::"v"(ch.sink ^ ch.phx));
     }
 #ifdef S2LC_PROF
     if (gl == 0) {
