@@ -184,10 +184,8 @@ int s2lc_load_jsonl(const char* path, const uint8_t* buf, size_t len, s2lc_histo
     }
     s2lc_history* h = history_acquire();
     std::string e;
-    int rc = load_jsonl(buf, len, h->h, e);
+    const int rc = load_jsonl_finalized(buf, len, h->h, e);
     if (rc) { set_err(err, errlen, e); history_release(h); return rc; }
-    rc = h->h.finalize();
-    if (rc) { set_err(err, errlen, h->h.error); history_release(h); return rc; }
     *out = h;
     return 0;
   } catch (const std::bad_alloc&) {
@@ -222,11 +220,7 @@ int s2lc_load_jsonl_many(const uint8_t* const* bufs, const size_t* lens, size_t 
       if (i >= n) return;
       try {
         s2lc_history* h = pre[i];  // (stays in pre[] until it is out[i] or released: an exception leaks nothing)
-        int rc = load_jsonl(bufs[i], lens[i], h->h, errs[i]);
-        if (!rc) {
-          rc = h->h.finalize();
-          if (rc) errs[i] = h->h.error;
-        }
+        const int rc = load_jsonl_finalized(bufs[i], lens[i], h->h, errs[i]);
         pre[i] = nullptr;
         if (rc) {
           history_release(h);

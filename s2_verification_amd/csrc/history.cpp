@@ -38,21 +38,7 @@ uint32_t History::intern(const std::string& s) {
 }
 
 static uint32_t classify(const Event& in, const Event& out) {
-  uint32_t f = in.input_type & OPF_KIND_MASK;
-  if (out.failure) f |= OPF_FAIL;
-  if (out.definite) f |= OPF_DEF;
-  if (out.has_tail) f |= OPF_HAS_TAIL;
-  if (out.has_hash) f |= OPF_HAS_HASH;
-  if (in.has_msn) f |= OPF_HAS_MSN;
-  if (in.input_type == S2LC_INPUT_APPEND) {
-    if (out.failure && out.definite) f |= OPF_CLS_E;       // main.go:283-285: {s}
-    else if (out.failure) f |= OPF_CLS_I;                  // main.go:286-300: {s} or {opt, s}
-    else f |= OPF_CLS_D | OPF_CONSTRAIN;                   // main.go:301-318: {} or {opt}
-  } else {
-    f |= OPF_CLS_E;                                        // main.go:320-331: {} or {s}
-    if (!out.failure || out.has_hash) f |= OPF_CONSTRAIN;
-  }
-  return f;
+  return op_flags(in.input_type, in.has_msn, out.failure, out.definite, out.has_tail, out.has_hash);
 }
 
 OpRec History::rec_of(uint32_t d) const {

@@ -98,8 +98,35 @@ struct History {
   size_t pooled_bytes = 0;  // used_bytes() when it was parked
 };
 
+// OpRec flags of an op from its call's and return's fields (History::rec_of
+// and the direct JSONL decoder; s2Model.Step's cases, main.go:264-335).
+inline uint32_t op_flags(uint8_t input_type, bool has_msn, bool failure, bool definite, bool has_tail, bool has_hash) {
+  uint32_t f = input_type & OPF_KIND_MASK;
+  if (failure) f |= OPF_FAIL;
+  if (definite) f |= OPF_DEF;
+  if (has_tail) f |= OPF_HAS_TAIL;
+  if (has_hash) f |= OPF_HAS_HASH;
+  if (has_msn) f |= OPF_HAS_MSN;
+  if (input_type == 0) {  // S2LC_INPUT_APPEND
+    if (failure && definite) f |= OPF_CLS_E;  // main.go:283-285: {s}
+    else if (failure) f |= OPF_CLS_I;         // main.go:286-300: {s} or {opt, s}
+    else f |= OPF_CLS_D | OPF_CONSTRAIN;      // main.go:301-318: {} or {opt}
+  } else {
+    f |= OPF_CLS_E;                           // main.go:320-331: {} or {s}
+    if (!failure || has_hash) f |= OPF_CONSTRAIN;
+  }
+  return f;
+}
+
 // JSONL loader (eventsFromReader, main.go:529-563). Returns 0 or S2LC_EDECODE.
 int load_jsonl(const uint8_t* buf, size_t len, History& h, std::string& err);
+// load_jsonl + History::finalize. A history entirely in the collector's form
+// (each record as serde writes it, op ids 0, 1, 2, ... in call order, every op
+// returned once) is decoded straight into the finalized form: records, chains
+// and op tables, with the event list built on first use (as a cache load
+// leaves it). Anything else goes through load_jsonl and finalize, which also
+// own every error message. Returns 0 or the status; the message in err.
+int load_jsonl_finalized(const uint8_t* buf, size_t len, History& h, std::string& err);
 
 // Deterministic simulator (collector workload, history.rs + collect-history.rs).
 struct SimParams;

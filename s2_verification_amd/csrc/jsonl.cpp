@@ -16,6 +16,9 @@
 #include <stdlib.h>
 #include <string.h>
 
+#include <algorithm>
+#include <functional>
+#include <mutex>
 #include <string>
 #include <vector>
 
@@ -580,19 +583,26 @@ struct Fast {
   }
 };
 
-// One record at buf[off..]; returns the bytes consumed (0: not in the
-// collector's form, nothing was changed).
-size_t fast_record(const uint8_t* base, const uint8_t* end, History& h) {
+// One record of the collector's form, decoded (its record hashes appended to
+// h.pool at hash_off); fields a record does not carry stay 0, as in Event.
+struct FastRec {
+  int64_t client_id = 0, op_id = 0;
+  uint64_t num_records = 0, msn = 0, hash_off = 0, hash_cnt = 0, tail = 0, stream_hash = 0;
+  uint32_t set_tok = 0, batch_tok = 0;
+  uint8_t kind = 0, input_type = 0, has_num_records = 0, has_msn = 0;
+  uint8_t failure = 0, definite = 0, has_tail = 0, has_hash = 0;
+};
+
+// One record at base; returns the bytes consumed (0: not in the collector's
+// form; h.pool and h.tokens unchanged).
+size_t fast_parse(const uint8_t* base, const uint8_t* end, History& h, FastRec& e) {
   Fast F{base, end, base};
-  h.events.emplace_back();  // decoded in place; dropped again if the record is not in the collector's form
-  Event& e = h.events.back();
-  size_t pool0 = h.pool.size();
+  const size_t pool0 = h.pool.size();
   bool set_has = false, tok_has = false;
   const char *set_s = nullptr, *tok_s = nullptr;
   size_t set_n = 0, tok_n = 0;
   auto undo = [&]() {
     h.pool.resize(pool0);
-    h.events.pop_back();
     return (size_t)0;
   };
   if (!F.lit("{\"event\":{\"")) return undo();
@@ -619,10 +629,7 @@ size_t fast_record(const uint8_t* base, const uint8_t* end, History& h) {
       if (!F.lit("],\"set_fencing_token\":") || !F.opt_tok(set_has, set_s, set_n)) return undo();
       if (!F.lit(",\"fencing_token\":") || !F.opt_tok(tok_has, tok_s, tok_n)) return undo();
       if (!F.lit(",\"match_seq_num\":")) return undo();
-      if (F.lit("null")) {
-        e.has_msn = 0;
-        e.msn = 0;
-      } else {
+      if (!F.lit("null")) {
         if (!F.u64(e.msn)) return undo();
         e.has_msn = 1;
       }
@@ -635,15 +642,11 @@ size_t fast_record(const uint8_t* base, const uint8_t* end, History& h) {
     e.kind = 1;
     if (F.peek('"')) {
       e.failure = 1;
-      e.has_tail = 0;
-      e.has_hash = 0;
       if (F.lit("\"AppendDefiniteFailure\"")) e.definite = 1;
       else if (F.lit("\"AppendIndefiniteFailure\"")) e.definite = 0;
       else if (F.lit("\"ReadFailure\"") || F.lit("\"CheckTailFailure\"")) e.definite = 1;
       else return undo();
     } else {
-      e.failure = 0;
-      e.definite = 0;
       e.has_tail = 1;
       if (F.lit("{\"AppendSuccess\":{\"tail\":") || F.lit("{\"CheckTailSuccess\":{\"tail\":")) {
         if (!F.u64(e.tail)) return undo();
@@ -666,6 +669,228 @@ size_t fast_record(const uint8_t* base, const uint8_t* end, History& h) {
   if (set_has) e.set_tok = h.intern(std::string(set_s, set_n));
   if (tok_has) e.batch_tok = h.intern(std::string(tok_s, tok_n));
   return (size_t)(F.p - base);
+}
+
+// One record at base appended to h.events; returns the bytes consumed (0: not
+// in the collector's form, nothing was changed).
+size_t fast_record(const uint8_t* base, const uint8_t* end, History& h) {
+  FastRec r;
+  const size_t used = fast_parse(base, end, h, r);
+  if (!used) return 0;
+  Event& e = h.events.emplace_back();
+  e.op_id = r.op_id;
+  e.client_id = r.client_id;
+  e.num_records = r.num_records;
+  e.msn = r.msn;
+  e.hash_off = r.hash_off;
+  e.hash_cnt = r.hash_cnt;
+  e.tail = r.tail;
+  e.stream_hash = r.stream_hash;
+  e.set_tok = r.set_tok;
+  e.batch_tok = r.batch_tok;
+  e.kind = r.kind;
+  e.input_type = r.input_type;
+  e.has_num_records = r.has_num_records;
+  e.has_msn = r.has_msn;
+  e.failure = r.failure;
+  e.definite = r.definite;
+  e.has_tail = r.has_tail;
+  e.has_hash = r.has_hash;
+  return used;
+}
+
+bool json_ws(uint8_t c) { return c == ' ' || c == '\t' || c == '\n' || c == '\r'; }
+
+// The direct decode behind load_jsonl_finalized: the records of the
+// collector's form straight into the finalized History, in one pass over the
+// bytes. Each op's record (OpRec) is filled in op order, its call fields at
+// the Start and its return fields at the Finish, and its chain is chosen at
+// the Start: finalize's greedy colouring takes, for op d in call order, the
+// chain whose last op returned earliest if that return precedes d's call.
+// Every op returned by then precedes the call and every op still open returns
+// after it, so the choice needs only the returns seen so far. The records are
+// then laid out chain-major with their sentinels and P1 suffix bounds, as
+// finalize writes them. Returns false (h left for recycle()) on anything
+// else: a record not in the collector's form, op ids out of order, a second
+// Start or Finish, an op never returned, more than 2^16 - 1 tokens.
+bool load_direct(const uint8_t* buf, size_t len, History& h) {
+  thread_local struct {
+    std::vector<OpRec> orec;  // per dense op (op-major)
+    std::vector<uint32_t> chain_of, chain_len, last, fill;
+    std::vector<std::pair<uint32_t, uint32_t>> heap;  // (last return, chain), many chains
+  } S;
+  constexpr uint32_t OPEN = EV_INF;  // a chain whose last op has not returned
+  std::vector<OpRec>& orec = S.orec;
+  std::vector<uint32_t>&chain_of = S.chain_of, &chain_len = S.chain_len, &last = S.last;
+  auto& heap = S.heap;
+  orec.clear(); chain_of.clear(); chain_len.clear(); last.clear(); heap.clear();
+  orec.reserve(len / 160 + 16);
+  h.pool.reserve(h.pool.size() + len / 24);
+  h.lazy_client.reserve(len / 56 + 16);
+  bool use_heap = false;
+  uint32_t returned = 0;
+  const uint8_t* p = buf;
+  const uint8_t* const end = buf + len;
+  auto gt = std::greater<std::pair<uint32_t, uint32_t>>();
+  for (;;) {
+    while (p < end && json_ws(*p)) ++p;
+    if (p >= end) break;
+    FastRec r;
+    const size_t used = fast_parse(p, end, h, r);
+    if (!used) return false;
+    p += used;
+    const size_t ev = h.lazy_client.size();
+    if (ev >= (size_t)EV_INF - 1) return false;
+    h.lazy_client.push_back(r.client_id);
+    if (r.kind == 0) {
+      if (r.op_id != (int64_t)orec.size()) return false;  // dense id = op id (renumber's first appearance)
+      const uint32_t d = (uint32_t)orec.size();
+      OpRec& o = orec.emplace_back();
+      o.num_records = r.num_records;
+      o.msn = r.msn;
+      o.sufmin = REQ_NONE;
+      o.call_ev = (uint32_t)ev;
+      o.ret_ev = EV_INF;
+      o.hash_off = (uint32_t)r.hash_off;
+      o.hash_cnt = (uint32_t)r.hash_cnt;
+      o.batch_tok = (uint16_t)r.batch_tok;
+      o.set_tok = (uint16_t)r.set_tok;
+      o.flags = r.input_type | (r.has_msn ? OPF_HAS_MSN : 0u);  // (the return's bits at the Finish)
+      if (r.hash_off > 0xFFFFFFFFull || r.batch_tok > 0xFFFF || r.set_tok > 0xFFFF) return false;
+      uint32_t c = EV_INF;
+      if (!use_heap) {
+        uint32_t best = EV_INF;
+        for (uint32_t k = 0; k < (uint32_t)last.size(); ++k)
+          if (last[k] < best) { best = last[k]; c = k; }
+      } else if (!heap.empty()) {
+        std::pop_heap(heap.begin(), heap.end(), gt);
+        c = heap.back().second;
+        heap.pop_back();
+      }
+      if (c == EV_INF) {
+        c = (uint32_t)chain_len.size();
+        chain_len.push_back(0);
+        last.push_back(OPEN);
+      }
+      chain_of.push_back(c);
+      chain_len[c]++;
+      last[c] = OPEN;
+      if (!use_heap && last.size() > 32) {  // many chains: a heap of the returned chain ends (same choices)
+        use_heap = true;
+        for (uint32_t k = 0; k < (uint32_t)last.size(); ++k)
+          if (last[k] != OPEN) heap.emplace_back(last[k], k);
+        std::make_heap(heap.begin(), heap.end(), gt);
+      }
+      (void)d;
+    } else {
+      if (r.op_id < 0 || r.op_id >= (int64_t)orec.size()) return false;
+      const uint32_t d = (uint32_t)r.op_id;
+      OpRec& o = orec[d];
+      if (o.ret_ev != EV_INF) return false;  // a second Finish: the literal search's case
+      o.ret_ev = (uint32_t)ev;
+      o.out_tail = r.tail;
+      o.out_hash = r.stream_hash;
+      o.flags = op_flags((uint8_t)(o.flags & OPF_KIND_MASK), o.flags & OPF_HAS_MSN, r.failure, r.definite, r.has_tail,
+                         r.has_hash);
+      const uint32_t c = chain_of[d];
+      last[c] = (uint32_t)ev;  // (d is its chain's last op: ops join only chains whose last op returned)
+      if (use_heap) {
+        heap.emplace_back((uint32_t)ev, c);
+        std::push_heap(heap.begin(), heap.end(), gt);
+      }
+      returned++;
+    }
+  }
+  const uint32_t m = (uint32_t)orec.size();
+  if (returned != m || h.tokens.size() > 0xFFFF || h.pool.size() > 0xFFFFFFFFull) return false;
+  // finalize's state (history.cpp), from the op-major records
+  h.status = 0;
+  h.error.clear();
+  h.structural = 0;
+  h.literal = false;
+  h.lit_id.clear();
+  h.lit_match.clear();
+  h.n_ops = m;
+  h.op_ids.resize(m);
+  h.op_call.resize(m);
+  h.op_ret.resize(m);
+  uint64_t total = 0;
+  bool nowrap = true;
+  for (uint32_t d = 0; d < m; ++d) {
+    const OpRec& o = orec[d];
+    h.op_ids[d] = d;
+    h.op_call[d] = o.call_ev;
+    h.op_ret[d] = o.ret_ev;
+    if ((o.flags & OPF_KIND_MASK) != S2LC_INPUT_APPEND) continue;
+    if (o.num_records > (1ull << 63) - total) nowrap = false;
+    else total += o.num_records;
+  }
+  // (a zero-record append carrying hashes is not in the collector's form:
+  // hash_cnt == num_records there)
+  h.hflags = H_P4 | H_IDEFER;
+  if (nowrap) h.hflags |= H_NOWRAP | H_P2OK;
+  if (nowrap && total <= 0xFFFFFFFCull) h.hflags |= H_TAIL32;
+  const uint32_t K = (uint32_t)chain_len.size();
+  h.K = K;
+  h.chain_start.resize(K + 1);
+  h.max_chain_len = 0;
+  uint32_t pos = 0;
+  for (uint32_t c = 0; c < K; ++c) {
+    h.chain_start[c] = pos;
+    pos += chain_len[c] + 1;
+    h.max_chain_len = std::max<uint32_t>(h.max_chain_len, chain_len[c]);
+  }
+  h.chain_start[K] = pos;
+  h.rec_op.assign(pos, EV_INF);
+  h.op_rec.resize(m);
+  std::vector<uint32_t>& fill = S.fill;
+  fill.assign(h.chain_start.begin(), h.chain_start.end() - 1);
+  for (uint32_t d = 0; d < m; ++d) {  // call order within every chain
+    const uint32_t q = fill[chain_of[d]]++;
+    h.rec_op[q] = d;
+    h.op_rec[d] = q;
+  }
+  // the records in position order, each written once
+  h.recs.clear();
+  h.recs.reserve(pos);
+  uint32_t n_ident = 0;
+  for (uint32_t q = 0; q < pos; ++q) {
+    const uint32_t d = h.rec_op[q];
+    if (d == EV_INF) {
+      h.recs.push_back(OpRec{});
+      continue;
+    }
+    h.recs.push_back(orec[d]);
+    if (orec[d].flags & OPF_CLS_E) n_ident++;
+  }
+  h.n_ident = n_ident;
+  for (uint32_t c = 0; c < K; ++c) {
+    const uint32_t q = h.chain_start[c + 1] - 1;
+    OpRec& s = h.recs[q];  // sentinel
+    s.call_ev = EV_INF;
+    s.ret_ev = EV_INF;
+    s.flags = OPF_SENTINEL;
+    s.sufmin = REQ_NONE;
+    uint64_t run = REQ_NONE;  // suffix minimum of the pre-tail each constraining op requires
+    for (uint32_t x = q; x-- > h.chain_start[c];) {
+      OpRec& o = h.recs[x];
+      if (o.flags & OPF_CONSTRAIN) {
+        uint64_t req;
+        if ((o.flags & OPF_KIND_MASK) == S2LC_INPUT_APPEND)
+          req = o.out_tail >= o.num_records ? o.out_tail - o.num_records : 0;  // 0: unsatisfiable
+        else if (!(o.flags & OPF_FAIL))
+          req = o.out_tail;
+        else
+          req = REQ_HASH_ONLY;
+        if (req > REQ_HASH_ONLY) req = REQ_HASH_ONLY;
+        run = std::min(run, req);
+      }
+      o.sufmin = run;
+    }
+  }
+  h.events.clear();
+  h.lazy_once = std::make_unique<std::once_flag>();
+  return true;
 }
 
 }  // namespace
@@ -777,6 +1002,19 @@ int load_jsonl(const uint8_t* buf, size_t len, History& h, std::string& err) {
     e.client_id = client;
     h.events.push_back(e);
   }
+}
+
+int load_jsonl_finalized(const uint8_t* buf, size_t len, History& h, std::string& err) {
+  const char* e = getenv("S2LC_JSONL_DIRECT");  // 0: always the event list + finalize (tests compare the two)
+  if (!(e && *e == '0') && getenv("S2LC_JSONL_GENERAL") == nullptr) {
+    if (load_direct(buf, len, h)) return 0;
+    h.recycle();
+  }
+  int rc = load_jsonl(buf, len, h, err);
+  if (rc) return rc;
+  rc = h.finalize();
+  if (rc) err = h.error;
+  return rc;
 }
 
 }  // namespace s2lc

@@ -282,3 +282,54 @@ def test_many_distinct_fencing_tokens(monkeypatch, general):
         assert v.SetFencingToken == "s%d" % i
         assert v.BatchFencingToken == ("s%d" % (i // 2) if i % 3 else None)
     assert h.info()["n_tokens"] == n
+
+
+def _structural_variants(text):
+    """Collector-form blobs the direct decode must hand to load_jsonl + finalize:
+    op ids not 0, 1, 2, ... in call order, a second Finish, an op never
+    returned, a Finish before its Start."""
+    lines = text.splitlines(keepends=True)
+    out = [text.replace('"op_id":', '"op_id":1', 1)]  # first op id 10.. (not dense)
+    fin = [i for i, ln in enumerate(lines) if '"Finish"' in ln]
+    if fin:
+        out.append("".join(lines + [lines[fin[len(fin) // 2]]]))  # a second Finish
+        out.append("".join(lines[:fin[-1]] + lines[fin[-1] + 1:]))  # an op never returned
+        i = fin[0]
+        out.append("".join([lines[i]] + lines[:i] + lines[i + 1:]))  # a Finish before its Start
+    return out
+
+
+def test_direct_decode_leaves_the_finalized_state(monkeypatch):
+    """load_jsonl_finalized decodes a history in the collector's form straight
+    into the finalized records, chains and op tables (events built on first
+    use). It must leave exactly what load_jsonl + History::finalize leave
+    (S2LC_JSONL_DIRECT=0): the same info, events and byte-identical cache
+    images (records with their P1 bounds, chain starts, op tables, pool, tokens,
+    client ids), over C4 and workflow histories, > 32 chains (the colouring's
+    heap), fencing tokens, and the structural variants it hands back to the
+    general path."""
+    from s2_verification_amd import workloads as W
+    blobs = [s2.simulate_jsonl(**W.c4_params(sd)) for sd in range(0, 24)]
+    for wf in (0, 1, 2):
+        blobs.append(s2.simulate_jsonl(workflow=wf, num_clients=5, ops_per_client=60, seed=3 + wf, p_indefinite=0.1))
+    blobs.append(s2.simulate_jsonl(workflow=0, num_clients=48, ops_per_client=12, seed=9, p_indefinite=0.05))
+    blobs += [open(os.path.join(GOLDEN, f), "rb").read() for f in sorted(os.listdir(GOLDEN)) if f.endswith(".jsonl")]
+    cases = list(blobs)
+    for b in blobs[:4] + blobs[24:28]:
+        cases += [v.encode() for v in _structural_variants(b.decode())]
+    many_chains = 0
+    for data in cases:
+        got = {}
+        for mode in ("1", "0"):
+            monkeypatch.setenv("S2LC_JSONL_DIRECT", mode)
+            try:
+                h = load(data)
+            except s2.S2LCError as e:
+                got[mode] = ("error", e.status, str(e))
+                continue
+            got[mode] = ("ok", h.info(), [(e.Kind, e.Id, e.ClientId, repr(e.Value)) for e in h.events()],
+                         s2.save_cache([h]))
+            if mode == "1" and h.info()["n_chains"] > 32:
+                many_chains += 1
+        assert got["1"] == got["0"], data[:200]
+    assert many_chains >= 1
