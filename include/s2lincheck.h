@@ -231,7 +231,14 @@ int s2lc_load_jsonl_many(const uint8_t* const* bufs, const size_t* lens, size_t 
 /* Build a history from porcupine-style events; all buffers are copied. */
 int s2lc_history_from_events(const s2lc_event* events, size_t n_events,
                              s2lc_history** out, char* err, size_t errlen);
+/* Release a history. Its arrays are parked in a process-wide pool of released
+ * histories (capacity kept) that the loaders decode the next histories into,
+ * up to S2LC_HISTORY_POOL_MB of array capacity (default 2048; 0 = off: arrays
+ * go back to the C heap here). */
 void s2lc_history_free(s2lc_history* h);
+/* Return every parked history's arrays to the C heap, and this thread's
+ * decode / finalize scratch; returns the array bytes (capacity) released. */
+size_t s2lc_history_pool_trim(void);
 size_t s2lc_history_event_count(const s2lc_history* h);
 /* Export event i (pointers stay valid while h lives). */
 int s2lc_history_get_event(const s2lc_history* h, size_t i, s2lc_event* out);

@@ -172,6 +172,7 @@ SIGNATURES = [
     ("s2lc_history_from_events", ctypes.c_int, [ctypes.POINTER(c_event), ctypes.c_size_t, ctypes.POINTER(_P),
                                                 ctypes.c_char_p, ctypes.c_size_t]),
     ("s2lc_history_free", None, [_P]),
+    ("s2lc_history_pool_trim", ctypes.c_size_t, []),
     ("s2lc_history_event_count", ctypes.c_size_t, [_P]),
     ("s2lc_history_get_event", ctypes.c_int, [_P, ctypes.c_size_t, ctypes.POINTER(c_event)]),
     ("s2lc_history_get_events", ctypes.c_int, [_P, _P, ctypes.c_size_t]),
@@ -474,6 +475,12 @@ def save_cache(hs: Sequence[History]) -> bytes:
     data = ctypes.string_at(buf, n.value)
     lib().s2lc_free(buf)
     return data
+
+
+def history_pool_trim() -> int:
+    """s2lc_history_pool_trim: return the released histories the decoders keep
+    for reuse (S2LC_HISTORY_POOL_MB) to the C heap; the array bytes released."""
+    return int(lib().s2lc_history_pool_trim())
 
 
 def load_cache(data: bytes, threads: int = 0) -> List[History]:

@@ -312,6 +312,7 @@ int s2lc_history_from_events(const s2lc_event* ev, size_t n, s2lc_history** out,
 }
 
 void s2lc_history_free(s2lc_history* h) { history_release(h); }
+size_t s2lc_history_pool_trim(void) { return history_pool_trim(); }
 
 size_t s2lc_history_event_count(const s2lc_history* h) { return h ? h->h.n_events() : 0; }
 

@@ -61,6 +61,18 @@ OpRec History::rec_of(uint32_t d) const {
   return r;
 }
 
+// finalize's working arrays: per decoder thread, reused from history to history
+namespace {
+struct FinalizeScratch {
+  std::vector<uint32_t> dense, dir, val, ncall, nret, call, ret, chain_of, chain_len, last, fill;
+  std::vector<int64_t> ids, key;
+  std::vector<int32_t> reg;
+};
+thread_local FinalizeScratch fin_scratch;
+}  // namespace
+
+void finalize_scratch_trim() { fin_scratch = FinalizeScratch(); }
+
 int History::finalize() {
   status = 0;
   error.clear();
@@ -68,12 +80,7 @@ int History::finalize() {
   const size_t E = events.size();
   if (E >= (size_t)EV_INF) { status = S2LC_EUNSUPPORTED; error = "too many events"; return status; }
 
-  // working arrays: per decoder thread, reused from history to history
-  thread_local struct {
-    std::vector<uint32_t> dense, dir, val, ncall, nret, call, ret, chain_of, chain_len, last, fill;
-    std::vector<int64_t> ids, key;
-    std::vector<int32_t> reg;
-  } S;
+  FinalizeScratch& S = fin_scratch;
   // porcupine renumber(): ids -> 0..m-1 in order of first appearance
   // (an open-addressing map, no per-id nodes)
   std::vector<uint32_t>& dense = S.dense;
@@ -304,6 +311,18 @@ static size_t used(const V& v) {
   return v.size() * sizeof(typename V::value_type);
 }
 
+template <class V>
+static size_t cap(const V& v) {
+  return v.capacity() * sizeof(typename V::value_type);
+}
+
+size_t History::capacity_bytes() const {
+  size_t b = cap(events) + cap(pool) + cap(op_call) + cap(op_ret) + cap(op_ids) + cap(chain_start) + cap(recs) +
+             cap(rec_op) + cap(op_rec) + cap(lit_id) + cap(lit_match) + cap(lazy_client) + cap(tokens);
+  for (const std::string& t : tokens) b += t.capacity();
+  return b;
+}
+
 size_t History::used_bytes() const {
   return used(events) + used(pool) + used(op_call) + used(op_ret) + used(op_ids) + used(chain_start) + used(recs) +
          used(rec_op) + used(op_rec) + used(lit_id) + used(lit_match) + used(lazy_client) + used(tokens);
@@ -339,7 +358,7 @@ struct HistoryPool {
   size_t budget;
   HistoryPool() {
     const char* e = getenv("S2LC_HISTORY_POOL_MB");
-    budget = (size_t)(e && *e ? strtoull(e, nullptr, 10) : 4096ull) << 20;
+    budget = (size_t)(e && *e ? strtoull(e, nullptr, 10) : 2048ull) << 20;
   }
 };
 // never destroyed: a history freed by another static destructor at exit must
@@ -386,11 +405,14 @@ void history_acquire_many(size_t n, s2lc_history** out) {
 void history_release(s2lc_history* h) {
   if (!h) return;
   HistoryPool& P = hpool();
-  // (accounted by the bytes in use at release: the pages a history touched
-  // stay resident, reserved capacity beyond them costs address space only)
-  const size_t b = h->h.used_bytes();
-  if (P.budget && b <= P.budget) {
+  // (accounted by capacity: an upper bound on what the parked arrays keep resident)
+  if (P.budget) {
     h->h.recycle();  // outside the lock: frees the token strings, keeps the arrays
+    const size_t b = h->h.capacity_bytes();
+    if (b > P.budget) {
+      delete h;
+      return;
+    }
     h->h.pooled_bytes = b;
     std::lock_guard<std::mutex> g(P.mu);
     if (P.bytes + b <= P.budget) {
@@ -400,6 +422,24 @@ void history_release(s2lc_history* h) {
     }
   }
   delete h;
+}
+
+size_t history_pool_trim() {
+  HistoryPool& P = hpool();
+  std::vector<s2lc_history*> v;
+  {
+    std::lock_guard<std::mutex> g(P.mu);
+    v.swap(P.free);
+    P.bytes = 0;
+  }
+  size_t b = 0;
+  for (s2lc_history* h : v) {
+    b += h->h.pooled_bytes;
+    delete h;
+  }
+  load_scratch_trim();
+  finalize_scratch_trim();
+  return b;
 }
 
 }  // namespace s2lc

@@ -95,7 +95,8 @@ struct History {
   // Back to the freshly constructed state, keeping every array's capacity.
   void recycle();
   size_t used_bytes() const;
-  size_t pooled_bytes = 0;  // used_bytes() when it was parked
+  size_t capacity_bytes() const;  // what its arrays hold allocated (the pool's accounting)
+  size_t pooled_bytes = 0;        // capacity_bytes() when it was parked
 };
 
 // OpRec flags of an op from its call's and return's fields (History::rec_of
@@ -143,10 +144,14 @@ namespace s2lc {
 // returning its arrays to the C heap. A long-running checker decodes batch N+1
 // into batch N's storage: no page faults, no heap growth or trim, no
 // address-space lock shared by the decoder threads. The pool is
-// bounded by S2LC_HISTORY_POOL_MB of array bytes in use at release (default
-// 4096; 0 = off).
+// bounded by S2LC_HISTORY_POOL_MB of array capacity (default 2048; 0 = off);
+// s2lc_history_pool_trim empties it.
 s2lc_history* history_acquire();
 // n histories under one lock (the parallel loaders take theirs up front)
 void history_acquire_many(size_t n, s2lc_history** out);
 void history_release(s2lc_history* h);
+size_t history_pool_trim();
+// this thread's decode / finalize scratch (jsonl.cpp, history.cpp) back to the heap
+void load_scratch_trim();
+void finalize_scratch_trim();
 }  // namespace s2lc

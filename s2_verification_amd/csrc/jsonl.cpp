@@ -713,20 +713,25 @@ bool json_ws(uint8_t c) { return c == ' ' || c == '\t' || c == '\n' || c == '\r'
 // finalize writes them. Returns false (h left for recycle()) on anything
 // else: a record not in the collector's form, op ids out of order, a second
 // Start or Finish, an op never returned, more than 2^16 - 1 tokens.
+struct DirectScratch {  // load_direct's working arrays, per decoder thread
+  std::vector<OpRec> orec;  // per dense op (op-major)
+  std::vector<uint32_t> chain_of, chain_len, last, fill;
+  std::vector<std::pair<uint32_t, uint32_t>> heap;  // (last return, chain), many chains
+};
+thread_local DirectScratch direct_scratch;
+
 bool load_direct(const uint8_t* buf, size_t len, History& h) {
-  thread_local struct {
-    std::vector<OpRec> orec;  // per dense op (op-major)
-    std::vector<uint32_t> chain_of, chain_len, last, fill;
-    std::vector<std::pair<uint32_t, uint32_t>> heap;  // (last return, chain), many chains
-  } S;
+  DirectScratch& S = direct_scratch;
   constexpr uint32_t OPEN = EV_INF;  // a chain whose last op has not returned
   std::vector<OpRec>& orec = S.orec;
   std::vector<uint32_t>&chain_of = S.chain_of, &chain_len = S.chain_len, &last = S.last;
   auto& heap = S.heap;
   orec.clear(); chain_of.clear(); chain_len.clear(); last.clear(); heap.clear();
-  orec.reserve(len / 160 + 16);
-  h.pool.reserve(h.pool.size() + len / 24);
-  h.lazy_client.reserve(len / 56 + 16);
+  // (sized for the collector's records, ~107 bytes per event and ~21 per
+  // record hash; a history past these grows them as usual)
+  orec.reserve(len / 128 + 16);
+  h.pool.reserve(h.pool.size() + len / 48 + 16);
+  h.lazy_client.reserve(len / 64 + 16);
   bool use_heap = false;
   uint32_t returned = 0;
   const uint8_t* p = buf;
@@ -1003,6 +1008,8 @@ int load_jsonl(const uint8_t* buf, size_t len, History& h, std::string& err) {
     h.events.push_back(e);
   }
 }
+
+void load_scratch_trim() { direct_scratch = DirectScratch(); }
 
 int load_jsonl_finalized(const uint8_t* buf, size_t len, History& h, std::string& err) {
   const char* e = getenv("S2LC_JSONL_DIRECT");  // 0: always the event list + finalize (tests compare the two)

@@ -333,3 +333,23 @@ def test_direct_decode_leaves_the_finalized_state(monkeypatch):
                 many_chains += 1
         assert got["1"] == got["0"], data[:200]
     assert many_chains >= 1
+
+
+def test_history_pool_trim():
+    """Released histories are parked for the next decode (S2LC_HISTORY_POOL_MB,
+    accounted by array capacity); s2lc_history_pool_trim returns them to the
+    heap and reports the bytes, and decoding afterwards is unchanged."""
+    import gc
+    from s2_verification_amd import workloads as W
+    blobs = [s2.simulate_jsonl(**W.c4_params(sd)) for sd in range(8)]
+    want = [h.events() for h in s2.load_many(blobs, threads=2)]
+    gc.collect()
+    s2.history_pool_trim()
+    hs = s2.load_many(blobs, threads=2)
+    n_bytes = sum(len(b) for b in blobs)
+    del hs
+    gc.collect()
+    freed = s2.history_pool_trim()
+    assert n_bytes // 4 < freed < 4 * n_bytes  # records, pool, op tables: ~0.7x the JSONL
+    assert s2.history_pool_trim() == 0
+    assert [h.events() for h in s2.load_many(blobs, threads=2)] == want
