@@ -475,15 +475,38 @@ struct Fast {
   template <size_t N>
   bool lit(const char (&w)[N]) {
     constexpr size_t n = N - 1;
-    if ((size_t)(end - p) < n) return false;
-    size_t i = 0;
-    for (; i + 8 <= n; i += 8) {
-      uint64_t a, b;
-      memcpy(&a, p + i, 8);
-      memcpy(&b, w + i, 8);
-      if (a != b) return false;
+    static_assert(n >= 1, "literal");
+    if ((size_t)(end - p) < (n < 8 ? 8 : n)) return lit_short(w);
+    // whole 8-byte words, the last one overlapping the one before (n >= 8),
+    // or one masked word (n < 8): no byte loop
+    if constexpr (n >= 8) {
+      for (size_t i = 0; i + 8 <= n; i += 8) {
+        uint64_t a, b;
+        memcpy(&a, p + i, 8);
+        memcpy(&b, w + i, 8);
+        if (a != b) return false;
+      }
+      if constexpr (n % 8 != 0) {
+        uint64_t a, b;
+        memcpy(&a, p + n - 8, 8);
+        memcpy(&b, w + n - 8, 8);
+        if (a != b) return false;
+      }
+    } else {
+      uint64_t a, b = 0;
+      memcpy(&a, p, 8);
+      memcpy(&b, w, n);
+      if ((a & (~0ull >> (8 * (8 - n)))) != b) return false;
     }
-    for (; i < n; ++i)
+    p += n;
+    return true;
+  }
+  // (within 8 bytes of the end of the input)
+  template <size_t N>
+  bool lit_short(const char (&w)[N]) {
+    constexpr size_t n = N - 1;
+    if ((size_t)(end - p) < n) return false;
+    for (size_t i = 0; i < n; ++i)
       if (p[i] != (uint8_t)w[i]) return false;
     p += n;
     return true;
@@ -531,6 +554,23 @@ struct Fast {
   }
   bool u64(uint64_t& v) {
     const uint8_t* s = p;
+    if (end - s >= 8) {  // fewer than 8 digits: one load, right-aligned by a shift
+      uint64_t w;
+      memcpy(&w, s, 8);
+      const uint64_t a = (w & 0xF0F0F0F0F0F0F0F0ull) ^ 0x3030303030303030ull;
+      const uint64_t b = ((w + 0x0606060606060606ull) & 0xF0F0F0F0F0F0F0F0ull) ^ 0x3030303030303030ull;
+      const uint64_t m = a | b;
+      if (m) {
+        const unsigned n = (unsigned)__builtin_ctzll(m) >> 3;  // digits
+        if (n == 0 || (n > 1 && s[0] == '0')) return false;
+        const unsigned sh = 8 * (8 - n);  // 8..56
+        const uint64_t x = (w << sh) | (0x3030303030303030ull >> (64 - sh));
+        v = eight_v(x);
+        p = s + n;
+        const uint8_t c = *p;  // (n < 8: the terminator is inside the loaded word)
+        return !(c == '.' || c == 'e' || c == 'E');
+      }
+    }
     p += digits(s);
     const size_t n = (size_t)(p - s);
     if (n == 0 || n > 20 || (n > 1 && s[0] == '0')) return false;
@@ -765,8 +805,13 @@ bool load_direct(const uint8_t* buf, size_t len, History& h) {
       uint32_t c = EV_INF;
       if (!use_heap) {
         uint32_t best = EV_INF;
-        for (uint32_t k = 0; k < (uint32_t)last.size(); ++k)
-          if (last[k] < best) { best = last[k]; c = k; }
+        const uint32_t nk = (uint32_t)last.size();
+        for (uint32_t k = 0; k < nk; ++k) {  // (branch-free: which chain ended first is data)
+          const uint32_t x = last[k];
+          const bool lt = x < best;
+          best = lt ? x : best;
+          c = lt ? k : c;
+        }
       } else if (!heap.empty()) {
         std::pop_heap(heap.begin(), heap.end(), gt);
         c = heap.back().second;
