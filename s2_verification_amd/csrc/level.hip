@@ -333,8 +333,9 @@ int level_search(DevBatch& b, uint32_t h, hipStream_t st, const RunOpts& ro, int
 
 #ifdef S2LC_PROF
   unsigned long long* d_prof = nullptr;
-  LVCHK(hipMalloc(&d_prof, 48 * sizeof(unsigned long long)));
-  LVCHK(hipMemset(d_prof, 0, 48 * sizeof(unsigned long long)));
+  const size_t prof_n = 48 + 11 * (size_t)LV_PROF_ROUNDS;
+  LVCHK(hipMalloc(&d_prof, prof_n * sizeof(unsigned long long)));
+  LVCHK(hipMemset(d_prof, 0, prof_n * sizeof(unsigned long long)));
   LVCHK(hipStreamSynchronize(nullptr));
   p.prof = d_prof;
 #endif
@@ -500,6 +501,19 @@ int level_search(DevBatch& b, uint32_t h, hipStream_t st, const RunOpts& ro, int
   {
     unsigned long long g[48];
     LVCHK(hipMemcpy(g, d_prof, sizeof g, hipMemcpyDeviceToHost));
+    if (const char* path = getenv("S2LC_LVPROF_ROUNDS")) {  // one line per persistent grid round
+      std::vector<unsigned long long> pr(11 * (size_t)LV_PROF_ROUNDS);
+      LVCHK(hipMemcpy(pr.data(), d_prof + 48, pr.size() * sizeof(unsigned long long), hipMemcpyDeviceToHost));
+      if (FILE* f = fopen(path, "a")) {
+        for (uint32_t r = 0; r < LV_PROF_ROUNDS; ++r)
+          if (pr[r])
+            fprintf(f, "%u %llu %llu %llu %llu %llu %llu %llu %llu %llu %llu %llu\n", r, pr[r], pr[LV_PROF_ROUNDS + r],
+                    pr[2 * LV_PROF_ROUNDS + r], pr[3 * LV_PROF_ROUNDS + r], pr[4 * LV_PROF_ROUNDS + r],
+                    pr[5 * LV_PROF_ROUNDS + r], pr[6 * LV_PROF_ROUNDS + r], pr[7 * LV_PROF_ROUNDS + r],
+                    pr[8 * LV_PROF_ROUNDS + r], pr[9 * LV_PROF_ROUNDS + r], pr[10 * LV_PROF_ROUNDS + r]);
+        fclose(f);
+      }
+    }
     (void)hipFree(d_prof);
     const double it = g[5] ? (double)g[5] : 1.0, ch = g[6] ? (double)g[6] : 1.0;
     fprintf(stderr,

@@ -484,6 +484,7 @@ __device__ __forceinline__ void lv_release(const LvParams& p, uint32_t st, uint3
     if (rk + i < p.scs) lv_cfg<NQ>(p.stg, st * p.scs + rk + i)->move = LV_HOLE;
 }
 
+constexpr uint32_t LV_PROF_ROUNDS = 16384;  // S2LC_PROF: persistent grid rounds logged one by one
 // S2LC_PROF: per-phase cycle counts of lv_expand (lane 0 of every wave, summed
 // into p.prof by the waves that had items; every lap first waits for the
 // wave's outstanding loads): [0] parent load, [1] heads + fingerprint, [2]
@@ -670,6 +671,139 @@ __device__ __forceinline__ void lv_stage_insert(const LvParams& p, const LvRound
   if (lane == 0) atomicExch(&p.ht[slot], mine);
 }
 
+// S2LC_BATCH_INSERT (default on): the persistent rounds' children are staged
+// first (the whole configuration, drained once per batch) and inserted LV_PEND
+// at a time, one lane per child: one CAS latency for the batch, tag hits
+// compared four at a time, one next-frontier atomic for the batch's winners.
+// Inserting each child on its own cost a chain of device-scope round trips per
+// child (~4.6 us each in C5's slowest grid rounds). C5 0.0913 -> 0.0905 s,
+// C5wide 0.0369 -> 0.0362 s (profiles/r05/c5_batch_insert_ab.txt); the
+// configurations and rounds are unchanged.
+#ifndef S2LC_BATCH_INSERT
+#define S2LC_BATCH_INSERT 1
+#endif
+constexpr uint32_t LV_PEND = 32;
+struct LvPend {
+  unsigned long long fp[LV_PEND];
+  uint32_t k[LV_PEND], mv[LV_PEND], pt[LV_PEND];
+};
+
+template <int NQ>
+__device__ __forceinline__ void lv_flush_pend(const LvParams& p, const LvRoundIn& in, LvPend& P, uint32_t& np) {
+  if (np == 0) return;
+  const int lane = (int)(threadIdx.x & 63);
+  lv_drain();  // every pending configuration has landed
+  __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  const bool act = (uint32_t)lane < np;
+  const unsigned long long fp = act ? P.fp[lane] : 0ull;
+  const uint32_t k = act ? P.k[lane] : 0u;
+  const uint32_t tag = (uint32_t)(fp >> 32);
+  const unsigned long long mine = ((unsigned long long)tag << 32) | k;
+  uint32_t slot = (uint32_t)fp & p.ht_mask;
+  bool probing = act, win = false;
+  while (__ballot(probing)) {
+    unsigned long long prev = HT_EMPTY;
+    if (probing) prev = atomicCAS(&p.ht[slot], HT_EMPTY, mine);
+    const bool hit = probing && prev != HT_EMPTY && (uint32_t)(prev >> 32) == tag;
+    if (probing && prev == HT_EMPTY) {
+      win = true;
+      probing = false;
+    } else if (probing && !hit) {
+      slot = (slot + 1) & p.ht_mask;  // another configuration's entry: the next slot
+    }
+    // the tag hits: each resident configuration compared with the pending one,
+    // wave-parallel, LV_CMP of them with their loads in flight together
+    constexpr int LV_CMP = 4;
+    uint64_t hm = __ballot(hit);
+    while (hm) {
+      int jj[LV_CMP];
+      bool ne[LV_CMP];
+#pragma unroll
+      for (int c = 0; c < LV_CMP; ++c) {
+        jj[c] = hm ? __ffsll((unsigned long long)hm) - 1 : -1;
+        if (hm) hm &= hm - 1;
+      }
+#pragma unroll
+      for (int c = 0; c < LV_CMP; ++c) {
+        ne[c] = false;
+        if (jj[c] < 0) continue;
+        const LCfg<NQ>* e = lv_cfg<NQ>(p.stg, (uint32_t)rl64(prev, jj[c]));
+        const LCfg<NQ>* m = lv_cfg<NQ>(p.stg, rl(k, jj[c]));
+        const unsigned long long et = ld_wt64(&e->tail), eh = ld_wt64(&e->hash), ek = ld_wt64(&e->tok);
+        const unsigned long long mt = ld_wt64(&m->tail), mh = ld_wt64(&m->hash), mk = ld_wt64(&m->tok);
+        bool x = et != mt || eh != mh || (uint32_t)ek != (uint32_t)mk;
+#pragma unroll
+        for (int q = 0; q < NQ; ++q) x |= ld_wt16(&e->cnt[lane + 64 * q]) != ld_wt16(&m->cnt[lane + 64 * q]);
+        ne[c] = x;
+      }
+#pragma unroll
+      for (int c = 0; c < LV_CMP; ++c) {
+        if (jj[c] < 0) continue;
+        const bool eq = __ballot(ne[c]) == 0;
+        if (lane == jj[c]) {
+          if (eq) probing = false;  // an equal configuration is already in the round
+          else slot = (slot + 1) & p.ht_mask;
+        }
+      }
+    }
+  }
+  // the winners' next-frontier positions: one atomic for the batch
+  const uint64_t wm = __ballot(win);
+  uint32_t base = 0;
+  if (lane == 0 && wm) base = atomicAdd(&p.ctl->nnext, (uint32_t)__popcll(wm));
+  base = rl(base, 0);
+  if (win) {
+    const uint32_t n = base + (uint32_t)__popcll(wm & ((1ull << lane) - 1));
+    const uint32_t tr = in.wit ? p.tgid + in.tbase + n : TRACE_NONE;
+    st_wt64(reinterpret_cast<unsigned long long*>(lv_cfg<NQ>(p.stg, k)) + 5, (unsigned long long)slot << 32 | tr);
+    st_wt32(&p.nxt_idx[n], k);
+    if (in.wit) p.trace[in.tbase + n] = TraceEnt{P.pt[lane], P.mv[lane]};
+  }
+  np = 0;
+}
+
+// Stage one closed child for a batched insert: the configuration (all but its
+// slot / trace word) with write-through stores, its key in the wave's list.
+template <int NQ>
+__device__ __forceinline__ void lv_stage_pend(const LvParams& p, const LvRoundIn& in, uint32_t st, uint32_t& rk,
+                                              uint32_t& rleft, const State& s, uint64_t fp, uint64_t chx,
+                                              uint32_t minret, uint32_t ptrace, uint32_t move,
+                                              const uint32_t (&cnt)[NQ], const uint32_t (&d)[NQ], LvPend& P,
+                                              uint32_t& np) {
+  const int lane = (int)(threadIdx.x & 63);
+  if (rleft == 0) {
+    uint32_t b = 0;
+    if (lane == 0) b = atomicAdd(&p.ctl->cnt[16 * st], LV_RESERVE);
+    rk = rl(b, 0);
+    rleft = LV_RESERVE;
+  }
+  const uint32_t i = rk++;
+  rleft--;
+  if (i >= p.scs) {
+    if (lane == 0) atomicExch(&p.ctl->overflow, 1u);
+    return;
+  }
+  const uint32_t k = st * p.scs + i;
+  LCfg<NQ>* o = lv_cfg<NQ>(p.stg, k);
+  const unsigned long long w = lane == 0 ? s.tail
+                             : lane == 1 ? s.hash
+                             : lane == 2 ? fp
+                             : lane == 3 ? ((unsigned long long)minret << 32 | s.tok)
+                             : lane == 4 ? ((unsigned long long)move << 32 | ptrace)
+                             : lane == 6 ? chx
+                                         : 0ull;
+  if (lane < 16 && lane != 5) st_wt64(reinterpret_cast<unsigned long long*>(o) + lane, w);
+  lv_store_cnt_wt<NQ>(o->cnt, cnt, d);
+  if (lane == 0) {
+    P.fp[np] = fp;
+    P.k[np] = k;
+    P.mv[np] = move;
+    P.pt[np] = ptrace;
+  }
+  if (++np == LV_PEND) lv_flush_pend<NQ>(p, in, P, np);
+}
+
 // Workgroup barrier over LDS only: waits for this wave's LDS operations, not
 // for its global loads and write-through stores (a __syncthreads release
 // would drain those too). Solo rounds share only LDS between their waves.
@@ -769,10 +903,19 @@ __device__ __forceinline__ bool lv_expand(const LvParams& p, const LvRoundIn& in
   unsigned long long kids = 0;
   uint32_t closed = 0;  // children closed by this wave (wave-uniform)
   uint32_t staged = 0;  // children it staged (grid rounds)
+  // (S2LC_BATCH_INSERT: the wave's children waiting for their batched insert)
+  __shared__ LvPend s_pend[FUSED && S2LC_BATCH_INSERT ? LV_BLOCK / 64 : 1];
+  LvPend& PP = s_pend[FUSED && S2LC_BATCH_INSERT ? (threadIdx.x >> 6) : 0];
+  uint32_t np = 0;
 #ifdef S2LC_PROF
   unsigned long long lv_acc[10] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0}, lv_t = 0;
+  const unsigned long long w_t0 = clock64();
+  unsigned long long w_ins = 0, w_cl = 0, w_items = 0, w_pend = 0;
 #endif
   for (uint32_t it = wave_id; it < items; it += nwaves) {
+#ifdef S2LC_PROF
+    ++w_items;
+#endif
     LV_T0();
     LV_ADD(5, 1);
     const uint32_t f = f0 + it / S;
@@ -1038,7 +1181,13 @@ __device__ __forceinline__ bool lv_expand(const LvParams& p, const LvRoundIn& in
         LV_LAP(4);
         LV_ADD(6, 1);
         ++closed;
+#ifdef S2LC_PROF
+        const unsigned long long w_c0 = clock64();
+#endif
         const int cr = lv_closure<NQ>(H, d, cnt, s_cs, PL, lane, cs_, p.hflags, pmin, p.recs, mr);
+#ifdef S2LC_PROF
+        w_cl += clock64() - w_c0;
+#endif
         LV_LAP(3);
         if (cr == CL_COMPLETE || cr == CL_P4) {
           if (lane == 0 && atomicCAS(&p.ctl->found, 0u, 1u) == 0u) {
@@ -1056,7 +1205,15 @@ __device__ __forceinline__ bool lv_expand(const LvParams& p, const LvRoundIn& in
           const uint64_t cdx = parent_chx ^ wave_xor_u64(dx);
           auto fp_of = [&]() { return mix64(cdx ^ lv_state_term(cs_.tail, cs_.hash, cs_.tok)); };
           if (FUSED) {
-            lv_stage_insert<NQ>(p, in, stripe, rk, rleft, cs_, fp_of(), cdx, mr, ptrace, mv, cnt, d);
+#ifdef S2LC_PROF
+            const unsigned long long w_i0 = clock64();
+#endif
+            if (S2LC_BATCH_INSERT) lv_stage_pend<NQ>(p, in, stripe, rk, rleft, cs_, fp_of(), cdx, mr, ptrace, mv, cnt, d, PP, np);
+            else lv_stage_insert<NQ>(p, in, stripe, rk, rleft, cs_, fp_of(), cdx, mr, ptrace, mv, cnt, d);
+#ifdef S2LC_PROF
+            w_ins += clock64() - w_i0;
+            ++w_pend;
+#endif
           } else {
             lv_stage<NQ>(p, stripe, rk, rleft, cs_, fp_of(), cdx, mr, ptrace, mv, cnt, d);
             ++staged;
@@ -1072,9 +1229,18 @@ __device__ __forceinline__ bool lv_expand(const LvParams& p, const LvRoundIn& in
       }
     }
   }
+  if (FUSED && S2LC_BATCH_INSERT) lv_flush_pend<NQ>(p, in, PP, np);
 #ifdef S2LC_PROF
   if (lane == 0 && p.prof && lv_acc[5])  // only waves that had work (idle waves would swamp the counters)
     for (int i_ = 0; i_ < 9; ++i_) atomicAdd(&p.prof[i_ < 7 ? i_ : i_ + 5], lv_acc[i_]);
+  if (FUSED && lane == 0 && p.prof && w_items && p.round < LV_PROF_ROUNDS) {  // per round: the busiest wave's split
+    unsigned long long* pr = p.prof + 48 + 6 * LV_PROF_ROUNDS;
+    atomicMax(&pr[p.round], clock64() - w_t0);
+    atomicMax(&pr[LV_PROF_ROUNDS + p.round], w_ins);
+    atomicMax(&pr[2 * LV_PROF_ROUNDS + p.round], w_cl);
+    atomicMax(&pr[3 * LV_PROF_ROUNDS + p.round], w_items);
+    atomicMax(&pr[4 * LV_PROF_ROUNDS + p.round], w_pend);
+  }
 #endif
   if (MODE == 0 && rleft) lv_release<NQ>(p, stripe, rk, rleft);
   if (lane == 0 && kids) atomicAdd(&p.ctl->children, kids);
@@ -1558,12 +1724,24 @@ __global__ __launch_bounds__(LV_BLOCK, 1) void lv_persist(LvParams p, LvPersist 
       atomicAdd(&p.prof[9], t_b - t_round);
       atomicAdd(&p.prof[10], e > t_round ? e - t_round : 0ull);
       atomicAdd(&p.prof[11], 1ull);
+      if (r < LV_PROF_ROUNDS) {  // per round: time, expansion critical path, frontier (wall-clock ticks)
+        p.prof[48 + r] = t_b - t_round;
+        p.prof[48 + LV_PROF_ROUNDS + r] = e > t_round ? e - t_round : 0ull;
+        p.prof[48 + 2 * LV_PROF_ROUNDS + r] = in.nf;
+      }
       t_round = t_b;
     }
 #endif
     if (threadIdx.x == 0) {
       if (ok) {
         const LvCounts k = lv_read_counts(rp.ctl);
+#ifdef S2LC_PROF
+        if (blockIdx.x == 0 && p.prof && r < LV_PROF_ROUNDS) {  // per round: closed, children, slices
+          p.prof[48 + 3 * LV_PROF_ROUNDS + r] = k.closed;
+          p.prof[48 + 4 * LV_PROF_ROUNDS + r] = k.ch;
+          p.prof[48 + 5 * LV_PROF_ROUNDS + r] = in.S;
+        }
+#endif
         lv_close_state(s_run, k, r, blockIdx.x == 0 ? p.rcounts : nullptr, p.scap, p.trace_cap);
         if (ld_agent(&rp.ctl->stop) && s_run.done == LVR_RUNNING) s_run.done = LVR_TIMEOUT;
       } else {
