@@ -43,6 +43,13 @@ enum LvKernel { LK_ROUND = 0, LK_INSERT, LK_BUCKET, LK_SCATTER, LK_KEEP, LK_GATH
 size_t lv_cfg_bytes(uint32_t nq) { return 128 + 128 * (size_t)nq; }
 
 // a host-driven round's bookkeeping, after its last chunk (one thread)
+// S2LC_TAG_DROP (tests): bits cleared from the dedupe tables' tags and first
+// slots (LvParams::tag_drop); unset or 0 in production
+uint32_t lv_tag_drop() {
+  const char* e = getenv("S2LC_TAG_DROP");
+  return e ? (uint32_t)strtoul(e, nullptr, 0) : 0u;
+}
+
 __global__ void lv_close_kernel(LvParams p) { lv_close_round(p); }
 
 template <int NQ>
@@ -292,6 +299,7 @@ int level_search(DevBatch& b, uint32_t h, hipStream_t st, const RunOpts& ro, int
 
   LvParams p;
   memset(&p, 0, sizeof p);
+  p.tag_drop = lv_tag_drop();
   p.recs = b.recs; p.pool = b.pool; p.cs = b.chain_start + hd.cs_base; p.K = K; p.hflags = hd.flags;
   p.scap = L.scap; p.scs = L.scap / LV_STRIPES; p.ht_mask = L.ht_mask;
   p.trace = b.trace; p.trace_cap = b.trace_cap;
@@ -677,6 +685,7 @@ static LvParams dist_params(DistLevel& d) {
   const HistDesc& hd = d.b.h_hist[0];
   LvParams p;
   memset(&p, 0, sizeof p);
+  p.tag_drop = lv_tag_drop();
   p.recs = d.b.recs; p.pool = d.b.pool; p.cs = d.b.chain_start + hd.cs_base; p.K = d.K; p.hflags = hd.flags;
   p.scap = L.scap; p.scs = L.scap / LV_STRIPES; p.ht = L.ht[0]; p.ht_clear = L.ht[0]; p.ht_mask = L.ht_mask;
   p.trace = d.trace; p.trace_cap = d.trace_cap;

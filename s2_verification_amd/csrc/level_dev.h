@@ -127,6 +127,10 @@ static_assert(sizeof(LvRun) == 128, "LvRun layout");
 constexpr uint32_t LV_WIDE_NF = 4096;  // (distributed.py's default `wide`)
 
 struct LvParams {
+  // test knob (S2LC_TAG_DROP, zero in production): bits cleared from every
+  // dedupe table tag and first probe slot, so that distinct configurations
+  // meet on one tag and the compare-and-probe paths run all the time
+  uint32_t tag_drop;
   const OpRec* __restrict__ recs;
   const uint64_t* __restrict__ pool;
   const uint32_t* __restrict__ cs;  // K+1 absolute chain starts of this history
@@ -622,9 +626,9 @@ __device__ __forceinline__ void lv_stage_insert(const LvParams& p, const LvRound
   // nothing at all (wide rounds stage several copies of most configurations).
   // A wave that meets a pending entry with its tag waits for the final form
   // before it reads the configuration.
-  const uint32_t tag = (uint32_t)(fp >> 32);
+  const uint32_t tag = (uint32_t)(fp >> 32) & ~p.tag_drop;
   const unsigned long long mine = ((unsigned long long)tag << 32) | k;
-  uint32_t slot = (uint32_t)fp & p.ht_mask;
+  uint32_t slot = (uint32_t)fp & p.ht_mask & ~p.tag_drop;
   for (;;) {
     unsigned long long prev = 0;
     if (lane == 0) prev = atomicCAS(&p.ht[slot], HT_EMPTY, mine | LV_PENDING);
@@ -698,9 +702,9 @@ __device__ __forceinline__ void lv_flush_pend(const LvParams& p, const LvRoundIn
   const bool act = (uint32_t)lane < np;
   const unsigned long long fp = act ? P.fp[lane] : 0ull;
   const uint32_t k = act ? P.k[lane] : 0u;
-  const uint32_t tag = (uint32_t)(fp >> 32);
+  const uint32_t tag = (uint32_t)(fp >> 32) & ~p.tag_drop;
   const unsigned long long mine = ((unsigned long long)tag << 32) | k;
-  uint32_t slot = (uint32_t)fp & p.ht_mask;
+  uint32_t slot = (uint32_t)fp & p.ht_mask & ~p.tag_drop;
   bool probing = act, win = false;
   while (__ballot(probing)) {
     unsigned long long prev = HT_EMPTY;
@@ -1489,9 +1493,9 @@ __global__ __launch_bounds__(LV_BLOCK) void lv_insert(LvParams p) {
     if (valid) {
       if (c->move != LV_HOLE) {
         const uint64_t fp = c->fp;
-        const uint32_t tag = (uint32_t)(fp >> 32);
+        const uint32_t tag = (uint32_t)(fp >> 32) & ~p.tag_drop;
         const unsigned long long mine = ((unsigned long long)tag << 32) | k;
-        slot = (uint32_t)fp & p.ht_mask;
+        slot = (uint32_t)fp & p.ht_mask & ~p.tag_drop;
         for (;;) {
           const unsigned long long prev = atomicCAS(&p.ht[slot], HT_EMPTY, mine);
           if (prev == HT_EMPTY) { win = true; break; }

@@ -98,3 +98,25 @@ def test_hard_single_history(checker, name):
     assert r.verdict == ref[name]["verdict"], (name, r, st)
     if r.verdict == s2.Ok:
         assert r.witness is not None and len(r.witness) == h.info()["n_ops"]
+
+
+@pytest.mark.parametrize("mode", [{}, {"S2LC_NO_SOLO": "1"}, {"S2LC_NO_PERSIST": "1"}])
+def test_dedupe_under_forced_tag_collisions(mode, monkeypatch):
+    """The level search's dedupe tables compare the whole configuration on a
+    tag hit and probe on. S2LC_TAG_DROP clears all but 8 bits of every tag and
+    first slot (256 of each), so distinct configurations meet on one tag all
+    the time: H174 must still give the committed reduced-search round counts
+    (every unique configuration kept, every duplicate dropped) in each round
+    mode: solo + persistent grid rounds (batched inserts), grid rounds only,
+    host-enqueued rounds (lv_insert)."""
+    from s2_verification_amd import workloads as W
+    monkeypatch.setenv("S2LC_TAG_DROP", "0xFFFFFF00")
+    for k, v in mode.items():
+        monkeypatch.setenv(k, v)
+    g = golden("hard_round_counts.json")["H174"]
+    assert config_digest("H174") == g["digest"]
+    h = W.config_history("H174")
+    b = s2.Checker(round_counts=True).batch([h])
+    r = b.check()[0]
+    assert (r.verdict, b.round_counts(0)) == (g["0"]["verdict"], g["0"]["counts"]), (mode, r)
+    assert r.witness is not None and len(r.witness) == h.info()["n_ops"]
