@@ -326,7 +326,8 @@ typedef struct s2lc_batch_stats {
   double pack16_ms;          /* its launch, HIP events on the ctx stream */
   uint64_t pack16_algo_bytes;/* algorithmic bytes of the histories it settled */
   uint32_t pack16_histories;
-  uint32_t _pad1;
+  uint32_t pack16_small;     /* of pack16_histories: settled from 32-byte records (every history of the list has
+                                tails <= 65,532, < 65,535 events and hash counts < 65,536; S2LC_PACK_SMALL=0: never) */
   /* level search round modes: rounds run inside the persistent kernel, its
    * launches, frontier-chunk re-runs after a staging overflow, host syncs */
   uint64_t level_persist_rounds;

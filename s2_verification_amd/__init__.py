@@ -104,7 +104,7 @@ class c_batch_stats(ctypes.Structure):
                 ("level_max_frontier", ctypes.c_uint32), ("level_rounds", ctypes.c_uint64),
                 ("level_configs", ctypes.c_uint64), ("level_children", ctypes.c_uint64),
                 ("pack16_ms", ctypes.c_double), ("pack16_algo_bytes", ctypes.c_uint64),
-                ("pack16_histories", ctypes.c_uint32), ("_pad1", ctypes.c_uint32),
+                ("pack16_histories", ctypes.c_uint32), ("pack16_small", ctypes.c_uint32),
                 ("level_persist_rounds", ctypes.c_uint64), ("level_persist_launches", ctypes.c_uint32),
                 ("level_chunk_retries", ctypes.c_uint32), ("level_syncs", ctypes.c_uint32), ("level_solo_rounds", ctypes.c_uint32),
                 ("n_ops_total", ctypes.c_uint64), ("pack8_ms", ctypes.c_double),

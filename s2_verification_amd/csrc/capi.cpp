@@ -694,6 +694,7 @@ int s2lc_batch_stats_get(const s2lc_batch* b, s2lc_batch_stats* out) {
   out->pack16_ms = b->stats.pack16_ms;
   out->pack16_algo_bytes = b->stats.pack16_algo_bytes;
   out->pack16_histories = b->stats.pack16_histories;
+  out->pack16_small = b->stats.pack16_small;
   out->level_persist_rounds = b->stats.level.persist_rounds;
   out->level_persist_launches = (uint32_t)b->stats.level.persist_launches;
   out->level_chunk_retries = b->stats.level.chunk_retries;

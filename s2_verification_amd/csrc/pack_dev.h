@@ -25,6 +25,7 @@
 // group (lanes l >= K take part with a null chain), so ballots and shuffles
 // never read a disabled lane. Groups of one wave diverge freely.
 #pragma once
+#include <type_traits>
 
 namespace s2lc {
 namespace {
@@ -154,13 +155,16 @@ constexpr int PACK_PN = S2LC_PACK_PN;  // read-ahead records per refill
 #define S2LC_PACK_PH 0
 #endif
 constexpr int PACK_PH = S2LC_PACK_PH;  // 1: a refill also touches the window's second record's hashes
+template <bool SMALL>
 struct ChainLane {
-  const OpRec* __restrict__ base;  // first record of chain l (valid iff on)
+  using Rec = typename std::conditional<SMALL, SRec, OpRec>::type;
+  static constexpr int NW = SMALL ? 2 : 4;  // uint4 words per record
+  const Rec* __restrict__ base;    // first record of chain l (valid iff on)
   bool on;                         // l < K
   uint32_t len;                    // records of chain l, its sentinel included
   uint32_t w0;                     // count of the window's first record
   uint32_t cc;                     // count of r
-  uint4 w[PACK_W][4];              // window: records at counts w0 .. w0+PACK_W-1
+  uint4 w[PACK_W][NW];             // window: records at counts w0 .. w0+PACK_W-1
   OpRec r;                         // record at count cc (null record when !on)
   uint32_t pfx[PACK_PN];           // read-ahead dwords of the last refill (PACK_PD)
   uint32_t sink;                   // read-ahead dwords consumed
@@ -169,7 +173,7 @@ struct ChainLane {
 #ifdef S2LC_PROF
   bool refilled;                   // the last at() reloaded the window
 #endif
-  __device__ __forceinline__ void reset(const OpRec* b, bool on_, uint32_t len_) {
+  __device__ __forceinline__ void reset(const Rec* b, bool on_, uint32_t len_) {
     base = b;
     on = on_;
     len = len_;
@@ -195,13 +199,13 @@ struct ChainLane {
       refilled = true;
 #endif
       // clamp to the chain: a record past its sentinel is never selected
-      const OpRec* q = base + c;
+      const Rec* q = base + c;
       const uint32_t last = len - 1 - c;  // c < len always (sentinel included)
 #pragma unroll
       for (int i = 0; i < PACK_W; ++i) {
         const uint4* qi = reinterpret_cast<const uint4*>(q + min((uint32_t)i, last));
 #pragma unroll
-        for (int k = 0; k < 4; ++k) w[i][k] = qi[k];
+        for (int k = 0; k < NW; ++k) w[i][k] = qi[k];
       }
       if (PACK_PD > 0) {
 #pragma unroll
@@ -210,7 +214,7 @@ struct ChainLane {
         for (int i = 0; i < PACK_PN; ++i)
           pfx[i] = *reinterpret_cast<const uint32_t*>(q + min((uint32_t)(PACK_PD + i), last));
       }
-      if (PACK_PH) {
+      if constexpr (PACK_PH && !SMALL) {
         sink ^= phx;
         phx = w[1][3].y ? pool32[2 * w[1][3].x] : 0u;  // hash_cnt, hash_off of record c+1
       }
@@ -218,9 +222,9 @@ struct ChainLane {
       o = 0;
     }
     // select dword-wise in registers (a struct-typed select goes through scratch)
-    uint4 sel[4];
+    uint4 sel[NW];
 #pragma unroll
-    for (int k = 0; k < 4; ++k) {
+    for (int k = 0; k < NW; ++k) {
       sel[k] = w[0][k];
 #pragma unroll
       for (int i = 1; i < PACK_W; ++i) {
@@ -231,15 +235,35 @@ struct ChainLane {
         sel[k].w = t ? w[i][k].w : sel[k].w;
       }
     }
-    __builtin_memcpy(&r, sel, sizeof(OpRec));
+    if constexpr (SMALL) {  // widen (search.h, SRec)
+      r.out_hash = (uint64_t)sel[0].x | ((uint64_t)sel[0].y << 32);
+      r.hash_off = sel[0].z;
+      r.num_records = sel[0].w & 0xFFFFu;
+      // msn / out_tail 0xFFFF and a bound 0xFFFD stay as they are: no
+      // reachable tail (<= 65,532) equals or passes them; REQ_NONE,
+      // REQ_HASH_ONLY and EV_INF widen to their 64 / 32-bit values
+      const uint32_t sf = sel[1].x >> 16;
+      r.msn = sel[0].w >> 16;
+      r.out_tail = sel[1].x & 0xFFFFu;
+      r.sufmin = (uint64_t)sf | (sf >= 0xFFFEu ? 0xFFFFFFFFFFFF0000ull : 0ull);
+      const uint32_t ce = sel[1].y & 0xFFFFu, re = sel[1].y >> 16;
+      r.call_ev = ce | (ce == 0xFFFFu ? 0xFFFF0000u : 0u);
+      r.ret_ev = re | (re == 0xFFFFu ? 0xFFFF0000u : 0u);
+      r.hash_cnt = sel[1].z & 0xFFFFu;
+      r.flags = sel[1].z >> 16;
+      r.batch_tok = (uint16_t)(sel[1].w & 0xFFFFu);
+      r.set_tok = (uint16_t)(sel[1].w >> 16);
+    } else {
+      __builtin_memcpy(&r, sel, sizeof(OpRec));
+    }
     cc = c;
   }
 };
 
 // Group closure of one configuration (state s, lane count cnt) under minimal,
 // legal identity ops + P1/P2/P4; returns CL_* and the exact minret.
-template <int L>
-__device__ __forceinline__ int pack_closure(ChainLane& ch, const uint64_t* __restrict__ pool, uint32_t& cnt,
+template <int L, class CL>
+__device__ __forceinline__ int pack_closure(CL& ch, const uint64_t* __restrict__ pool, uint32_t& cnt,
                                             const State& s, uint32_t hflags,
                                             uint64_t gmask, uint32_t& minret_out,
                                             unsigned long long* prof_pass = nullptr) {
@@ -300,7 +324,7 @@ __device__ __forceinline__ int pack_closure(ChainLane& ch, const uint64_t* __res
 #ifndef S2LC_PACK_MINW
 #define S2LC_PACK_MINW 1
 #endif
-template <int L>
+template <int L, bool SMALL = false>
 __global__ __launch_bounds__(PACK_BLOCK, S2LC_PACK_MINW) void pack_kernel(Params p) {
 #ifdef S2LC_PROF
   unsigned long long pk_acc[6] = {0, 0, 0, 0, 0, 0};
@@ -345,8 +369,9 @@ __global__ __launch_bounds__(PACK_BLOCK, S2LC_PACK_MINW) void pack_kernel(Params
     uint32_t* const rc = p.rcounts ? p.rcounts + p.res[h].witness_off : nullptr;
     const uint32_t cs = on ? p.chain_start[hd.cs_base + gl] : 0u;
     const uint32_t ce = on ? p.chain_start[hd.cs_base + gl + 1] : 0u;
-    ChainLane ch;
-    ch.reset(p.recs + cs, on, ce - cs);
+    ChainLane<SMALL> ch;
+    if constexpr (SMALL) ch.reset(p.srecs + cs, on, ce - cs);
+    else ch.reset(p.recs + cs, on, ce - cs);
     ch.pool32 = reinterpret_cast<const uint32_t*>(p.pool);
     bool witness_ok = p.witness != 0;
     // the first record hashes of this lane's head in the next round's first

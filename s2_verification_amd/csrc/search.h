@@ -20,6 +20,23 @@ struct HistDesc {
   uint32_t n_ops;
 };
 
+// A history's op record in 32 bytes, for histories whose tails, event
+// indices and per-op hash counts fit 16 bits (HistDesc flag H_SMALL, set at
+// upload): the packed kernels read these (a window of two records is 16
+// registers instead of 32). Values the packed search only compares with
+// reachable tails (msn, out_tail) saturate to 0xFFFF above 65,532, which no
+// reachable tail equals; a P1 bound above 65,532 (never pruning) is 0xFFFD,
+// REQ_HASH_ONLY 0xFFFE, REQ_NONE 0xFFFF; EV_INF is 0xFFFF.
+struct __attribute__((aligned(32))) SRec {
+  uint64_t out_hash;
+  uint32_t hash_off;     // batch-wide pool offset
+  uint16_t num_records, msn, out_tail, suf;
+  uint16_t call_ev, ret_ev, hash_cnt, flags;
+  uint16_t batch_tok, set_tok;
+};
+static_assert(sizeof(SRec) == 32, "SRec is 32 bytes");
+constexpr uint16_t H_SMALL = 0x20;  // HistDesc.flags: the history's SRec table is exact (above)
+
 struct TraceEnt {
   uint32_t parent;  // trace index of the parent configuration
   uint32_t move;    // chain | MOVE_IDENT
@@ -129,6 +146,7 @@ struct DevBatch {
   uint8_t* stage = nullptr;         // pinned host memory
   size_t stage_cap = 0;
   OpRec* recs = nullptr;
+  SRec* srecs = nullptr;            // the same records in 32 bytes (H_SMALL histories; device, filled after the upload)
   uint64_t* pool = nullptr;
   uint32_t* chain_start = nullptr;
   HistDesc* hist = nullptr;
@@ -140,6 +158,8 @@ struct DevBatch {
   uint32_t n_pack8 = 0, n_pack16 = 0, n_pack32 = 0;  // packed-kernel lists (order[]: pack8 | pack16 | pack32)
   uint32_t pack8_kmax = 8;                            // K bound of the pack8 list (0: none)
   int pack_bpc[3] = {0, 0, 0};                        // resident pack_kernel<8/16/32> blocks per CU (0: not queried)
+  int pack_bpc_s[3] = {0, 0, 0};                      // ... of the SRec (H_SMALL) instances
+  bool list_small[3] = {false, false, false};         // every history of the packed list is H_SMALL
   uint64_t n_ops_total = 0;                           // ops over the uploaded histories
   std::vector<uint32_t> lpt;        // searchable histories, longest (n_ops x K) first
   std::vector<uint64_t> h_in_bytes; // per history: input SoA bytes (48 per op + 8 per record hash)
@@ -204,6 +224,7 @@ struct RunStats {
   double pack16_ms = 0;              // pack_kernel<16> launch (HIP events)
   uint64_t pack16_algo_bytes = 0;    // algorithmic bytes of the histories it settled
   uint32_t pack16_histories = 0;
+  uint32_t pack16_small = 0;     // of those: settled by the SRec instance (32-byte records)
   double pack8_ms = 0;               // pack_kernel<8> (K <= 8: every C4 history)
   uint64_t pack8_algo_bytes = 0;
   uint32_t pack8_histories = 0;

@@ -153,6 +153,32 @@ int grow_pinned(uint8_t** p, size_t& cap, size_t need, std::string& err) {
   return 0;
 }
 
+// OpRec -> SRec (search.h): exact for the records of H_SMALL histories
+// (their tails, events and hash counts fit 16 bits); the other records'
+// SRec are never read
+__global__ void srec_kernel(const OpRec* __restrict__ in, SRec* __restrict__ out, uint32_t n) {
+  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const OpRec x = load_rec(in + i);
+  auto sat = [](uint64_t v) -> uint16_t { return v <= 65532u ? (uint16_t)v : (uint16_t)0xFFFFu; };
+  SRec y;
+  y.out_hash = x.out_hash;
+  y.hash_off = x.hash_off;
+  y.num_records = (uint16_t)min<uint64_t>(x.num_records, 0xFFFFu);
+  y.msn = sat(x.msn);
+  y.out_tail = sat(x.out_tail);
+  y.suf = x.sufmin == REQ_NONE ? (uint16_t)0xFFFFu
+        : x.sufmin == REQ_HASH_ONLY ? (uint16_t)0xFFFEu
+        : x.sufmin <= 65532u ? (uint16_t)x.sufmin : (uint16_t)0xFFFDu;
+  y.call_ev = (uint16_t)min(x.call_ev, 0xFFFFu);
+  y.ret_ev = (uint16_t)min(x.ret_ev, 0xFFFFu);
+  y.hash_cnt = (uint16_t)min(x.hash_cnt, 0xFFFFu);
+  y.flags = (uint16_t)x.flags;
+  y.batch_tok = x.batch_tok;
+  y.set_tok = x.set_tok;
+  out[i] = y;
+}
+
 }  // namespace
 
 int batch_upload(DevBatch& b, const std::vector<const History*>& hs, uint32_t red_off, std::string& err) {
@@ -213,7 +239,8 @@ int batch_upload(DevBatch& b, const std::vector<const History*>& hs, uint32_t re
   const size_t o_moves = stage_bytes;
   const size_t o_rc = align256(o_moves + std::max<uint64_t>(moves_total, 1) * sizeof(uint32_t));
   const size_t o_list = align256(o_rc + std::max<uint64_t>(moves_total, 1) * sizeof(uint32_t));
-  const size_t arena_bytes = align256(o_list + std::max<size_t>(n, 1) * sizeof(uint32_t));
+  const size_t o_srec = align256(o_list + std::max<size_t>(n, 1) * sizeof(uint32_t));
+  const size_t arena_bytes = align256(o_srec + (size_t)b.n_recs * sizeof(SRec));
   if (grow_pinned(&b.stage, b.stage_cap, stage_bytes, err)) return S2LC_EHIP;
   if (grow_device(&b.arena, b.arena_cap, arena_bytes, err)) return S2LC_EHIP;
   OpRec* s_recs = reinterpret_cast<OpRec*>(b.stage + o_recs);
@@ -231,6 +258,8 @@ int batch_upload(DevBatch& b, const std::vector<const History*>& hs, uint32_t re
   b.moves = reinterpret_cast<uint32_t*>(b.arena + o_moves);
   b.rcounts = reinterpret_cast<uint32_t*>(b.arena + o_rc);
   b.list = reinterpret_cast<uint32_t*>(b.arena + o_list);
+  b.srecs = reinterpret_cast<SRec*>(b.arena + o_srec);
+  std::atomic<uint32_t> n_small{0};
   // Pack every history into the pinned stage (in parallel: ~0.5 GB for C4).
   // The records and the hash pool (nearly all of the stage) go up in slices
   // of histories as the slices complete: this thread queues each slice's two
@@ -251,11 +280,22 @@ int batch_upload(DevBatch& b, const std::vector<const History*>& hs, uint32_t re
     d.flags = (uint16_t)(h.hflags & ~clear);
     d.n_ops = h.n_ops;
     uint64_t in_bytes = 48ull * h.n_ops;
+    uint64_t tot_nr = 0;  // every reachable tail is at most the sum of the appends' num_records
+    uint32_t max_hc = 0;
     for (const OpRec& r0 : h.recs) {
       OpRec r = r0;
       r.hash_off = (uint32_t)(r0.hash_off + pp);
       in_bytes += 8ull * r0.hash_cnt;
+      if (!(r0.flags & OPF_SENTINEL) && (r0.flags & OPF_KIND_MASK) == S2LC_INPUT_APPEND)
+        tot_nr += std::min<uint64_t>(r0.num_records, 1ull << 32);
+      max_hc = std::max(max_hc, r0.hash_cnt);
       s_recs[pr++] = r;
+    }
+    // the 32-byte records (SRec) are exact for this history
+    if ((d.flags & H_TAIL32) && !h.literal && !h.structural && h.n_events() < 0xFFFFu && tot_nr <= 65532u &&
+        max_hc <= 0xFFFFu) {
+      d.flags |= H_SMALL;
+      n_small.fetch_add(1, std::memory_order_relaxed);
     }
     b.h_in_bytes[i] = in_bytes;
     if (h.chain_start.empty()) s_cs[pc++] = d.rec_base;
@@ -338,9 +378,15 @@ int batch_upload(DevBatch& b, const std::vector<const History*>& hs, uint32_t re
   {
     const uint32_t lim[3] = {b.n_pack8, b.n_pack8 + b.n_pack16, no};
     uint32_t k = 0;
+    const bool small_on = !(getenv("S2LC_PACK_SMALL") && getenv("S2LC_PACK_SMALL")[0] == '0');
     for (int li = 0; li < 3; ++li) {
       b.in_bytes_list[li] = 0;
-      for (; k < lim[li]; ++k) b.in_bytes_list[li] += b.h_in_bytes[s_order[k]];
+      bool all_small = small_on;
+      for (; k < lim[li]; ++k) {
+        b.in_bytes_list[li] += b.h_in_bytes[s_order[k]];
+        all_small = all_small && (b.h_hist[s_order[k]].flags & H_SMALL);
+      }
+      b.list_small[li] = all_small;
     }
   }
   b.h_res_stale = false;
@@ -348,8 +394,14 @@ int batch_upload(DevBatch& b, const std::vector<const History*>& hs, uint32_t re
     HIPCHK(hipMemcpy(b.arena, b.stage, stage_bytes, hipMemcpyHostToDevice));
   } else {  // the rest of the stage after the records and the pool, then wait for every slice
     HIPCHK(hipMemcpyAsync(b.arena + o_cs, b.stage + o_cs, stage_bytes - o_cs, hipMemcpyHostToDevice, 0));
-    HIPCHK(hipStreamSynchronize(0));
   }
+  // the 32-byte records of the H_SMALL histories, from the uploaded ones
+  if (n_small.load() > 0) {
+    hipLaunchKernelGGL(srec_kernel, dim3((uint32_t)((n_recs + 255) / 256)), dim3(256), 0, 0, b.recs, b.srecs,
+                       (uint32_t)n_recs);
+    HIPCHK(hipGetLastError());
+  }
+  HIPCHK(hipStreamSynchronize(0));
   return 0;
 }
 
@@ -451,7 +503,7 @@ int batch_run(DevBatch& b, hipStream_t stream, const RunOpts& ro, RunStats& st, 
 
   Params prm;
   memset(&prm, 0, sizeof prm);
-  prm.recs = b.recs; prm.pool = b.pool; prm.chain_start = b.chain_start; prm.hist = b.hist;
+  prm.recs = b.recs; prm.srecs = b.srecs; prm.pool = b.pool; prm.chain_start = b.chain_start; prm.hist = b.hist;
   prm.trace = b.trace; prm.trace_head = b.trace_head; prm.trace_cap = witness ? b.trace_cap : 0;
   prm.res = b.res; prm.max_configs = ro.max_configs; prm.witness = witness ? 1 : 0;
   prm.moves = b.moves;
@@ -550,14 +602,17 @@ int batch_run(DevBatch& b, hipStream_t stream, const RunOpts& ro, RunStats& st, 
       pp.zero_agg = no_reset && first_launch ? b.agg + 32 * (par ^ 1u) : nullptr;
       const uint32_t L = 8u << li;
       const size_t smem = li == 0 ? pack_smem_bytes<8>() : li == 1 ? pack_smem_bytes<16>() : pack_smem_bytes<32>();
-      int bpc = b.pack_bpc[li];  // resident blocks per CU (queried once per batch)
+      // SMALL: every history of the list reads its 32-byte records (H_SMALL)
+      const bool sm = b.list_small[li];
+      int& bpc_c = sm ? b.pack_bpc_s[li] : b.pack_bpc[li];
+      int bpc = bpc_c;  // resident blocks per CU (queried once per batch)
       if (bpc == 0) {
-        if (li == 0) HIPCHK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&bpc, pack_kernel<8>, PACK_BLOCK, smem));
-        else if (li == 1) HIPCHK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&bpc, pack_kernel<16>, PACK_BLOCK, smem));
-        else HIPCHK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&bpc, pack_kernel<32>, PACK_BLOCK, smem));
+        if (li == 0) HIPCHK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&bpc, sm ? pack_kernel<8, true> : pack_kernel<8>, PACK_BLOCK, smem));
+        else if (li == 1) HIPCHK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&bpc, sm ? pack_kernel<16, true> : pack_kernel<16>, PACK_BLOCK, smem));
+        else HIPCHK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&bpc, sm ? pack_kernel<32, true> : pack_kernel<32>, PACK_BLOCK, smem));
         bpc = std::max(1, bpc);
         if (const char* e = getenv("S2LC_PACK_BPC")) bpc = std::max(1, atoi(e));  // (diagnostics: grid blocks per CU)
-        b.pack_bpc[li] = bpc;
+        bpc_c = bpc;
       }
       // lane groups per wave that take histories: 1 up to half a history per
       // resident wave, 2 up to 2.5, then 4 (x2 per x5). The groups of a wave
@@ -580,9 +635,9 @@ int batch_run(DevBatch& b, hipStream_t stream, const RunOpts& ro, RunStats& st, 
       // around it: with hipEventRecord the launch started 20-30 us after the
       // previous kernel ended, rocprofv3 trace r03a)
       hipEvent_t e0 = b.ev[2 * li], e1 = b.ev[2 * li + 1];
-      if (li == 0) hipExtLaunchKernelGGL(pack_kernel<8>, dim3(grid), dim3(PACK_BLOCK), smem, stream, e0, e1, 0, pp);
-      else if (li == 1) hipExtLaunchKernelGGL(pack_kernel<16>, dim3(grid), dim3(PACK_BLOCK), smem, stream, e0, e1, 0, pp);
-      else hipExtLaunchKernelGGL(pack_kernel<32>, dim3(grid), dim3(PACK_BLOCK), smem, stream, e0, e1, 0, pp);
+      if (li == 0) hipExtLaunchKernelGGL(sm ? pack_kernel<8, true> : pack_kernel<8>, dim3(grid), dim3(PACK_BLOCK), smem, stream, e0, e1, 0, pp);
+      else if (li == 1) hipExtLaunchKernelGGL(sm ? pack_kernel<16, true> : pack_kernel<16>, dim3(grid), dim3(PACK_BLOCK), smem, stream, e0, e1, 0, pp);
+      else hipExtLaunchKernelGGL(sm ? pack_kernel<32, true> : pack_kernel<32>, dim3(grid), dim3(PACK_BLOCK), smem, stream, e0, e1, 0, pp);
       HIPCHK(hipGetLastError());
       if (pp.zero_ctr) b.force_reset = false;
       launched[li] = true;
@@ -629,7 +684,11 @@ int batch_run(DevBatch& b, hipStream_t stream, const RunOpts& ro, RunStats& st, 
         st.algo_bytes += a[PACK_AGG_SEARCH_BYTES];
         // (S2LC_PACK8 lists settle in pack_kernel<8>; the 32-lane list is not a roofline line)
         if (li == 0) { st.pack8_algo_bytes = a[PACK_AGG_SEARCH_BYTES] + b.in_bytes_list[0]; st.pack8_histories = (uint32_t)a[PACK_AGG_SETTLED]; }
-        if (li == 1) { st.pack16_algo_bytes = a[PACK_AGG_SEARCH_BYTES] + b.in_bytes_list[1]; st.pack16_histories = (uint32_t)a[PACK_AGG_SETTLED]; }
+        if (li == 1) {
+          st.pack16_algo_bytes = a[PACK_AGG_SEARCH_BYTES] + b.in_bytes_list[1];
+          st.pack16_histories = (uint32_t)a[PACK_AGG_SETTLED];
+          st.pack16_small = b.list_small[1] ? st.pack16_histories : 0u;
+        }
       }
       st.algo_bytes += b.algo_bytes_inputs;
       b.h_res_stale = true;
@@ -802,6 +861,7 @@ int batch_run(DevBatch& b, hipStream_t stream, const RunOpts& ro, RunStats& st, 
       // pack_kernel<16> alone: its histories' search bytes + their input SoA
       st.pack16_algo_bytes += 2 * S * r.configs + 8 * r.children + b.h_in_bytes[i];
       st.pack16_histories++;
+      if (b.list_small[1]) st.pack16_small++;
     } else if (pack_done[i] == 8) {
       st.pack8_algo_bytes += 2 * S * r.configs + 8 * r.children + b.h_in_bytes[i];
       st.pack8_histories++;

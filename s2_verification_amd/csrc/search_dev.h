@@ -82,6 +82,7 @@ static_assert(sizeof(Cfg<32>) == 112, "cfg32");
 
 struct Params {
   const OpRec* recs;
+  const SRec* srecs;   // the same records in 32 bytes (H_SMALL histories; the packed kernels' SMALL instances)
   const uint64_t* pool;
   const uint32_t* chain_start;
   const HistDesc* hist;

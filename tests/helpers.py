@@ -133,7 +133,11 @@ U64_REGIMES = ("tail32_edge", "above32", "wrap", "zero_hashes")
 def random_history_u64(rng: random.Random, n_ops: int, n_clients: int = 3, regime: str = "tail32_edge",
                        p_perturb: float = 0.15, tokens=("aaaaaa", "bbbbbb")):
     """A random small history over the u64 edges of s2Model.Step
-    (main.go:264-335), the bug class main_test.go:313-343 pins:
+    (main.go:264-335), the bug class main_test.go:313-343 pins, and over the
+    16-bit fields of the packed kernels' 32-byte records ("small_edge": the
+    first append leaves the tail at 65,520 .. 65,532, later appends carry
+    65,535 .. 65,537 records now and then, match_seq_num = tail +- 2^16 and
+    0xFFFD .. 0x10000, success tails perturbed by +-2^16):
 
       - num_records drawn independently of the record-hash count (expressible
         only through the event API, main_test.go:322);
@@ -171,6 +175,10 @@ def random_history_u64(rng: random.Random, n_ops: int, n_clients: int = 3, regim
                                    (1 << 63) - rng.randint(0, 3)])
             elif regime == "zero_hashes" and rng.random() < 0.5:
                 nrec, nh = 0, rng.randint(1, 2)
+            elif regime == "small_edge" and first_append:
+                nrec = 65532 - rng.randint(0, 12)
+            elif regime == "small_edge" and rng.random() < 0.08:
+                nrec = rng.choice([65535, 65536, 65537])
             elif nrec == 0 and regime != "zero_hashes" and rng.random() < 0.9:
                 nh = 0  # (keep P2 on in most histories of the other regimes)
             first_append = False
@@ -178,7 +186,12 @@ def random_history_u64(rng: random.Random, n_ops: int, n_clients: int = 3, regim
             set_tok = rng.choice(tokens) if rng.random() < 0.15 else None
             batch_tok = rng.choice(tokens) if rng.random() < 0.15 else None
             msn = None
-            if rng.random() < 0.4:
+            if rng.random() >= 0.4:
+                pass
+            elif regime == "small_edge":
+                msn = rng.choice([tail, tail, tail + 65536, (tail - 65536) & M64, tail + 1, (tail - 1) & M64,
+                                  0xFFFD, 0xFFFE, 0xFFFF, 0x10000])
+            else:
                 msn = rng.choice([tail, tail, (tail + (1 << 32)) & M64, (tail - (1 << 32)) & M64,
                                   (tail + 1) & M64, (tail - 1) & M64])
             guards = (batch_tok is None or batch_tok == tok) and (msn is None or msn == tail)
@@ -215,7 +228,8 @@ def random_history_u64(rng: random.Random, n_ops: int, n_clients: int = 3, regim
                 out = {"failure": False, "definite_failure": False, "tail": tail, "stream_hash": None}
         if rng.random() < p_perturb:
             if out["tail"] is not None and rng.random() < 0.6:
-                out["tail"] = (out["tail"] + rng.choice([-1, 1, 1 << 32, -(1 << 32)])) & M64
+                d = [-1, 1, 65536, -65536] if regime == "small_edge" else [-1, 1, 1 << 32, -(1 << 32)]
+                out["tail"] = (out["tail"] + rng.choice(d)) & M64
             elif out["stream_hash"] is not None:
                 out["stream_hash"] ^= 1 << rng.randrange(64)
             elif out["failure"] and kind == "append":

@@ -27,7 +27,7 @@ import pytest
 
 import oracle as orc
 import s2_verification_amd as s2
-from helpers import (U64_REGIMES, config_digest, golden, hard_variant, random_history_u64, to_s2_events,
+from helpers import (U64_REGIMES, _fold, config_digest, golden, hard_variant, random_history_u64, to_s2_events,
                      u64_regime)
 
 pytestmark = pytest.mark.gpu
@@ -182,3 +182,81 @@ def test_h174_u64_variants(variant, mode, monkeypatch):
         assert st["level_solo_rounds"] == 0, st
     else:
         assert st["level_solo_rounds"] > r.rounds // 2, st
+
+
+def _small_edge_cases():
+    """~600 small histories around the 16-bit fields of the 32-byte records
+    (regime "small_edge"), brute force = WGL, split by whether the host packs
+    them as H_SMALL (every append's num_records summed <= 65,532)."""
+    if "small_edge" not in _cases:
+        rng = random.Random(65532)
+        sm, big = ([], []), ([], [])
+        for _ in range(600):
+            ev = random_history_u64(rng, rng.randint(1, 9), n_clients=rng.randint(1, 4), regime="small_edge")
+            w, _ = orc.check_wgl(ev)
+            assert orc.check_brute(ev)[0] == w
+            tot = sum(min(e["num_records"], 1 << 32) for e in ev if e["kind"] == "call" and e["input_type"] == 0)
+            dst = sm if tot <= 65532 else big
+            dst[0].append(ev)
+            dst[1].append(w)
+        _cases["small_edge"] = (sm, big)
+    return _cases["small_edge"]
+
+
+def _sequential_appends(n_ops, bad_last):
+    """One client, n_ops appends of one record in a row (tails 1..n_ops); the
+    last return off by one when bad_last."""
+    evs = []
+    for i in range(n_ops):
+        evs.append(s2.Event(s2.CallEvent, s2.StreamInput(InputType=0, NumRecords=1, RecordHashes=[]), i, 0))
+        evs.append(s2.Event(s2.ReturnEvent, s2.StreamOutput(Tail=i + 1 + (1 if bad_last and i == n_ops - 1 else 0)),
+                            i, 0))
+    return s2.History.from_events(evs)
+
+
+def _hash_count_history(n_hashes, bad):
+    """An append of n_hashes record hashes, then a read of the folded hash
+    (a bit flipped when bad): oracle dict events."""
+    rng = random.Random(n_hashes)
+    hs = [rng.getrandbits(64) for _ in range(n_hashes)]
+    ev = [{"kind": "call", "op_id": 0, "client_id": 0, "input_type": 0, "num_records": 2, "record_hashes": hs,
+           "set_fencing_token": None, "fencing_token": None, "match_seq_num": None},
+          {"kind": "return", "op_id": 0, "client_id": 0, "failure": False, "definite_failure": False, "tail": 2,
+           "stream_hash": None},
+          {"kind": "call", "op_id": 1, "client_id": 1, "input_type": 1},
+          {"kind": "return", "op_id": 1, "client_id": 1, "failure": False, "definite_failure": False, "tail": 2,
+           "stream_hash": None}]
+    ev[3]["stream_hash"] = _fold(0, hs) ^ (1 if bad else 0)
+    return ev
+
+
+@pytest.mark.parametrize("small", ["1", "0"])
+def test_small_records_at_their_bounds(small, monkeypatch):
+    """The packed kernels' 32-byte records (csrc/search.h SRec: 16-bit
+    num_records, match_seq_num, tails, event indices and hash counts,
+    saturating) against brute force / WGL at their bounds: random histories
+    whose tails end at 65,520 .. 65,537 with match_seq_num = tail +- 2^16 and
+    0xFFFD .. 0x10000 (a batch of H_SMALL histories and a batch of the rest),
+    65,534 / 65,536 events, 65,535 / 65,536 hashes on one append. With
+    S2LC_PACK_SMALL=0 every list takes the 64-byte records: same verdicts."""
+    monkeypatch.setenv("S2LC_PACK_SMALL", small)
+    sm, big = _small_edge_cases()
+    assert len(sm[0]) > 100 and len(big[0]) > 100 and {"Ok", "Illegal"} <= set(sm[1]) and {"Ok", "Illegal"} <= set(big[1])
+    b, _ = _check("auto", *sm)
+    st = b.stats()
+    assert st["pack16_histories"] == len(sm[0]), st
+    assert st["pack16_small"] == (len(sm[0]) if small == "1" else 0), st
+    b, _ = _check("auto", *big)
+    assert b.stats()["pack16_small"] == 0
+    # event indices: 65,534 events fit (0xFFFF is "never"), 65,536 do not
+    for n_ops, want_small in ((32767, True), (32768, False)):
+        hs = [_sequential_appends(n_ops, False), _sequential_appends(n_ops, True)]
+        b = s2.Checker().batch(hs)
+        assert [r.verdict for r in b.check()] == [s2.Ok, s2.Illegal]
+        assert b.stats()["pack16_small"] == (2 if want_small and small == "1" else 0), (n_ops, b.stats())
+    # hash counts: 65,535 fit in the 16-bit count, 65,536 do not
+    for n, want_small in ((65535, True), (65536, False)):
+        evs = [_hash_count_history(n, False), _hash_count_history(n, True)]
+        assert [orc.check_wgl(ev)[0] for ev in evs] == [s2.Ok, s2.Illegal]
+        b, _ = _check("auto", evs, [s2.Ok, s2.Illegal])
+        assert b.stats()["pack16_small"] == (2 if want_small and small == "1" else 0), (n, b.stats())
