@@ -28,7 +28,7 @@ def kname(n):
         if k == base:
             return k
         arg = k[len(base) + 1:-1]
-        if f"<{arg}>" in n or f"ILi{arg}E" in n:
+        if f"<{arg}>" in n or f"<{arg}," in n or f"ILi{arg}E" in n:
             return k
     m = re.search(r"(\w+_kernel|lv_\w+)", n)
     return m.group(1) if m else n[:40]

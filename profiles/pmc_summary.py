@@ -13,6 +13,7 @@ import csv
 import glob
 import json
 import os
+import re
 import sys
 from collections import defaultdict
 
@@ -20,15 +21,23 @@ sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
 from kernel_digest import src_digest  # noqa: E402
 
 
-def per_dispatch(d, counter, kernel):
+def canonical(name):
+    """pack_kernel<16, true> (the 32-byte-record instance, search.h SRec) and
+    pack_kernel<16, false> are both the bench's pack_kernel<16>."""
+    return re.sub(r", (true|false)>", ">", name)
+
+
+def per_dispatch(d, counter, kernel, seen):
     vals = defaultdict(float)
     for path in glob.glob(os.path.join(d, "**", "*counter_collection.csv"), recursive=True):
         with open(path) as f:
             for row in csv.DictReader(f):
-                if kernel not in row.get("Kernel_Name", ""):
+                name = row.get("Kernel_Name", "")
+                if kernel not in canonical(name):
                     continue
                 if row.get("Counter_Name") != counter:
                     continue
+                seen.add(name)
                 vals[row.get("Dispatch_Id")] += float(row.get("Counter_Value", 0))
     return list(vals.values())
 
@@ -41,14 +50,16 @@ def main():
         with open(sys.argv[5]) as fh:
             line = [x for x in fh if x.startswith("{")][-1]
         hist = json.loads(line)["roofline"]["histories_per_launch"]
-    fetch = per_dispatch(fetch_dir, "FETCH_SIZE", kernel)
-    write = per_dispatch(write_dir, "WRITE_SIZE", kernel)
+    seen = set()
+    fetch = per_dispatch(fetch_dir, "FETCH_SIZE", kernel, seen)
+    write = per_dispatch(write_dir, "WRITE_SIZE", kernel, seen)
     if not fetch or not write:
         raise SystemExit(f"no {kernel} counters found (fetch={len(fetch)}, write={len(write)})")
     f = sum(fetch) / len(fetch)
     w = sum(write) / len(write)
     res = {
         "kernel": kernel,
+        "instances": sorted(seen),
         "dispatches": {"fetch_pass": len(fetch), "write_pass": len(write)},
         "FETCH_SIZE_KiB": f, "WRITE_SIZE_KiB": w,
         "hbm_bytes_per_launch": int((2 * f + w) * 1024),

@@ -615,17 +615,20 @@ int batch_run(DevBatch& b, hipStream_t stream, const RunOpts& ro, RunStats& st, 
         bpc_c = bpc;
       }
       // lane groups per wave that take histories: 1 up to half a history per
-      // resident wave, 2 up to 2.5, then 4 (x2 per x5). The groups of a wave
+      // resident wave, 2 up to 4, then 4 (x2 per x8). The groups of a wave
       // run in lockstep, so fewer per wave give shorter rounds; more groups
       // per wave issue one instruction stream for several histories, which
-      // wins once the SIMDs are shared. C4 sweep with the expand-time P1
-      // precheck (tools/gpw_sweep.sh, profiles/r04/gpw_sweep.txt), ms at
-      // 1 / 2 / 4 groups: 1,000 histories 0.97 / 1.10 / 1.26; 2,500 1.53 /
-      // 1.10 / 1.27; 6,000 1.90 / 1.28 / 1.34; 10,000 2.38 / 1.63 / 1.35.
+      // wins once the SIMDs are shared. C4 sweeps (tools/gpw_sweep.sh), ms at
+      // 1 / 2 / 4 groups. 64-byte records, 2 blocks per CU (2,048 waves;
+      // profiles/r04/gpw_sweep.txt): 1,000 histories 0.97 / 1.10 / 1.26;
+      // 2,500 1.53 / 1.10 / 1.27; 6,000 1.90 / 1.28 / 1.34; 10,000 2.38 /
+      // 1.63 / 1.35. 32-byte records, 3 blocks per CU (3,072 waves;
+      // profiles/r05/gpw_sweep_srec.txt): 1,000 0.92 / 1.01 / 1.16; 4,000
+      // 1.30 / 0.98 / 1.12; 10,000 1.66 / 1.09 / 1.18.
       const uint32_t gpw_all = 64 / L;
       const uint64_t waves = (uint64_t)n_cu * (uint64_t)bpc * (PACK_BLOCK / 64);
       uint32_t gpw = 1;
-      for (uint64_t lim2 = 1; gpw < gpw_all && (uint64_t)n_l * 2 > waves * lim2; lim2 *= 5) gpw *= 2;
+      for (uint64_t lim2 = 1; gpw < gpw_all && (uint64_t)n_l * 2 > waves * lim2; lim2 *= 8) gpw *= 2;
       if (const char* e = getenv("S2LC_PACK_GPW")) gpw = std::max<uint32_t>(1, std::min<uint32_t>(gpw_all, (uint32_t)atoi(e)));
       pp.gpw = gpw < gpw_all ? gpw : 0u;
       const uint32_t groups = (PACK_BLOCK / 64) * gpw;
@@ -697,7 +700,8 @@ int batch_run(DevBatch& b, hipStream_t stream, const RunOpts& ro, RunStats& st, 
       if (step_timing)
         fprintf(stderr, "[s2lc step] enqueue %.1f us, wait %.1f us (kernel %.1f us), after %.1f us (totals only); "
                 "pack16 blocks/CU %d\n",
-                1e-3 * (t_enq - t0), 1e-3 * (t_wait - t_enq), 1e3 * st.pack_ms, 1e-3 * (t_end - t_wait), b.pack_bpc[1]);
+                1e-3 * (t_enq - t0), 1e-3 * (t_wait - t_enq), 1e3 * st.pack_ms, 1e-3 * (t_end - t_wait),
+                b.list_small[1] ? b.pack_bpc_s[1] : b.pack_bpc[1]);
       return 0;
     }
     if (fast)  // a packed frontier overflowed: the full path needs every result
