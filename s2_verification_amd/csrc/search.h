@@ -37,6 +37,49 @@ struct __attribute__((aligned(32))) SRec {
 static_assert(sizeof(SRec) == 32, "SRec is 32 bytes");
 constexpr uint16_t H_SMALL = 0x20;  // HistDesc.flags: the history's SRec table is exact (above)
 
+// OpRec -> SRec (the host packs H_SMALL histories' records in this form)
+inline SRec to_srec(const OpRec& x) {
+  auto sat = [](uint64_t v) -> uint16_t { return v <= 65532u ? (uint16_t)v : (uint16_t)0xFFFFu; };
+  SRec y;
+  y.out_hash = x.out_hash;
+  y.hash_off = x.hash_off;
+  y.num_records = (uint16_t)(x.num_records < 0xFFFFu ? x.num_records : 0xFFFFu);
+  y.msn = sat(x.msn);
+  y.out_tail = sat(x.out_tail);
+  y.suf = x.sufmin == REQ_NONE ? (uint16_t)0xFFFFu
+        : x.sufmin == REQ_HASH_ONLY ? (uint16_t)0xFFFEu
+        : x.sufmin <= 65532u ? (uint16_t)x.sufmin : (uint16_t)0xFFFDu;
+  y.call_ev = (uint16_t)(x.call_ev < 0xFFFFu ? x.call_ev : 0xFFFFu);
+  y.ret_ev = (uint16_t)(x.ret_ev < 0xFFFFu ? x.ret_ev : 0xFFFFu);
+  y.hash_cnt = (uint16_t)(x.hash_cnt < 0xFFFFu ? x.hash_cnt : 0xFFFFu);
+  y.flags = (uint16_t)x.flags;
+  y.batch_tok = x.batch_tok;
+  y.set_tok = x.set_tok;
+  return y;
+}
+
+// SRec -> OpRec (on the device, for the engines that read 64-byte records).
+// Not bit-exact where SRec saturates, but equal in every comparison the
+// search makes for an H_SMALL history: a saturated msn / out_tail (0xFFFF)
+// equals no reachable tail, as the original did not, and a P1 bound of
+// 0xFFFD passes every reachable tail, as the original did.
+__host__ __device__ inline OpRec from_srec(const SRec& y) {
+  OpRec x;
+  x.num_records = y.num_records;
+  x.msn = y.msn;
+  x.out_tail = y.out_tail;
+  x.out_hash = y.out_hash;
+  x.sufmin = y.suf == 0xFFFFu ? REQ_NONE : y.suf == 0xFFFEu ? REQ_HASH_ONLY : (uint64_t)y.suf;
+  x.call_ev = y.call_ev == 0xFFFFu ? EV_INF : y.call_ev;
+  x.ret_ev = y.ret_ev == 0xFFFFu ? EV_INF : y.ret_ev;
+  x.hash_off = y.hash_off;
+  x.hash_cnt = y.hash_cnt;
+  x.batch_tok = y.batch_tok;
+  x.set_tok = y.set_tok;
+  x.flags = y.flags;
+  return x;
+}
+
 struct TraceEnt {
   uint32_t parent;  // trace index of the parent configuration
   uint32_t move;    // chain | MOVE_IDENT
@@ -134,8 +177,11 @@ struct LevelStats {
 // A batch of histories resident on one device. Every buffer is grown on
 // demand and reused by later uploads/runs (a context's scratch batch serves
 // s2lc_check with no device allocation once it is large enough):
-//   device arena : recs | pool | chain_start | hist | order | res | moves | rcounts | list
-//   pinned stage : recs | pool | chain_start | hist | order | res   (one H2D copy)
+//   device arena : recs | srecs | pool | chain_start | hist | order | res | moves | rcounts | list
+//   pinned stage : recs | srecs | pool | chain_start | hist | order | res   (the uploaded prefix)
+// An H_SMALL history's records are packed and uploaded as SRec only (half
+// the bytes); a device kernel widens them into recs for the other engines.
+// Every other history's records go up as OpRec; its srecs are never read.
 struct DevBatch {
   int device = 0;
   uint32_t n_hist = 0;
@@ -146,7 +192,7 @@ struct DevBatch {
   uint8_t* stage = nullptr;         // pinned host memory
   size_t stage_cap = 0;
   OpRec* recs = nullptr;
-  SRec* srecs = nullptr;            // the same records in 32 bytes (H_SMALL histories; device, filled after the upload)
+  SRec* srecs = nullptr;            // the same records in 32 bytes (H_SMALL histories: uploaded as such)
   uint64_t* pool = nullptr;
   uint32_t* chain_start = nullptr;
   HistDesc* hist = nullptr;

@@ -153,30 +153,27 @@ int grow_pinned(uint8_t** p, size_t& cap, size_t need, std::string& err) {
   return 0;
 }
 
-// OpRec -> SRec (search.h): exact for the records of H_SMALL histories
-// (their tails, events and hash counts fit 16 bits); the other records'
-// SRec are never read
-__global__ void srec_kernel(const OpRec* __restrict__ in, SRec* __restrict__ out, uint32_t n) {
-  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= n) return;
-  const OpRec x = load_rec(in + i);
-  auto sat = [](uint64_t v) -> uint16_t { return v <= 65532u ? (uint16_t)v : (uint16_t)0xFFFFu; };
-  SRec y;
-  y.out_hash = x.out_hash;
-  y.hash_off = x.hash_off;
-  y.num_records = (uint16_t)min<uint64_t>(x.num_records, 0xFFFFu);
-  y.msn = sat(x.msn);
-  y.out_tail = sat(x.out_tail);
-  y.suf = x.sufmin == REQ_NONE ? (uint16_t)0xFFFFu
-        : x.sufmin == REQ_HASH_ONLY ? (uint16_t)0xFFFEu
-        : x.sufmin <= 65532u ? (uint16_t)x.sufmin : (uint16_t)0xFFFDu;
-  y.call_ev = (uint16_t)min(x.call_ev, 0xFFFFu);
-  y.ret_ev = (uint16_t)min(x.ret_ev, 0xFFFFu);
-  y.hash_cnt = (uint16_t)min(x.hash_cnt, 0xFFFFu);
-  y.flags = (uint16_t)x.flags;
-  y.batch_tok = x.batch_tok;
-  y.set_tok = x.set_tok;
-  out[i] = y;
+// The 64-byte records of the H_SMALL histories, from their uploaded SRec
+// (search.h from_srec): one block per history at a time
+__global__ void widen_kernel(const HistDesc* __restrict__ hist, const SRec* __restrict__ in, OpRec* __restrict__ out,
+                             uint32_t n_hist, uint32_t n_recs) {
+  for (uint32_t i = blockIdx.x; i < n_hist; i += gridDim.x) {
+    const HistDesc d = hist[i];
+    if (!(d.flags & H_SMALL)) continue;
+    const uint32_t end = i + 1 < n_hist ? hist[i + 1].rec_base : n_recs;
+    for (uint32_t r = d.rec_base + threadIdx.x; r < end; r += blockDim.x) {
+      const uint4* q = reinterpret_cast<const uint4*>(in + r);
+      SRec y;
+      uint4 w[2] = {q[0], q[1]};
+      __builtin_memcpy(&y, w, sizeof(SRec));
+      const OpRec x = from_srec(y);
+      uint4 o[4];
+      __builtin_memcpy(o, &x, sizeof(OpRec));
+      uint4* dst = reinterpret_cast<uint4*>(out + r);
+#pragma unroll
+      for (int k = 0; k < 4; ++k) dst[k] = o[k];
+    }
+  }
 }
 
 }  // namespace
@@ -230,7 +227,8 @@ int batch_upload(DevBatch& b, const std::vector<const History*>& hs, uint32_t re
   b.n_pool = (uint32_t)std::max<size_t>(n_pool, 1);
   // layout (stage = the uploaded prefix of the arena)
   const size_t o_recs = 0;
-  const size_t o_pool = align256(o_recs + b.n_recs * sizeof(OpRec));
+  const size_t o_srec = align256(o_recs + b.n_recs * sizeof(OpRec));
+  const size_t o_pool = align256(o_srec + (size_t)b.n_recs * sizeof(SRec));
   const size_t o_cs = align256(o_pool + b.n_pool * sizeof(uint64_t));
   const size_t o_hist = align256(o_cs + std::max<size_t>(n_cs, 1) * sizeof(uint32_t));
   const size_t o_order = align256(o_hist + std::max<size_t>(n, 1) * sizeof(HistDesc));
@@ -239,11 +237,11 @@ int batch_upload(DevBatch& b, const std::vector<const History*>& hs, uint32_t re
   const size_t o_moves = stage_bytes;
   const size_t o_rc = align256(o_moves + std::max<uint64_t>(moves_total, 1) * sizeof(uint32_t));
   const size_t o_list = align256(o_rc + std::max<uint64_t>(moves_total, 1) * sizeof(uint32_t));
-  const size_t o_srec = align256(o_list + std::max<size_t>(n, 1) * sizeof(uint32_t));
-  const size_t arena_bytes = align256(o_srec + (size_t)b.n_recs * sizeof(SRec));
+  const size_t arena_bytes = align256(o_list + std::max<size_t>(n, 1) * sizeof(uint32_t));
   if (grow_pinned(&b.stage, b.stage_cap, stage_bytes, err)) return S2LC_EHIP;
   if (grow_device(&b.arena, b.arena_cap, arena_bytes, err)) return S2LC_EHIP;
   OpRec* s_recs = reinterpret_cast<OpRec*>(b.stage + o_recs);
+  SRec* s_srecs = reinterpret_cast<SRec*>(b.stage + o_srec);
   uint64_t* s_pool = reinterpret_cast<uint64_t*>(b.stage + o_pool);
   uint32_t* s_cs = reinterpret_cast<uint32_t*>(b.stage + o_cs);
   b.h_hist = reinterpret_cast<HistDesc*>(b.stage + o_hist);
@@ -268,7 +266,16 @@ int batch_upload(DevBatch& b, const std::vector<const History*>& hs, uint32_t re
   const size_t n_sl = n >= 2048 ? 16 : 1;
   const size_t sl_len = (n + n_sl - 1) / std::max<size_t>(n_sl, 1);
   std::unique_ptr<std::atomic<uint32_t>[]> sl_left(new std::atomic<uint32_t>[n_sl]);
-  for (size_t k = 0; k < n_sl; ++k) sl_left[k] = (uint32_t)(std::min(n, (k + 1) * sl_len) - std::min(n, k * sl_len));
+  // per slice: histories packed as SRec / as OpRec (which record ranges go up)
+  std::unique_ptr<std::atomic<uint32_t>[]> sl_small(new std::atomic<uint32_t>[n_sl]);
+  std::unique_ptr<std::atomic<uint32_t>[]> sl_big(new std::atomic<uint32_t>[n_sl]);
+  for (size_t k = 0; k < n_sl; ++k) {
+    sl_left[k] = (uint32_t)(std::min(n, (k + 1) * sl_len) - std::min(n, k * sl_len));
+    sl_small[k] = 0;
+    sl_big[k] = 0;
+  }
+  // S2LC_PACK_SMALL=0: every history as OpRec, the packed kernels' 64-byte instances
+  const bool small_on = !(getenv("S2LC_PACK_SMALL") && getenv("S2LC_PACK_SMALL")[0] == '0');
   auto pack_one = [&](size_t i) {
     const History& h = *hs[i];
     HistDesc& d = b.h_hist[i];
@@ -283,19 +290,30 @@ int batch_upload(DevBatch& b, const std::vector<const History*>& hs, uint32_t re
     uint64_t tot_nr = 0;  // every reachable tail is at most the sum of the appends' num_records
     uint32_t max_hc = 0;
     for (const OpRec& r0 : h.recs) {
-      OpRec r = r0;
-      r.hash_off = (uint32_t)(r0.hash_off + pp);
       in_bytes += 8ull * r0.hash_cnt;
       if (!(r0.flags & OPF_SENTINEL) && (r0.flags & OPF_KIND_MASK) == S2LC_INPUT_APPEND)
         tot_nr += std::min<uint64_t>(r0.num_records, 1ull << 32);
       max_hc = std::max(max_hc, r0.hash_cnt);
-      s_recs[pr++] = r;
     }
-    // the 32-byte records (SRec) are exact for this history
-    if ((d.flags & H_TAIL32) && !h.literal && !h.structural && h.n_events() < 0xFFFFu && tot_nr <= 65532u &&
-        max_hc <= 0xFFFFu) {
+    // the 32-byte records (SRec) are exact for this history: packed and
+    // uploaded as such (widened on the device), else as OpRec
+    if (small_on && (d.flags & H_TAIL32) && !h.literal && !h.structural && h.n_events() < 0xFFFFu &&
+        tot_nr <= 65532u && max_hc <= 0xFFFFu) {
       d.flags |= H_SMALL;
       n_small.fetch_add(1, std::memory_order_relaxed);
+      sl_small[i / sl_len].store(1, std::memory_order_relaxed);
+      for (const OpRec& r0 : h.recs) {
+        SRec y = to_srec(r0);
+        y.hash_off = (uint32_t)(r0.hash_off + pp);
+        s_srecs[pr++] = y;
+      }
+    } else {
+      sl_big[i / sl_len].store(1, std::memory_order_relaxed);
+      for (const OpRec& r0 : h.recs) {
+        OpRec r = r0;
+        r.hash_off = (uint32_t)(r0.hash_off + pp);
+        s_recs[pr++] = r;
+      }
     }
     b.h_in_bytes[i] = in_bytes;
     if (h.chain_start.empty()) s_cs[pc++] = d.rec_base;
@@ -318,9 +336,12 @@ int batch_upload(DevBatch& b, const std::vector<const History*>& hs, uint32_t re
       if (i0 >= i1 || ce != hipSuccess) continue;
       const size_t r0 = off_rec[i0], r1 = i1 < n ? off_rec[i1] : n_recs;
       const size_t p0 = off_pool[i0], p1 = i1 < n ? off_pool[i1] : n_pool;
-      if (r1 > r0)
+      if (r1 > r0 && sl_big[k].load(std::memory_order_relaxed))
         ce = hipMemcpyAsync(b.arena + o_recs + r0 * sizeof(OpRec), b.stage + o_recs + r0 * sizeof(OpRec),
                             (r1 - r0) * sizeof(OpRec), hipMemcpyHostToDevice, 0);
+      if (ce == hipSuccess && r1 > r0 && sl_small[k].load(std::memory_order_relaxed))
+        ce = hipMemcpyAsync(b.arena + o_srec + r0 * sizeof(SRec), b.stage + o_srec + r0 * sizeof(SRec),
+                            (r1 - r0) * sizeof(SRec), hipMemcpyHostToDevice, 0);
       if (ce == hipSuccess && p1 > p0)
         ce = hipMemcpyAsync(b.arena + o_pool + p0 * sizeof(uint64_t), b.stage + o_pool + p0 * sizeof(uint64_t),
                             (p1 - p0) * sizeof(uint64_t), hipMemcpyHostToDevice, 0);
@@ -378,10 +399,9 @@ int batch_upload(DevBatch& b, const std::vector<const History*>& hs, uint32_t re
   {
     const uint32_t lim[3] = {b.n_pack8, b.n_pack8 + b.n_pack16, no};
     uint32_t k = 0;
-    const bool small_on = !(getenv("S2LC_PACK_SMALL") && getenv("S2LC_PACK_SMALL")[0] == '0');
     for (int li = 0; li < 3; ++li) {
       b.in_bytes_list[li] = 0;
-      bool all_small = small_on;
+      bool all_small = k < lim[li];
       for (; k < lim[li]; ++k) {
         b.in_bytes_list[li] += b.h_in_bytes[s_order[k]];
         all_small = all_small && (b.h_hist[s_order[k]].flags & H_SMALL);
@@ -395,10 +415,10 @@ int batch_upload(DevBatch& b, const std::vector<const History*>& hs, uint32_t re
   } else {  // the rest of the stage after the records and the pool, then wait for every slice
     HIPCHK(hipMemcpyAsync(b.arena + o_cs, b.stage + o_cs, stage_bytes - o_cs, hipMemcpyHostToDevice, 0));
   }
-  // the 32-byte records of the H_SMALL histories, from the uploaded ones
+  // the 64-byte records of the H_SMALL histories, from their uploaded SRec
   if (n_small.load() > 0) {
-    hipLaunchKernelGGL(srec_kernel, dim3((uint32_t)((n_recs + 255) / 256)), dim3(256), 0, 0, b.recs, b.srecs,
-                       (uint32_t)n_recs);
+    hipLaunchKernelGGL(widen_kernel, dim3((uint32_t)std::min<size_t>(n, 4096)), dim3(256), 0, 0, b.hist, b.srecs,
+                       b.recs, (uint32_t)n, (uint32_t)n_recs);
     HIPCHK(hipGetLastError());
   }
   HIPCHK(hipStreamSynchronize(0));

@@ -248,6 +248,10 @@ def test_small_records_at_their_bounds(small, monkeypatch):
     assert st["pack16_small"] == (len(sm[0]) if small == "1" else 0), st
     b, _ = _check("auto", *big)
     assert b.stats()["pack16_small"] == 0
+    # the other engines read the 64-byte records widened on the device from
+    # the uploaded 32-byte ones (search.h from_srec)
+    for engine in ("workgroup", "level"):
+        _check(engine, *sm)
     # event indices: 65,534 events fit (0xFFFF is "never"), 65,536 do not
     for n_ops, want_small in ((32767, True), (32768, False)):
         hs = [_sequential_appends(n_ops, False), _sequential_appends(n_ops, True)]
@@ -260,3 +264,30 @@ def test_small_records_at_their_bounds(small, monkeypatch):
         assert [orc.check_wgl(ev)[0] for ev in evs] == [s2.Ok, s2.Illegal]
         b, _ = _check("auto", evs, [s2.Ok, s2.Illegal])
         assert b.stats()["pack16_small"] == (2 if want_small and small == "1" else 0), (n, b.stats())
+
+
+@pytest.mark.parametrize("small", ["1", "0"])
+def test_small_records_in_sliced_uploads(small, monkeypatch):
+    """Batches of >= 2,048 histories are packed and uploaded in 16 slices,
+    each slice's records as SRec (H_SMALL histories) and / or OpRec (the
+    rest). A batch mixing both (2,400 histories, the small_edge cases four
+    times, interleaved) runs the packed kernels' 64-byte instance, which reads
+    the small histories' widened records; an all-small batch runs the 32-byte
+    instance. Verdicts against brute force / WGL, every engine forced."""
+    monkeypatch.setenv("S2LC_PACK_SMALL", small)
+    sm, big = _small_edge_cases()
+    evs, want = [], []
+    for _ in range(4):
+        for i in range(max(len(sm[0]), len(big[0]))):
+            for src in (sm, big):
+                if i < len(src[0]):
+                    evs.append(src[0][i])
+                    want.append(src[1][i])
+    assert len(evs) >= 2048
+    for engine in ("auto", "workgroup", "level"):
+        b, _ = _check(engine, evs, want)
+        if engine == "auto":
+            assert b.stats()["pack16_small"] == 0
+    evs_s, want_s = sm[0] * 6, sm[1] * 6
+    b, _ = _check("auto", evs_s, want_s)
+    assert b.stats()["pack16_small"] == (len(evs_s) if small == "1" else 0)
