@@ -75,3 +75,23 @@ def test_bench_two_gloo_ranks_on_one_gpu():
         assert leg["single_gpu_verdict"] == hard[name]["verdict"], (name, leg)
         assert leg["single_gpu_seconds"] > 0 and leg["speedup"] > 0, (name, leg)
         assert abs(leg["speedup"] - leg["single_gpu_seconds"] / leg["seconds"]) < 0.01 * leg["speedup"] + 1e-3
+
+
+@pytest.mark.gpu
+def test_bench_watchdog_keeps_the_c4_line():
+    """A multi-GPU leg that stalls must not cost the C4 line: with a watchdog
+    budget far below the legs' time, every rank ends itself and rank 0 prints
+    the line with the legs finished so far (the C4 measurement) and a
+    `watchdog` note, exit status 0."""
+    import random
+    port = random.randint(20000, 40000)
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
+           "--master-addr", "127.0.0.1", "--master-port", str(port), os.path.join(ROOT, "bench.py"),
+           "--gpus", "2", "--steps", "2", "--warmup", "1", "--no-e2e", "--c5-reps", "1"]
+    env = dict(os.environ, S2LC_BENCH_GLOO="1", S2LC_BENCH_WATCHDOG="0.05")
+    p = subprocess.run(cmd, capture_output=True, text=True, timeout=600, cwd=ROOT, env=env)
+    assert p.returncode == 0, p.stderr[-4000:]
+    lines = [x for x in p.stdout.splitlines() if x.startswith("{")]
+    assert len(lines) == 1, p.stdout[-2000:]
+    d = json.loads(lines[0])
+    assert "watchdog" in d and d["n_gpus"] == 2 and d["value"] > 0 and d["verdicts"]["Unknown"] == 0, d
