@@ -1523,11 +1523,16 @@ __global__ __launch_bounds__(LV_BLOCK) void lv_insert(LvParams p) {
     n += (uint32_t)__popcll(bw & ((1ull << lane) - 1));
     __syncthreads();  // s_wcnt / s_base are rewritten next iteration
     if (win) {
-      if (n < p.scap) p.nxt_idx[n] = k;  // (beyond: the close stops the run, lv_xclose)
+      // An exchanged round inserts its whole local share plus the received
+      // blocks, so n can pass scap. Winners there are dropped: the close stops
+      // the run (lv_xclose), and the witness cutoff (tnext + scap <= trace_cap)
+      // only covers n < scap, so no index or trace entry is written for them.
+      const bool kept = n < p.scap;
+      if (kept) p.nxt_idx[n] = k;
       c->slot = slot;
       if (wit) {
-        c->trace = p.tgid + tbase + n;
-        p.trace[tbase + n] = TraceEnt{c->ptrace, c->move};
+        c->trace = kept ? p.tgid + tbase + n : TRACE_NONE;
+        if (kept) p.trace[tbase + n] = TraceEnt{c->ptrace, c->move};
       }
       if (p.pmax) {  // LinearizationInfo: this configuration as the longest one holding each chain's prefix
         uint32_t size = 0;

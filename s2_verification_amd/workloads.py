@@ -7,7 +7,7 @@ an injected violation), C5 32x1000 (seed 5, client-id cap lifted, 3% indefinite
 appends) and its non-linearizable variant.
 """
 from . import (VIOL_DEFINITE_APPLIED, VIOL_NONE, VIOL_READ_HASH, VIOL_STALE_MSN, VIOL_TAIL, WF_FENCING,
-               WF_MATCH_SEQ_NUM, WF_REGULAR, simulate_history, simulate_jsonl)
+               WF_MATCH_SEQ_NUM, WF_REGULAR, sim_params, simulate_history, simulate_jsonl)
 
 BASE = dict(p_indefinite=0.01, p_definite=0.02, p_read_failure=0.01, p_check_tail_failure=0.01)
 
@@ -68,6 +68,21 @@ def c4_params(seed: int) -> dict:
     wf = (WF_REGULAR, WF_MATCH_SEQ_NUM, WF_FENCING)[seed % 3]
     viol = _C4_VIOLS[(seed // 10) % 4] if seed % 10 == 7 else VIOL_NONE
     return dict(workflow=wf, num_clients=5 + seed % 4, ops_per_client=100, seed=seed, violation=viol, **BASE)
+
+
+def config_meta(name: str) -> dict:
+    """What a config name promises against what the simulator is asked for:
+    the planned op count (clients x ops per client) and the client-id cap
+    (the collector's MAX_CLIENT_IDS = 20, history.rs:33, unless lifted). Under
+    the cap a client stops at its first indefinite failure once its ids run
+    out, so a history can hold fewer ops than planned (C3: 4,325 of 8,000)."""
+    c = CONFIGS[name]
+    p = sim_params(**c)
+    return {"n_ops_planned": c["num_clients"] * c["ops_per_client"], "client_id_cap": int(p.max_client_ids),
+            "client_id_cap_lifted": int(p.max_client_ids) != COLLECTOR_MAX_CLIENT_IDS}
+
+
+COLLECTOR_MAX_CLIENT_IDS = 20  # collect-history's MAX_CLIENT_IDS (history.rs:33)
 
 
 def config_history(name: str):

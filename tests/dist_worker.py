@@ -76,3 +76,36 @@ def search_worker(rank, world, port, backend, names, wide, persistent, self_exch
         dist.destroy_process_group()
     except Exception:
         q.put((rank, "error", traceback.format_exc()))
+
+
+def overflow_worker(rank, world, port, backend, name, wide, scap, q):
+    """GPU: an exchanged round whose winners (the rank's own share
+    plus the received blocks) can pass the staging capacity, with the witness
+    on: a staging array forced small (S2LC_LEVEL_SCAP, read when the level
+    buffers are first sized). The search must end cleanly (a verdict, or the
+    buffer error), never write past its trace pool; a second history checked
+    afterwards in the same process must still be right."""
+    try:
+        os.environ["S2LC_LEVEL_SCAP"] = str(scap)
+        import torch
+        import s2_verification_amd as s2
+        from s2_verification_amd import workloads as W
+        from s2_verification_amd.distributed import check_distributed
+        torch.cuda.set_device(0 if backend == "gloo" else rank)
+        dist = _init(rank, world, port, backend)
+        checker = s2.Checker(device=torch.cuda.current_device())
+        out = []
+        try:
+            r = check_distributed(checker, W.config_history(name), wide=wide, persistent=False, witness=True)
+            out.append(("verdict", r.verdict, r.rounds, r.witness_valid))
+        except s2.S2LCError as e:
+            out.append(("error", str(e)))
+        # the process (and its device) is still sound: the single-GPU engine
+        # on a small history
+        h = W.config_history("C1")
+        rr = checker.check(h)
+        out.append(("after", rr.verdict, rr.witness is not None))
+        q.put((rank, out))
+        dist.destroy_process_group()
+    except Exception:
+        q.put((rank, "error", traceback.format_exc()))

@@ -67,6 +67,15 @@ def test_bench_two_gloo_ranks_on_one_gpu():
     assert c5["verdict"] == hard["C5"]["verdict"] and c5["witness_replayed"], c5
     assert c5["bad_variant_verdict"] == hard["C5bad"]["verdict"]
     assert c5["replicated_only"]["verdict"] == c5["verdict"]
+    # every rank self-checks H212 / C5bad with forced block
+    # overflows and re-runs before the timed C5 legs
+    dp = d["dist_parity"]
+    assert dp["ok"] is True and dp["failing_cases_summed_over_ranks"] == 0, dp
+    for name in ("H212", "C5bad"):
+        cs = dp["cases"][name]
+        assert cs["verdict"] == hard[name]["verdict"] and cs["rounds"] == hard[name]["reduced"]["rounds"], cs
+        assert cs["xreruns_rank0"] >= 1 and cs["partitioned_rounds"] > 0, cs
+    assert d["config"]["client_id_cap"] == 20 and c5["client_id_cap"] > 20 and c5["n_ops_planned"] == 32000
     w = c5["c5wide"]
     assert w["verdict"] == hard["C5wide"]["verdict"] and w["witness_replayed"], w
     # the N-GPU legs carry the single-GPU engine's time and the
@@ -79,10 +88,11 @@ def test_bench_two_gloo_ranks_on_one_gpu():
 
 @pytest.mark.gpu
 def test_bench_watchdog_keeps_the_c4_line():
-    """A multi-GPU leg that stalls must not cost the C4 line: with a watchdog
-    budget far below the legs' time, every rank ends itself and rank 0 prints
-    the line with the legs finished so far (the C4 measurement) and a
-    `watchdog` note, exit status 0."""
+    """A multi-GPU leg that stalls must not cost the C4 line, and must not read
+    as success: with a watchdog budget far below the legs' time,
+    every rank ends itself and rank 0 prints the line with the legs finished
+    so far (the C4 measurement), `stalled_leg` and a `watchdog` note; the run
+    exits non-zero."""
     import random
     port = random.randint(20000, 40000)
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
@@ -90,8 +100,9 @@ def test_bench_watchdog_keeps_the_c4_line():
            "--gpus", "2", "--steps", "2", "--warmup", "1", "--no-e2e", "--c5-reps", "1"]
     env = dict(os.environ, S2LC_BENCH_GLOO="1", S2LC_BENCH_WATCHDOG="0.05")
     p = subprocess.run(cmd, capture_output=True, text=True, timeout=600, cwd=ROOT, env=env)
-    assert p.returncode == 0, p.stderr[-4000:]
+    assert p.returncode != 0, p.stdout[-2000:]
     lines = [x for x in p.stdout.splitlines() if x.startswith("{")]
     assert len(lines) == 1, p.stdout[-2000:]
     d = json.loads(lines[0])
     assert "watchdog" in d and d["n_gpus"] == 2 and d["value"] > 0 and d["verdicts"]["Unknown"] == 0, d
+    assert d["stalled_leg"] == "strong_split" and "strong_split" not in d and "c5" not in d, d

@@ -174,3 +174,32 @@ def test_distributed_search_on_a_side_stream(world, wide, backend, selfx):
             assert part > 0, (rank, name)
             if verdict == "Ok":
                 assert wvalid and wlen == n_ops, (rank, name, wvalid, wlen)
+
+
+@pytest.mark.gpu
+def test_exchanged_round_past_staging_capacity_with_witness():
+    """in an exchanged round lv_insert takes the rank's whole local
+    share plus the received blocks, so a round's winners can number more than
+    the staging capacity. Those winners get no frontier index and no trace
+    entry (the close stops the run). With a staging array forced to 1,024
+    configurations, H212's partitioned rounds (2 ranks, from a frontier of
+    256) end either with the committed verdict and round count or with the
+    capacity error, identically on both ranks, and the process then checks
+    another history correctly."""
+    import dist_worker
+    ref = golden("hard_reduced.json")["H212"]
+    port = random.randint(20000, 40000)
+    out = _spawn(dist_worker.overflow_worker, [(r, 2, port, "gloo", "H212", 256, 1024) for r in range(2)])
+    outcomes = set()
+    for rank, res in out:
+        first, after = res
+        if first[0] == "verdict":
+            assert first[1] == ref["verdict"] and first[2] == ref["reduced"]["rounds"], (rank, first)
+            if first[1] == "Ok":
+                assert first[3], (rank, first)
+            outcomes.add(first[:3])
+        else:
+            assert "exceeds" in first[1] or "frontier" in first[1], (rank, first)
+            outcomes.add(("error",))
+        assert after[1:] == ("Ok", True), (rank, after)
+    assert len(outcomes) == 1, outcomes
