@@ -201,15 +201,24 @@ __device__ __forceinline__ void lv_solo_head(const uint64_t* pool, const OpRec* 
 }
 
 // What the solo round loop reads besides LDS (kernel-parameter values; the
-// loop is a function of its own).
+// loop is a function of its own). A by-value argument: the caller writes it to
+// the call frame right before the call and the callee reads it in its
+// prologue (tests/test_kernel_resources.py checks exactly that). No field is
+// indexed dynamically (the staging arrays by round parity are two fields,
+// selected by a ternary): a dynamic index would keep the struct in scratch
+// inside the round loop. (Handing it over through LDS instead was measured in
+// round 6: C5's solo rounds 63.5 -> 64.8 ms, the callee's registers allocated
+// differently; profiles/r06/solo_args_ab.txt.)
 struct SoloArgs {
   const OpRec* recs;
   const uint64_t* pool;
   TraceEnt* trace;
   uint32_t* rcounts;
   unsigned long long* prof;
-  uint8_t* stg[2];
-  uint32_t* idx[2];
+  uint8_t* stg0;
+  uint8_t* stg1;
+  uint32_t* idx0;
+  uint32_t* idx1;
   uint64_t trace_cap;
   unsigned long long deadline;  // device wall clock; 0 = none
   uint32_t K, hflags, scap, scs, tgid, max_rounds, max_live;
@@ -325,9 +334,10 @@ enum : uint32_t { SX_END = 0, SX_OVF = 1, SX_STAGED = 2, SX_MAX = 3, SX_GRID = 4
 // barrier per round; waves 1..3 wait for the phase's end). Returns how the
 // phase ended (SX_*); the configuration / kept child to write is left in S.
 template <int NQ>
-__device__ __attribute__((noinline)) uint32_t lv_solo_wave(const SoloArgs p, LvRun& R, LvSoloHeads<NQ>& PL,
+__device__ __attribute__((noinline)) uint32_t lv_solo_wave(const SoloArgs pa, LvRun& R, LvSoloHeads<NQ>& PL,
                                                            LvSoloHeads<NQ>& NX, LvSoloExt<NQ>& FR,
                                                            const uint32_t* s_cs, LvSolo<NQ>& S) {
+  const SoloArgs& p = pa;
   const int lane = (int)(threadIdx.x & 63);
   const uint32_t K = p.K, hf = p.hflags;
   const bool p1 = hf & H_NOWRAP, p2 = hf & H_P2OK, p4 = hf & H_P4, idefer = hf & H_IDEFER;
@@ -586,10 +596,10 @@ __device__ __attribute__((noinline)) uint32_t lv_solo_wave(const SoloArgs p, LvR
               if (dd == 1) lv_solo_hashes(p.pool, S.nx_hoff[jj], S.nx_hcnt[jj], hv8);
               pre_j = jj; pre_c0 = c0; pre_dd = dd;
             }
-          } else if (k < p.scs) {
+          } else if (k < pa.scs) {
 #pragma unroll
             for (int q = 0; q < NQ; ++q) S.keep[lane + 64 * q] = (uint16_t)d[q];
-            lv_solo_stage<NQ>(S, p.stg[r & 1], p.idx[r & 1], p.trace, p.tgid, K, k, ct, ch, ck, minret, ptrace, mv,
+            lv_solo_stage<NQ>(S, (r & 1) ? pa.stg1 : pa.stg0, (r & 1) ? pa.idx1 : pa.idx0, p.trace, p.tgid, K, k, ct, ch, ck, minret, ptrace, mv,
                               tbase, wit, chx_ok ? 1u : 0u);
             chx_ok = true;
           } else {
@@ -788,7 +798,7 @@ __device__ void lv_solo_rounds(const LvParams& p, const LvPersist& q, LvRun& R, 
   if (threadIdx.x < 64) {
     SoloArgs a;
     a.recs = p.recs; a.pool = p.pool; a.trace = p.trace; a.rcounts = p.rcounts; a.prof = p.prof;
-    for (int i = 0; i < 2; ++i) { a.stg[i] = q.stg[i]; a.idx[i] = q.idx[i]; }
+    a.stg0 = q.stg[0]; a.stg1 = q.stg[1]; a.idx0 = q.idx[0]; a.idx1 = q.idx[1];
     a.trace_cap = p.trace_cap;
     a.deadline = deadline;
     a.K = p.K; a.hflags = p.hflags; a.scap = p.scap; a.scs = p.scs; a.tgid = p.tgid;
