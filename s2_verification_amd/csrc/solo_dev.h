@@ -385,10 +385,20 @@ __device__ __attribute__((noinline)) uint32_t lv_solo_wave(const SoloArgs pa, Lv
     // (I-op, deferral), the identity child's existence needs the fold (opt ==
     // s on everything but the hash).
     uint32_t b_opt = 0, b_tip = 0, b_eqn = 0, n_dead = 0;
+    // every slot's values read first, with one wait for all of them: a value
+    // only some lanes need (msn) would otherwise be loaded under a branch,
+    // one LDS round trip after another
+    uint32_t a_nr[NQ], a_msn[NQ], a_toks[NQ], a_ot[NQ], a_nxs[NQ];
 #pragma unroll
     for (int q = 0; q < NQ; ++q) {
       const uint32_t j = (uint32_t)(64 * q + lane);
-      const uint32_t nr = FR.nr[j], msn = FR.msn[j], toks = FR.toks[j], otl = PL.ot[j], nxs = NX.suf[j];
+      a_nr[q] = FR.nr[j]; a_msn[q] = FR.msn[j]; a_toks[q] = FR.toks[j]; a_ot[q] = PL.ot[j]; a_nxs[q] = NX.suf[j];
+    }
+#pragma unroll
+    for (int q = 0; q < NQ; ++q) asm volatile("" : "+v"(a_nr[q]), "+v"(a_msn[q]), "+v"(a_toks[q]), "+v"(a_ot[q]), "+v"(a_nxs[q]));
+#pragma unroll
+    for (int q = 0; q < NQ; ++q) {
+      const uint32_t nr = a_nr[q], msn = a_msn[q], toks = a_toks[q], otl = a_ot[q], nxs = a_nxs[q];
       const uint32_t fl = hfl[q];
       const bool cand = !(fl & (OPF_SENTINEL | OPF_CLS_E)) && hcall[q] < pmin;
       const uint32_t bt = toks & 0xFFFFu, st = toks >> 16;
@@ -456,11 +466,13 @@ __device__ __attribute__((noinline)) uint32_t lv_solo_wave(const SoloArgs pa, Lv
       const uint32_t otail = ptail + nr, otok = (toks >> 16) ? (toks >> 16) : ptok;
       uint64_t ohash = phash;
       if (m_opt || m_eqn) {
-        uint64_t h = phash;
+        // (uni64 at every step: phash is a loop-carried VGPR value, so
+        // without it the chain of 64-bit multiplies is selected as VALU code)
+        uint64_t h = uni64(phash);
 #pragma unroll
         for (int k = 0; k < LV_SOLO_HPT; ++k)
-          if ((uint32_t)k < hcnt) h = chain_hash(h, uni64(hv[k]));
-        for (uint32_t k = LV_SOLO_HPT; k < hcnt; ++k) h = chain_hash(h, uni64(p.pool[hoff + k]));
+          if ((uint32_t)k < hcnt) h = uni64(chain_hash(h, uni64(hv[k])));
+        for (uint32_t k = LV_SOLO_HPT; k < hcnt; ++k) h = uni64(chain_hash(h, uni64(p.pool[hoff + k])));
         ohash = h;
       }
 #ifdef S2LC_PROF
