@@ -547,6 +547,21 @@ __device__ __forceinline__ void st_wt32(uint32_t* p, uint32_t v) {
 __device__ __forceinline__ void st_wt64(void* p, unsigned long long v) {
   __hip_atomic_store((lv_g64*)p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
+// Plain loads / stores through a global (address space 1) pointer. A pointer
+// that reaches a noinline function (the solo rounds) is generic, and generic
+// accesses compile to flat_* instructions, which count on lgkmcnt as well as
+// vmcnt: every later LDS wait (s_waitcnt lgkmcnt(0)) then also waits for the
+// memory access (round 6: C5's solo rounds 61.2 -> 60.5 ms with these,
+// profiles/r06/solo_args_ab.txt).
+typedef unsigned int lv_u32x4 __attribute__((ext_vector_type(4)));
+__device__ __forceinline__ uint4 lv_gld16(const void* p) {
+  const lv_u32x4 v = *(const __attribute__((address_space(1))) lv_u32x4*)p;
+  return make_uint4(v.x, v.y, v.z, v.w);
+}
+__device__ __forceinline__ uint32_t lv_gld32(const void* p) { return *(const lv_g32*)p; }
+__device__ __forceinline__ unsigned long long lv_gld64(const void* p) { return *(const lv_g64*)p; }
+__device__ __forceinline__ void lv_gst32(void* p, uint32_t v) { *(lv_g32*)p = v; }
+__device__ __forceinline__ void lv_gst64(void* p, unsigned long long v) { *(lv_g64*)p = v; }
 __device__ __forceinline__ uint16_t ld_wt16(const uint16_t* p) {
   return __hip_atomic_load((lv_g16*)p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
@@ -1336,7 +1351,7 @@ __device__ __forceinline__ void lv_close_state(LvRun& R, const LvCounts& k, uint
     R.found_move = k.fmov;
     R.found_p4 = k.fp4;
   } else {
-    if (rcounts) rcounts[rnd] = k.nn;
+    if (rcounts) lv_gst32(rcounts + rnd, k.nn);
     R.round = rnd;
     if (k.nn == 0) {
       R.done = LVR_EMPTY;

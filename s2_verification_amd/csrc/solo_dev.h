@@ -147,7 +147,7 @@ __device__ __forceinline__ SoloKeys solo_keys(uint32_t fl, uint32_t call, uint32
 __device__ __forceinline__ void lv_solo_hashes(const uint64_t* __restrict__ pool, uint32_t ho, uint32_t hc,
                                                uint64_t (&hv)[LV_SOLO_HPT]) {
 #pragma unroll
-  for (int k = 0; k < LV_SOLO_HPT; ++k) hv[k] = pool[hc ? ho + min((uint32_t)k, hc - 1u) : 0u];
+  for (int k = 0; k < LV_SOLO_HPT; ++k) hv[k] = lv_gld64(pool + (hc ? ho + min((uint32_t)k, hc - 1u) : 0u));
 }
 
 // A solo configuration's head on chain j (record x = bytes 0..63, its next
@@ -192,8 +192,8 @@ __device__ __forceinline__ void lv_solo_head(const uint64_t* pool, const OpRec* 
                                              LvSoloExt<NQ>& FR, LvSolo<NQ>& S) {
   const uint4* a = reinterpret_cast<const uint4*>(h);
   const uint4* b = reinterpret_cast<const uint4*>(h + 1 < end ? h + 1 : h);  // (the sentinel has no next record)
-  const uint4 x0 = a[0], x1 = a[1], x2 = a[2], x3 = a[3];
-  const uint4 y1 = b[1], y2 = b[2], y3 = b[3];
+  const uint4 x0 = lv_gld16(a), x1 = lv_gld16(a + 1), x2 = lv_gld16(a + 2), x3 = lv_gld16(a + 3);
+  const uint4 y1 = lv_gld16(b + 1), y2 = lv_gld16(b + 2), y3 = lv_gld16(b + 3);
   uint64_t hv[LV_SOLO_HPT];
   if (known) lv_solo_hashes(pool, S.nx_hoff[j], S.nx_hcnt[j], hv);
   else lv_solo_hashes(pool, x3.x, x3.y, hv);
@@ -298,9 +298,10 @@ __device__ __attribute__((noinline)) void lv_solo_reload_lane(const OpRec* recs,
 // A closure's head after a chain's second advance (not in LDS): its closure fields
 struct SoloHead { uint64_t oh; uint32_t ot, suf, call, ret, fl; };
 __device__ __attribute__((noinline)) SoloHead lv_solo_load_head(const OpRec* r) {
-  const uint4 o = ld16(r, 16), mm = ld16(r, 32);
+  const uint8_t* rb = reinterpret_cast<const uint8_t*>(r);
+  const uint4 o = lv_gld16(rb + 16), mm = lv_gld16(rb + 32);
   SoloHead h;
-  h.fl = r->flags;
+  h.fl = lv_gld32(&r->flags);
   h.ot = o.y ? 0xFFFFFFFFu : o.x;
   h.oh = (uint64_t)o.z | ((uint64_t)o.w << 32);
   h.suf = suf32((uint64_t)mm.x | ((uint64_t)mm.y << 32));
@@ -436,10 +437,6 @@ __device__ __attribute__((noinline)) uint32_t lv_solo_wave(const SoloArgs pa, Lv
     // the moves with a child to close
     uint32_t alive = 0, found = 0, ovf = 0, fpar = 0, fmov = 0, fp4 = 0;
     unsigned long long kids = n_dead;  // (P1-dead opt children: counted, never closed)
-    // the kept child's advanced chain on this lane (loaded early: VGPRs)
-    uint32_t pre_j = 0, pre_c0 = 0, pre_dd = 0;
-    uint4 x0, x1, x2, x3, y1, y2, y3;
-    uint64_t hv8[LV_SOLO_HPT];
     for (;;) {
       const uint64_t m = __ballot(b_live != 0);
       if (m == 0 || found) break;
@@ -472,7 +469,7 @@ __device__ __attribute__((noinline)) uint32_t lv_solo_wave(const SoloArgs pa, Lv
 #pragma unroll
         for (int k = 0; k < LV_SOLO_HPT; ++k)
           if ((uint32_t)k < hcnt) h = uni64(chain_hash(h, uni64(hv[k])));
-        for (uint32_t k = LV_SOLO_HPT; k < hcnt; ++k) h = uni64(chain_hash(h, uni64(p.pool[hoff + k])));
+        for (uint32_t k = LV_SOLO_HPT; k < hcnt; ++k) h = uni64(chain_hash(h, uni64(lv_gld64(p.pool + hoff + k))));
         ohash = h;
       }
 #ifdef S2LC_PROF
@@ -587,27 +584,8 @@ __device__ __attribute__((noinline)) uint32_t lv_solo_wave(const SoloArgs pa, Lv
           const uint32_t k = alive++;
           if (k == 0) {
             ktail = ct; khash = ch; ktok = ck; kmr = minret; kmv = mv;
-            uint32_t nmine = 0, qm = 0;
 #pragma unroll
-            for (int q = 0; q < NQ; ++q) {
-              kd[q] = d[q];
-              if (d[q]) { ++nmine; qm = (uint32_t)q; }
-            }
-            // its advanced chains' records and first hashes, loaded now
-            // (one chain per lane; a lane with more reloads after the round)
-            if (nmine == 1) {
-              const uint32_t jj = (uint32_t)lane + 64u * qm, dd = sel_u32<NQ>(d, qm);
-              const uint32_t c0 = S.cnt[jj];
-              const OpRec* h = p.recs + s_cs[jj] + c0 + dd;
-              const OpRec* end = p.recs + (jj + 1 < K ? s_cs[jj + 1] : S.cs_end);
-              const uint4* a4 = reinterpret_cast<const uint4*>(h);
-              const uint4* b4 = reinterpret_cast<const uint4*>(h + 1 < end ? h + 1 : h);
-              x0 = a4[0]; x1 = a4[1]; x2 = a4[2]; x3 = a4[3];
-              y1 = b4[1]; y2 = b4[2]; y3 = b4[3];
-              // (dd >= 2: the head's hash range is in its record, loaded after the round)
-              if (dd == 1) lv_solo_hashes(p.pool, S.nx_hoff[jj], S.nx_hcnt[jj], hv8);
-              pre_j = jj; pre_c0 = c0; pre_dd = dd;
-            }
+            for (int q = 0; q < NQ; ++q) kd[q] = d[q];
           } else if (k < pa.scs) {
 #pragma unroll
             for (int q = 0; q < NQ; ++q) S.keep[lane + 64 * q] = (uint16_t)d[q];
@@ -637,7 +615,7 @@ __device__ __attribute__((noinline)) uint32_t lv_solo_wave(const SoloArgs pa, Lv
       lv_close_state(R, kc, r, p.rcounts, p.scap, p.trace_cap, false);
       R.solo_rounds++;
       // the first survivor's trace entry (it was not staged)
-      if (!found && !ovf && alive && wit) p.trace[tbase] = TraceEnt{ptrace, kmv};
+      if (!found && !ovf && alive && wit) lv_gst64(p.trace + tbase, (unsigned long long)kmv << 32 | ptrace);
 #ifdef S2LC_PROF
       if (p.prof) { atomicAdd(&p.prof[29], (unsigned long long)alive); atomicAdd(&p.prof[30], alive == 1 ? 1ull : 0ull); }
 #endif
@@ -647,13 +625,16 @@ __device__ __attribute__((noinline)) uint32_t lv_solo_wave(const SoloArgs pa, Lv
       // the kept child becomes the configuration: its advanced chains into
       // LDS (early loads; a lane with two advanced slots loads them now) and
       // their closure fields into registers
-      uint32_t nmine = 0;
+      uint32_t nmine = 0, qm = 0;
 #pragma unroll
-      for (int q = 0; q < NQ; ++q) nmine += kd[q] ? 1u : 0u;
-      if (pre_dd) {
-        if (pre_dd != 1) lv_solo_hashes(p.pool, x3.x, x3.y, hv8);
-        S.cnt[pre_j] = (uint16_t)(pre_c0 + pre_dd);
-        lv_solo_head_put<NQ>(x0, x1, x2, x3, y1, y2, y3, hv8, pre_j, PL, NX, FR, S);
+      for (int q = 0; q < NQ; ++q)
+        if (kd[q]) { ++nmine; qm = (uint32_t)q; }
+      if (nmine == 1) {
+        const uint32_t jj = (uint32_t)lane + 64u * qm, dd = sel_u32<NQ>(kd, qm);
+        const uint32_t c = (uint32_t)S.cnt[jj] + dd;
+        S.cnt[jj] = (uint16_t)c;
+        lv_solo_head<NQ>(p.pool, p.recs + s_cs[jj] + c, p.recs + (jj + 1 < K ? s_cs[jj + 1] : S.cs_end), jj, dd == 1,
+                         PL, NX, FR, S);
       } else if (nmine > 1) {
 #pragma unroll
         for (int q = 0; q < NQ; ++q) S.keep[lane + 64 * q] = (uint16_t)kd[q];
