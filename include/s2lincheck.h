@@ -237,7 +237,10 @@ int s2lc_history_from_events(const s2lc_event* events, size_t n_events,
  * go back to the C heap here). */
 void s2lc_history_free(s2lc_history* h);
 /* Return every parked history's arrays to the C heap, and this thread's
- * decode / finalize scratch; returns the array bytes (capacity) released. */
+ * decode / finalize scratch; returns the array bytes (capacity) released.
+ * (s2lc_load_jsonl_many's other decoder threads live for one call: their
+ * scratch is released when they exit; the calling thread's stays until this
+ * call.) */
 size_t s2lc_history_pool_trim(void);
 size_t s2lc_history_event_count(const s2lc_history* h);
 /* Export event i (pointers stay valid while h lives). */

@@ -411,7 +411,14 @@ int batch_upload(DevBatch& b, const std::vector<const History*>& hs, uint32_t re
   }
   b.h_res_stale = false;
   if (n_sl == 1) {
-    HIPCHK(hipMemcpy(b.arena, b.stage, stage_bytes, hipMemcpyHostToDevice));
+    // only the record region(s) this batch filled (64-byte OpRec, 32-byte
+    // SRec, or both), then the pool and the small sections (the
+    // whole stage had gone up, both record regions included)
+    if (n_recs && sl_big[0].load(std::memory_order_relaxed))
+      HIPCHK(hipMemcpyAsync(b.arena + o_recs, b.stage + o_recs, n_recs * sizeof(OpRec), hipMemcpyHostToDevice, 0));
+    if (n_recs && sl_small[0].load(std::memory_order_relaxed))
+      HIPCHK(hipMemcpyAsync(b.arena + o_srec, b.stage + o_srec, n_recs * sizeof(SRec), hipMemcpyHostToDevice, 0));
+    HIPCHK(hipMemcpyAsync(b.arena + o_pool, b.stage + o_pool, stage_bytes - o_pool, hipMemcpyHostToDevice, 0));
   } else {  // the rest of the stage after the records and the pool, then wait for every slice
     HIPCHK(hipMemcpyAsync(b.arena + o_cs, b.stage + o_cs, stage_bytes - o_cs, hipMemcpyHostToDevice, 0));
   }
