@@ -125,3 +125,28 @@ def test_fence_token_hash_is_xxh3():
             assert st["Append"]["record_hashes"] == [xxhash.xxh3_64_intdigest(tok.encode())]
             n += 1
     assert n >= 3
+
+
+def test_bench_watchdog_exits_nonzero_with_the_stalled_leg():
+    """bench.py's multi-GPU watchdog, on the CPU: a leg
+    that outlives S2LC_BENCH_WATCHDOG makes rank 0 print the line it has so
+    far with `stalled_leg`, and the process exit with WATCHDOG_EXIT (non-zero:
+    a stalled collective never reads as success); a disarmed timer never
+    fires."""
+    import json
+    import os
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    code = ("import sys, time; sys.path.insert(0, %r); import bench; "
+            "line = {'metric': 'm', 'value': 1.0}; wd = bench._Watchdog(0, line); "
+            "wd.arm('quick'); wd.disarm(); time.sleep(0.3); "
+            "line['quick'] = {'ok': True}; wd.arm('stuck'); time.sleep(30)" % root)
+    p = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, timeout=60,
+                       env=dict(os.environ, S2LC_BENCH_WATCHDOG="0.2"))
+    import bench  # noqa: E402  (the exit code it promises)
+    assert p.returncode == bench.WATCHDOG_EXIT != 0, (p.returncode, p.stderr[-2000:])
+    lines = [x for x in p.stdout.splitlines() if x.startswith("{")]
+    assert len(lines) == 1, p.stdout
+    d = json.loads(lines[0])
+    assert d["stalled_leg"] == "stuck" and d["quick"] == {"ok": True} and "watchdog" in d, d
