@@ -23,8 +23,10 @@
 //     every chain's head (closure fields, the move's fields, its first 8
 //     record hashes) and the record after it (a child's first new head on
 //     that chain); the heads' closure fields also stay in registers. Only the
-//     chains the surviving child advanced are reloaded, and their loads go
-//     out as soon as that child is kept;
+//     chains the surviving child advanced are reloaded, at the carry; each
+//     reload then touches what that chain's next advance will load (the
+//     record after the next one, the next one's record hashes) with loads
+//     into an LDS sink, so the next reload hits the caches;
 //   - the precheck of every candidate move (guards, outcome, the P1 bound
 //     without the move's own chain) is branch-free over the chain slots, its
 //     results per-lane bit masks;
@@ -42,6 +44,11 @@
 //     registers are allocated for the loop alone.
 #pragma once
 
+// After a carry, touch the records the advanced chains' next advance will
+// load (S2LC_SOLO_TOUCH=0 turns it off; profiles/r06/solo_touch_ab.txt)
+#ifndef S2LC_SOLO_TOUCH
+#define S2LC_SOLO_TOUCH 1
+#endif
 constexpr int LV_SOLO_HP = 4;   // record hashes of each head kept in LvSolo
 constexpr int LV_SOLO_HP2 = 4;  // the next ones, in LvSoloExt (8 in LDS: 91 % of C5's appends)
 constexpr int LV_SOLO_HPT = LV_SOLO_HP + LV_SOLO_HP2;
@@ -80,6 +87,9 @@ struct LvSolo {
   uint64_t ktail, khash, kchx;     // the kept child
   uint32_t tok, pmin, ptrace, ktok, kmr, kmv, cs_end, xtrace;
   uint64_t wx[LV_BLOCK / 64];
+#if S2LC_SOLO_TOUCH
+  uint32_t sink[64];  // destination of the cache-touch loads (never read)
+#endif
 #ifdef S2LC_PROF
   unsigned long long pt[8];  // wave 0 phase cycles: [0] start [1] setup [2] pre [3] moves [4] close [5] next [6] wait; [7] last stamp
   unsigned long long pc[6];  // closure cycles (ALIVE, other), ALIVE closures, stage cycles, closure passes, closure head loads
@@ -186,10 +196,22 @@ __device__ __forceinline__ void lv_solo_head_put(const uint4& x0, const uint4& x
 // loaded and put. `known`: the head's hash range is already known (it was the
 // previous head's next record), so the hash loads go out with the record
 // loads instead of after them.
+#if S2LC_SOLO_TOUCH
+// (inline asm, not the builtin: the compiler tracks the builtin's LDS write
+// and waits for it before every later LDS read it cannot tell apart from the
+// sink, which makes the touch a blocking load. Untracked, it only makes a
+// later counted vmcnt wait over-wait, never under-wait: loads retire in order.)
+__device__ __forceinline__ void lv_touch(const void* g, uint32_t* sink) {
+  const uint32_t dst = (uint32_t)(uintptr_t)(__attribute__((address_space(3))) uint32_t*)sink;
+  uint32_t keep;
+  asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dword %1, off\n\ts_mov_b32 m0, %0"
+               : "=&s"(keep) : "v"(g), "s"(dst));
+}
+#endif
 template <int NQ>
 __device__ __forceinline__ void lv_solo_head(const uint64_t* pool, const OpRec* h, const OpRec* end, uint32_t j,
                                              bool known, LvSoloHeads<NQ>& PL, LvSoloHeads<NQ>& NX,
-                                             LvSoloExt<NQ>& FR, LvSolo<NQ>& S) {
+                                             LvSoloExt<NQ>& FR, LvSolo<NQ>& S, bool touch = false) {
   const uint4* a = reinterpret_cast<const uint4*>(h);
   const uint4* b = reinterpret_cast<const uint4*>(h + 1 < end ? h + 1 : h);  // (the sentinel has no next record)
   const uint4 x0 = lv_gld16(a), x1 = lv_gld16(a + 1), x2 = lv_gld16(a + 2), x3 = lv_gld16(a + 3);
@@ -198,6 +220,17 @@ __device__ __forceinline__ void lv_solo_head(const uint64_t* pool, const OpRec* 
   if (known) lv_solo_hashes(pool, S.nx_hoff[j], S.nx_hcnt[j], hv);
   else lv_solo_hashes(pool, x3.x, x3.y, hv);
   lv_solo_head_put<NQ>(x0, x1, x2, x3, y1, y2, y3, hv, j, PL, NX, FR, S);
+#if S2LC_SOLO_TOUCH
+  if (touch) {
+    // what this chain's next advance loads (the record after the next one,
+    // the next one's record hashes), pulled into the caches by loads that
+    // write LDS (no register waits for them)
+    lv_touch(h + 2 < end ? h + 2 : h, S.sink);
+    const uint32_t ho = y3.y ? y3.x : 0u;
+    lv_touch(pool + ho, S.sink);
+    lv_touch(pool + ho + (y3.y > 8u ? 7u : (y3.y ? y3.y - 1u : 0u)), S.sink);
+  }
+#endif
 }
 
 // What the solo round loop reads besides LDS (kernel-parameter values; the
@@ -634,7 +667,7 @@ __device__ __attribute__((noinline)) uint32_t lv_solo_wave(const SoloArgs pa, Lv
         const uint32_t c = (uint32_t)S.cnt[jj] + dd;
         S.cnt[jj] = (uint16_t)c;
         lv_solo_head<NQ>(p.pool, p.recs + s_cs[jj] + c, p.recs + (jj + 1 < K ? s_cs[jj + 1] : S.cs_end), jj, dd == 1,
-                         PL, NX, FR, S);
+                         PL, NX, FR, S, true);
       } else if (nmine > 1) {
 #pragma unroll
         for (int q = 0; q < NQ; ++q) S.keep[lane + 64 * q] = (uint16_t)kd[q];
@@ -698,6 +731,9 @@ __device__ __attribute__((noinline)) uint32_t lv_solo_wave(const SoloArgs pa, Lv
     }
 #endif
   }
+#if S2LC_SOLO_TOUCH
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // (the touches land before the phase ends)
+#endif
   return ex;
 }
 
