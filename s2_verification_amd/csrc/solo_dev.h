@@ -44,6 +44,12 @@
 //     registers are allocated for the loop alone.
 #pragma once
 
+// A carry round's close on registers (the run state's per-round fields held
+// by the solo wave for the phase, written back before its last close and at
+// its exit; S2LC_SOLO_REGRUN=0: every round closes on the LDS run state)
+#ifndef S2LC_SOLO_REGRUN
+#define S2LC_SOLO_REGRUN 1
+#endif
 // After a carry, touch the records the advanced chains' next advance will
 // load (S2LC_SOLO_TOUCH=0 turns it off; profiles/r06/solo_touch_ab.txt)
 #ifndef S2LC_SOLO_TOUCH
@@ -397,11 +403,38 @@ __device__ __attribute__((noinline)) uint32_t lv_solo_wave(const SoloArgs pa, Lv
 #ifdef S2LC_PROF
   unsigned long long pf_closures = 0, pf_dead = 0;
 #endif
+#if S2LC_SOLO_REGRUN
+  // the run state's fields a carry round's close changes (lv_close_state with
+  // one new configuration, no overflow, not found), wave-uniform; R is behind
+  // by `nfast` such closes until flush() writes them back (lane 0)
+  uint32_t g_round = uni32(R.round), g_wit = uni32(R.witness), g_ltb = uni32(R.last_tbase), g_done = uni32(R.done);
+  uint64_t g_tnext = uni64(R.tnext), g_cfg = uni64(R.configs), g_ch = 0;
+  const uint64_t g_maxc = uni64(R.max_configs);
+  uint32_t nfast = 0;
+  auto flush = [&]() {
+    if (nfast && lane == 0) {
+      R.round = g_round; R.witness = g_wit; R.last_tbase = g_ltb; R.done = g_done;
+      R.tnext = g_tnext; R.configs = g_cfg; R.children += g_ch;
+      R.nf = 1; R.last_nf = 1; R.last_closed = 0; R.max_frontier = max(R.max_frontier, 1u);
+      R.solo_rounds += nfast;
+    }
+    nfast = 0;
+    g_ch = 0;
+  };
+#endif
   for (uint32_t n = 0;; ++n) {
+#if S2LC_SOLO_REGRUN
+    const uint32_t r = g_round + 1;
+    const uint32_t tbase = (uint32_t)g_tnext, wit = g_wit;
+#else
     const uint32_t r = uni32(R.round) + 1;
     const uint32_t tbase = uni32((uint32_t)R.tnext), wit = uni32(R.witness);
+#endif
     if (p.deadline && (n & 15) == 15 && uni64(wall_clock64()) > p.deadline) {
       // the run's deadline (checked every 16 rounds): Unknown (timeout)
+#if S2LC_SOLO_REGRUN
+      flush();
+#endif
       if (lane == 0) R.done = LVR_TIMEOUT;
       ex = SX_END;
       break;
@@ -462,6 +495,9 @@ __device__ __attribute__((noinline)) uint32_t lv_solo_wave(const SoloArgs pa, Lv
       if (tot > p.max_live) {
         // a wide round: the grid expands it (its moves spread over many waves)
         ex = SX_GRID;
+#if S2LC_SOLO_REGRUN
+        flush();  // (before the writes below: the grid round's slices read last_closed)
+#endif
         if (lane == 0) { R.solo_skip = r; R.last_nf = 1; R.last_closed = tot; }
         break;
       }
@@ -638,8 +674,32 @@ __device__ __attribute__((noinline)) uint32_t lv_solo_wave(const SoloArgs pa, Lv
 #ifdef S2LC_PROF
     pf_dead += n_dead;
 #endif
+    const bool carry = !found && !ovf && alive == 1;
+#if S2LC_SOLO_REGRUN
+    if (carry) {
+      // lv_close_state for one new configuration, on the registers
+      g_ch += kids;
+      g_round = r;
+      g_cfg += 1;
+      if (g_wit) {
+        g_ltb = (uint32_t)g_tnext;
+        g_tnext += 1;
+        if (g_tnext + p.scap > p.trace_cap) g_wit = 0;
+      }
+      if (g_maxc && g_cfg > g_maxc) g_done = LVR_BUDGET;
+      ++nfast;
+      if (lane == 0) {
+        if (p.rcounts) lv_gst32(p.rcounts + r, 1u);
+        if (wit) lv_gst64(p.trace + tbase, (unsigned long long)kmv << 32 | ptrace);
+      }
+    } else {
+      flush();
+    }
+    if (!carry && lane == 0) {
+#else
     // close the round on the run state (lane 0; every lane reads it back)
     if (lane == 0) {
+#endif
       LvCounts kc;
       kc.nn = alive; kc.ovf = ovf; kc.fnd = found;
       kc.fpar = fpar; kc.fmov = fmov; kc.fp4 = fp4; kc.ch = kids; kc.closed = 0;
@@ -653,7 +713,9 @@ __device__ __attribute__((noinline)) uint32_t lv_solo_wave(const SoloArgs pa, Lv
       if (p.prof) { atomicAdd(&p.prof[29], (unsigned long long)alive); atomicAdd(&p.prof[30], alive == 1 ? 1ull : 0ull); }
 #endif
     }
-    const bool carry = !found && !ovf && alive == 1;
+#if S2LC_SOLO_REGRUN && defined(S2LC_PROF)
+    if (carry && lane == 0 && p.prof) { atomicAdd(&p.prof[29], 1ull); atomicAdd(&p.prof[30], 1ull); }
+#endif
     if (carry) {
       // the kept child becomes the configuration: its advanced chains into
       // LDS (early loads; a lane with two advanced slots loads them now) and
@@ -691,12 +753,19 @@ __device__ __attribute__((noinline)) uint32_t lv_solo_wave(const SoloArgs pa, Lv
     }
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // (lane 0's close, read back by every lane)
     LV_SOLO_T(4);
+#if S2LC_SOLO_REGRUN
+    const uint32_t done = carry ? g_done : uni32(R.done), nf = carry ? 1u : uni32(R.nf);
+#else
     const uint32_t done = uni32(R.done), nf = uni32(R.nf);
+#endif
     if (found || done != LVR_RUNNING) { ex = (ovf && !found) ? SX_OVF : SX_END; break; }
     if (alive >= 2) { ex = SX_STAGED; xtrace = wit ? p.tgid + tbase : TRACE_NONE; break; }
     if (nf != 1) { ex = SX_END; break; }
     if (n + 1 >= p.max_rounds) { ex = SX_MAX; break; }
   }
+#if S2LC_SOLO_REGRUN
+  flush();
+#endif
   // leave the configuration (and the kept child) in S for the phase's exit writes
   if (ex != SX_END) {
     uint32_t z[NQ];
