@@ -467,20 +467,22 @@ __device__ __attribute__((noinline)) uint32_t lv_solo_wave(const SoloArgs pa, Lv
     for (int q = 0; q < NQ; ++q) {
       const uint32_t nr = a_nr[q], msn = a_msn[q], toks = a_toks[q], otl = a_ot[q], nxs = a_nxs[q];
       const uint32_t fl = hfl[q];
-      const bool cand = !(fl & (OPF_SENTINEL | OPF_CLS_E)) && hcall[q] < pmin;
+      // (bitwise & | on the conditions, not && ||: the short-circuit forms
+      // were compiled into exec-mask branches per slot)
+      const bool cand = ((fl & (OPF_SENTINEL | OPF_CLS_E)) == 0) & (hcall[q] < pmin);
       const uint32_t bt = toks & 0xFFFFu, st = toks >> 16;
-      const bool g = (bt == 0 || (ptok != 0 && ptok == bt)) && (!(fl & OPF_HAS_MSN) || msn == ptail);
+      const bool g = ((bt == 0) | ((ptok != 0) & (ptok == bt))) & (((fl & OPF_HAS_MSN) == 0) | (msn == ptail));
       const uint32_t ot = ptail + nr;  // (no wrap under H_TAIL32)
-      const bool to = (fl & OPF_CLS_D) ? (g && ot == otl) : g;
+      const bool to = g & (((fl & OPF_CLS_D) == 0) | (ot == otl));
       const uint32_t others = hsuf[q] == b1 ? b2 : b1;
-      const bool dead = p1 && to && ot > min(others, nxs);
-      const bool tip = (fl & OPF_CLS_I) && (!idefer || hret[q] == pmin);
-      const bool eqn = g && nr == 0 && (st ? st : ptok) == ptok;
+      const bool dead = p1 & to & (ot > min(others, nxs));
+      const bool tip = ((fl & OPF_CLS_I) != 0) & (!idefer | (hret[q] == pmin));
+      const bool eqn = g & (nr == 0) & ((st == 0) | (st == ptok));
       const uint32_t bit = cand ? 1u << q : 0u;
-      b_opt |= (to && !dead) ? bit : 0u;
+      b_opt |= (to & !dead) ? bit : 0u;
       b_tip |= tip ? bit : 0u;
-      b_eqn |= (tip && eqn) ? bit : 0u;
-      n_dead += (uint32_t)__popcll(__ballot(cand && dead));
+      b_eqn |= (tip & eqn) ? bit : 0u;
+      n_dead += (uint32_t)__popcll(__ballot(cand & dead));
     }
     uint32_t b_live = b_opt | b_tip;
     LV_SOLO_T(2);
