@@ -103,6 +103,9 @@ struct LvSolo {
 #endif
 };
 
+// (the ballot builtin on a bool: HIP's __ballot(int) had the compiler
+// materialize the condition as 0 / 1 in a VGPR and compare it again)
+__device__ __forceinline__ uint64_t wballot(bool b) { return __builtin_amdgcn_ballot_w64(b); }
 __device__ __forceinline__ uint32_t uni32(uint32_t v) { return (uint32_t)__builtin_amdgcn_readfirstlane((int)v); }
 __device__ __forceinline__ uint64_t uni64(uint64_t v) {
   return ((uint64_t)uni32((uint32_t)(v >> 32)) << 32) | uni32((uint32_t)v);
@@ -147,14 +150,14 @@ __device__ __forceinline__ void wave_min2_32(const uint32_t (&v)[NQ], uint32_t& 
 struct SoloKeys { uint32_t ekey, dkey; };
 __device__ __forceinline__ SoloKeys solo_keys(uint32_t fl, uint32_t call, uint32_t ot, uint64_t oh, uint32_t t,
                                               uint64_t h, bool p2) {
-  const bool e = fl & OPF_CLS_E;
+  const bool e = (fl & OPF_CLS_E) != 0;
   const bool defin = (fl & OPF_KIND_MASK) == 0;  // a definite append failure (the only E append): {s}
-  const bool fail = fl & OPF_FAIL;
-  const bool hash_bad = (fl & OPF_HAS_HASH) && h != oh;
+  const bool fail = (fl & OPF_FAIL) != 0;
+  const bool hash_bad = ((fl & OPF_HAS_HASH) != 0) & (h != oh);
   const bool tail_eq = ot == t;
-  const bool legal = defin || (!hash_bad && (fail || tail_eq));
-  const bool p2d = p2 && !defin && hash_bad && !fail && tail_eq;
-  return SoloKeys{(e && legal) ? call : EV_INF, (e && p2d) ? call : EV_INF};
+  const bool legal = defin | (!hash_bad & (fail | tail_eq));
+  const bool p2d = p2 & !defin & hash_bad & !fail & tail_eq;
+  return SoloKeys{(e & legal) ? call : EV_INF, (e & p2d) ? call : EV_INF};
 }
 
 // A head's first 8 record hashes (range [ho, ho + hc)), loaded together:
@@ -451,7 +454,7 @@ __device__ __attribute__((noinline)) uint32_t lv_solo_wave(const SoloArgs pa, Lv
     // masks over the slots: opt child to close, identity child possible
     // (I-op, deferral), the identity child's existence needs the fold (opt ==
     // s on everything but the hash).
-    uint32_t b_opt = 0, b_tip = 0, b_eqn = 0, n_dead = 0;
+    uint32_t b_opt = 0, b_tip = 0, b_eqn = 0, b_dead = 0;
     // every slot's values read first, with one wait for all of them: a value
     // only some lanes need (msn) would otherwise be loaded under a branch,
     // one LDS round trip after another
@@ -482,18 +485,22 @@ __device__ __attribute__((noinline)) uint32_t lv_solo_wave(const SoloArgs pa, Lv
       b_opt |= (to & !dead) ? bit : 0u;
       b_tip |= tip ? bit : 0u;
       b_eqn |= (tip & eqn) ? bit : 0u;
-      n_dead += (uint32_t)__popcll(__ballot(cand & dead));
+      b_dead |= (cand & dead) ? bit : 0u;
     }
     uint32_t b_live = b_opt | b_tip;
     LV_SOLO_T(2);
+    uint32_t n_dead, tot;
     {
-      // live moves of the round (a wave-wide sum of the per-lane counts)
-      uint32_t c = (uint32_t)__popc(b_live);
+      // live moves of the round and P1-dead opt children (wave-wide sums of
+      // the per-lane counts, one reduction: 16 bits each, at most 320)
+      uint32_t c = (uint32_t)__popc(b_live) | ((uint32_t)__popc(b_dead) << 16);
       c += lv_dpp<0xB1>(c);
       c += lv_dpp<0x4E>(c);
       c += lv_dpp<0x124>(c);
       c += lv_dpp<0x128>(c);
-      const uint32_t tot = rl(c, 0) + rl(c, 16) + rl(c, 32) + rl(c, 48);
+      const uint32_t sum = rl(c, 0) + rl(c, 16) + rl(c, 32) + rl(c, 48);
+      tot = sum & 0xFFFFu;
+      n_dead = sum >> 16;
       if (tot > p.max_live) {
         // a wide round: the grid expands it (its moves spread over many waves)
         ex = SX_GRID;
@@ -509,7 +516,7 @@ __device__ __attribute__((noinline)) uint32_t lv_solo_wave(const SoloArgs pa, Lv
     uint32_t alive = 0, found = 0, ovf = 0, fpar = 0, fmov = 0, fp4 = 0;
     unsigned long long kids = n_dead;  // (P1-dead opt children: counted, never closed)
     for (;;) {
-      const uint64_t m = __ballot(b_live != 0);
+      const uint64_t m = wballot(b_live != 0);
       if (m == 0 || found) break;
       const int src = __ffsll((unsigned long long)m) - 1;
       const uint32_t lb = rl(b_live, src);
@@ -591,14 +598,14 @@ __device__ __attribute__((noinline)) uint32_t lv_solo_wave(const SoloArgs pa, Lv
           for (int q = 0; q < NQ; ++q) {
             mr = min(mr, cret[q]);
             advb |= ek[q] < mprev ? 1u << q : 0u;
-            bad |= (dk[q] < mprev || (p1 && csuf[q] < ct)) ? 1u : 0u;
+            bad |= (uint32_t)((dk[q] < mprev) | (p1 & (csuf[q] < ct)));
           }
           minret = wave_min_u32(mr);
 #ifdef S2LC_PROF
           if (lane == 0) S.pc[4] += 1;
 #endif
-          if (__ballot(bad != 0)) { res = CL_DEAD; break; }
-          const uint64_t am = __ballot(advb != 0);
+          if (wballot(bad != 0)) { res = CL_DEAD; break; }
+          const uint64_t am = wballot(advb != 0);
           if (am == 0 && minret == mprev) {
             if (minret == EV_INF) {
               res = CL_COMPLETE;
@@ -606,21 +613,21 @@ __device__ __attribute__((noinline)) uint32_t lv_solo_wave(const SoloArgs pa, Lv
               bool con = false;  // P4: no pending op constrains the state
 #pragma unroll
               for (int q = 0; q < NQ; ++q) con |= csuf[q] != 0xFFFFFFFFu;
-              res = (p4 && __ballot(con) == 0) ? CL_P4 : CL_ALIVE;
+              res = (p4 && wballot(con) == 0) ? CL_P4 : CL_ALIVE;
             }
             break;
           }
 #pragma unroll
           for (int q = 0; q < NQ; ++q) {
             const bool a = (advb >> q) & 1u;
-            if (__ballot(a) == 0) continue;
+            if (wballot(a) == 0) continue;
             // the head after the current one: the next record (LDS) after
             // the parent's head, else a load (a chain advanced twice: rare)
             const uint32_t jq = (uint32_t)(64 * q + lane);
             uint32_t n_call = NX.call[jq], n_ret = NX.ret[jq], n_fl = NX.fl[jq], n_suf = NX.suf[jq], n_ot = NX.ot[jq];
             uint64_t n_oh = NX.oh[jq];
             const bool gl = a && d[q] != 0;
-            if (__ballot(gl)) {
+            if (wballot(gl)) {
               if (gl) {
                 const SoloHead hh = lv_solo_load_head(p.recs + s_cs[jq] + S.cnt[jq] + d[q] + 1);
                 n_fl = hh.fl; n_ot = hh.ot; n_oh = hh.oh; n_suf = hh.suf; n_call = hh.call; n_ret = hh.ret;
@@ -740,7 +747,7 @@ __device__ __attribute__((noinline)) uint32_t lv_solo_wave(const SoloArgs pa, Lv
       asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
 #pragma unroll
       for (int q = 0; q < NQ; ++q) {
-        if (!__ballot(kd[q] != 0)) continue;
+        if (!wballot(kd[q] != 0)) continue;
         if (kd[q]) {
           const uint32_t jq = (uint32_t)(64 * q + lane);
           hcall[q] = PL.call[jq];
