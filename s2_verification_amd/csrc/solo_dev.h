@@ -52,6 +52,11 @@
 #endif
 // After a carry, touch the records the advanced chains' next advance will
 // load (S2LC_SOLO_TOUCH=0 turns it off; profiles/r06/solo_touch_ab.txt)
+// After a carry, the advanced heads' closure fields from the registers the
+// reload loaded them into (1) or read back from LDS (0)
+#ifndef S2LC_SOLO_REGHEAD
+#define S2LC_SOLO_REGHEAD 1
+#endif
 #ifndef S2LC_SOLO_TOUCH
 #define S2LC_SOLO_TOUCH 1
 #endif
@@ -220,7 +225,8 @@ __device__ __forceinline__ void lv_touch(const void* g, uint32_t* sink) {
 template <int NQ>
 __device__ __forceinline__ void lv_solo_head(const uint64_t* pool, const OpRec* h, const OpRec* end, uint32_t j,
                                              bool known, LvSoloHeads<NQ>& PL, LvSoloHeads<NQ>& NX,
-                                             LvSoloExt<NQ>& FR, LvSolo<NQ>& S, bool touch = false) {
+                                             LvSoloExt<NQ>& FR, LvSolo<NQ>& S, bool touch = false,
+                                             uint32_t* head4 = nullptr) {
   const uint4* a = reinterpret_cast<const uint4*>(h);
   const uint4* b = reinterpret_cast<const uint4*>(h + 1 < end ? h + 1 : h);  // (the sentinel has no next record)
   const uint4 x0 = lv_gld16(a), x1 = lv_gld16(a + 1), x2 = lv_gld16(a + 2), x3 = lv_gld16(a + 3);
@@ -229,6 +235,12 @@ __device__ __forceinline__ void lv_solo_head(const uint64_t* pool, const OpRec* 
   if (known) lv_solo_hashes(pool, S.nx_hoff[j], S.nx_hcnt[j], hv);
   else lv_solo_hashes(pool, x3.x, x3.y, hv);
   lv_solo_head_put<NQ>(x0, x1, x2, x3, y1, y2, y3, hv, j, PL, NX, FR, S);
+  if (head4) {  // the head's closure fields (call, ret, flags, P1 bound), as put
+    head4[0] = x2.z;
+    head4[1] = x2.w;
+    head4[2] = x3.w;
+    head4[3] = suf32((uint64_t)x2.x | ((uint64_t)x2.y << 32));
+  }
 #if S2LC_SOLO_TOUCH
   if (touch) {
     // what this chain's next advance loads (the record after the next one,
@@ -733,18 +745,43 @@ __device__ __attribute__((noinline)) uint32_t lv_solo_wave(const SoloArgs pa, Lv
 #pragma unroll
       for (int q = 0; q < NQ; ++q)
         if (kd[q]) { ++nmine; qm = (uint32_t)q; }
+      uint32_t h4[4] = {0u, 0u, 0u, 0u};
       if (nmine == 1) {
         const uint32_t jj = (uint32_t)lane + 64u * qm, dd = sel_u32<NQ>(kd, qm);
         const uint32_t c = (uint32_t)S.cnt[jj] + dd;
         S.cnt[jj] = (uint16_t)c;
         lv_solo_head<NQ>(p.pool, p.recs + s_cs[jj] + c, p.recs + (jj + 1 < K ? s_cs[jj + 1] : S.cs_end), jj, dd == 1,
-                         PL, NX, FR, S, true);
+                         PL, NX, FR, S, true, S2LC_SOLO_REGHEAD ? h4 : nullptr);
       } else if (nmine > 1) {
 #pragma unroll
         for (int q = 0; q < NQ; ++q) S.keep[lane + 64 * q] = (uint16_t)kd[q];
         lv_solo_reload_lane<NQ>(p.recs, p.pool, s_cs, K, PL, NX, FR, S);
       }
       asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+#if S2LC_SOLO_REGHEAD
+      // a lane's one advanced slot: its closure fields from the record
+      // registers (selects); two or more: read back from LDS (rare)
+#pragma unroll
+      for (int q = 0; q < NQ; ++q) {
+        const bool one = (nmine == 1) & (qm == (uint32_t)q);
+        hcall[q] = one ? h4[0] : hcall[q];
+        hret[q] = one ? h4[1] : hret[q];
+        hfl[q] = one ? h4[2] : hfl[q];
+        hsuf[q] = one ? h4[3] : hsuf[q];
+      }
+      if (wballot(nmine > 1)) {
+#pragma unroll
+        for (int q = 0; q < NQ; ++q) {
+          if ((nmine > 1) & (kd[q] != 0)) {
+            const uint32_t jq = (uint32_t)(64 * q + lane);
+            hcall[q] = PL.call[jq];
+            hret[q] = PL.ret[jq];
+            hfl[q] = PL.fl[jq];
+            hsuf[q] = PL.suf[jq];
+          }
+        }
+      }
+#else
 #pragma unroll
       for (int q = 0; q < NQ; ++q) {
         if (!wballot(kd[q] != 0)) continue;
@@ -756,6 +793,7 @@ __device__ __attribute__((noinline)) uint32_t lv_solo_wave(const SoloArgs pa, Lv
           hsuf[q] = PL.suf[jq];
         }
       }
+#endif
       ptail = ktail; phash = khash; ptok = ktok; pmin = kmr;
       ptrace = wit ? p.tgid + tbase : TRACE_NONE;
       chx_ok = false;
