@@ -54,6 +54,9 @@
 // load (S2LC_SOLO_TOUCH=0 turns it off; profiles/r06/solo_touch_ab.txt)
 // After a carry, the advanced heads' closure fields from the registers the
 // reload loaded them into (1) or read back from LDS (0)
+#ifndef S2LC_SOLO_NOHOIST
+#define S2LC_SOLO_NOHOIST 1
+#endif
 #ifndef S2LC_SOLO_REGHEAD
 #define S2LC_SOLO_REGHEAD 1
 #endif
@@ -585,7 +588,16 @@ __device__ __attribute__((noinline)) uint32_t lv_solo_wave(const SoloArgs pa, Lv
         for (int q = 0; q < NQ; ++q) {
           const uint32_t jq = (uint32_t)(64 * q + lane);
           const bool mvd = (uint32_t)q == q_cur && lane == src;
+#if S2LC_SOLO_NOHOIST
+          // (an opaque copy of the flags: the compiler would hoist their
+          // per-slot tests out of the move loop, which runs ~1.1 times a
+          // round, and hold ~20 VGPRs and 10 SGPR masks across it)
+          uint32_t flq = hfl[q];
+          asm volatile("" : "+v"(flq));
+          const SoloKeys k0 = solo_keys(flq, hcall[q], PL.ot[jq], PL.oh[jq], ct, ch, p2);
+#else
           const SoloKeys k0 = solo_keys(hfl[q], hcall[q], PL.ot[jq], PL.oh[jq], ct, ch, p2);
+#endif
           ccall[q] = mvd ? nx_call : hcall[q];
           cret[q] = mvd ? nx_ret : hret[q];
           csuf[q] = mvd ? nx_suf : hsuf[q];
