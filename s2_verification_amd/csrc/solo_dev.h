@@ -412,12 +412,7 @@ __device__ __attribute__((noinline)) uint32_t lv_solo_wave(const SoloArgs pa, Lv
     hfl[q] = PL.fl[j];
     hsuf[q] = PL.suf[j];
   }
-  uint32_t kd[NQ];  // the kept child's advance per slot
-#pragma unroll
-  for (int q = 0; q < NQ; ++q) kd[q] = 0;
   uint32_t ex = SX_END;
-  uint32_t ktail = ptail, ktok = ptok, kmr = 0, kmv = 0, xtrace = TRACE_NONE;  // the kept child
-  uint64_t khash = phash;
 #ifdef S2LC_PROF
   unsigned long long pf_closures = 0, pf_dead = 0;
 #endif
@@ -426,13 +421,18 @@ __device__ __attribute__((noinline)) uint32_t lv_solo_wave(const SoloArgs pa, Lv
   // one new configuration, no overflow, not found), wave-uniform; R is behind
   // by `nfast` such closes until flush() writes them back (lane 0)
   uint32_t g_round = uni32(R.round), g_wit = uni32(R.witness), g_ltb = uni32(R.last_tbase), g_done = uni32(R.done);
-  uint64_t g_tnext = uni64(R.tnext), g_cfg = uni64(R.configs), g_ch = 0;
-  const uint64_t g_maxc = uni64(R.max_configs);
-  uint32_t nfast = 0;
+  uint64_t g_tnext = uni64(R.tnext), g_ch = 0;
+  uint32_t nfast = 0;  // (each adds one configuration: R.configs += nfast)
+  // fast rounds the budget allows (lv_close_state: configs > max_configs)
+  uint32_t fast_cap;
+  {
+    const uint64_t mc = uni64(R.max_configs), cf = uni64(R.configs);
+    fast_cap = !mc ? 0xFFFFFFFFu : cf >= mc ? 0u : (uint32_t)min<uint64_t>(mc - cf, 0xFFFFFFFFull);
+  }
   auto flush = [&]() {
     if (nfast && lane == 0) {
       R.round = g_round; R.witness = g_wit; R.last_tbase = g_ltb; R.done = g_done;
-      R.tnext = g_tnext; R.configs = g_cfg; R.children += g_ch;
+      R.tnext = g_tnext; R.configs += nfast; R.children += g_ch;
       R.nf = 1; R.last_nf = 1; R.last_closed = 0; R.max_frontier = max(R.max_frontier, 1u);
       R.solo_rounds += nfast;
     }
@@ -527,8 +527,14 @@ __device__ __attribute__((noinline)) uint32_t lv_solo_wave(const SoloArgs pa, Lv
       }
     }
 
-    // the moves with a child to close
+    // the moves with a child to close; the first survivor (the kept child:
+    // the next configuration when it is the only one) stays in registers
     uint32_t alive = 0, found = 0, ovf = 0, fpar = 0, fmov = 0, fp4 = 0;
+    uint32_t kd[NQ];  // the kept child's advance per slot
+#pragma unroll
+    for (int q = 0; q < NQ; ++q) kd[q] = 0;
+    uint32_t ktail = ptail, ktok = ptok, kmr = 0, kmv = 0;
+    uint64_t khash = phash;
     unsigned long long kids = n_dead;  // (P1-dead opt children: counted, never closed)
     for (;;) {
       const uint64_t m = wballot(b_live != 0);
@@ -713,14 +719,13 @@ __device__ __attribute__((noinline)) uint32_t lv_solo_wave(const SoloArgs pa, Lv
       // lv_close_state for one new configuration, on the registers
       g_ch += kids;
       g_round = r;
-      g_cfg += 1;
       if (g_wit) {
         g_ltb = (uint32_t)g_tnext;
         g_tnext += 1;
         if (g_tnext + p.scap > p.trace_cap) g_wit = 0;
       }
-      if (g_maxc && g_cfg > g_maxc) g_done = LVR_BUDGET;
       ++nfast;
+      if (nfast > fast_cap) g_done = LVR_BUDGET;
       if (lane == 0) {
         if (p.rcounts) lv_gst32(p.rcounts + r, 1u);
         if (wit) lv_gst64(p.trace + tbase, (unsigned long long)kmv << 32 | ptrace);
@@ -818,7 +823,19 @@ __device__ __attribute__((noinline)) uint32_t lv_solo_wave(const SoloArgs pa, Lv
     const uint32_t done = uni32(R.done), nf = uni32(R.nf);
 #endif
     if (found || done != LVR_RUNNING) { ex = (ovf && !found) ? SX_OVF : SX_END; break; }
-    if (alive >= 2) { ex = SX_STAGED; xtrace = wit ? p.tgid + tbase : TRACE_NONE; break; }
+    if (alive >= 2) {
+      // the kept child joins the staged ones at the phase's exit (S.keep, S.k*)
+      ex = SX_STAGED;
+      const uint64_t kx = lv_solo_chx<NQ>(S, K, kd);
+#pragma unroll
+      for (int q = 0; q < NQ; ++q) S.keep[lane + 64 * q] = (uint16_t)kd[q];
+      if (lane == 0) {
+        S.kchx = kx;
+        S.ktail = ktail; S.khash = khash; S.ktok = ktok; S.kmr = kmr; S.kmv = kmv;
+        S.xtrace = wit ? p.tgid + tbase : TRACE_NONE;
+      }
+      break;
+    }
     if (nf != 1) { ex = SX_END; break; }
     if (n + 1 >= p.max_rounds) { ex = SX_MAX; break; }
   }
@@ -833,16 +850,6 @@ __device__ __attribute__((noinline)) uint32_t lv_solo_wave(const SoloArgs pa, Lv
     if (!chx_ok) {
       const uint64_t x = lv_solo_chx<NQ>(S, K, z);
       if (lane == 0) S.chx = x;
-    }
-    if (ex == SX_STAGED) {
-      const uint64_t kx = lv_solo_chx<NQ>(S, K, kd);
-#pragma unroll
-      for (int q = 0; q < NQ; ++q) S.keep[lane + 64 * q] = (uint16_t)kd[q];
-      if (lane == 0) {
-        S.kchx = kx;
-        S.ktail = ktail; S.khash = khash; S.ktok = ktok; S.kmr = kmr; S.kmv = kmv;
-        S.xtrace = xtrace;
-      }
     }
   }
   if (lane == 0) {
