@@ -22,7 +22,7 @@
 //   - the configuration lives in LDS (structure of arrays, conflict-free):
 //     every chain's head (closure fields, the move's fields, its first 8
 //     record hashes) and the record after it (a child's first new head on
-//     that chain); the heads' closure fields also stay in registers. Only the
+//     that chain), read by each round once, with one wait. Only the
 //     chains the surviving child advanced are reloaded, at the carry; each
 //     reload then touches what that chain's next advance will load (the
 //     record after the next one, the next one's record hashes) with loads
@@ -50,16 +50,14 @@
 #ifndef S2LC_SOLO_REGRUN
 #define S2LC_SOLO_REGRUN 1
 #endif
-// After a carry, touch the records the advanced chains' next advance will
-// load (S2LC_SOLO_TOUCH=0 turns it off; profiles/r06/solo_touch_ab.txt)
-// After a carry, the advanced heads' closure fields from the registers the
-// reload loaded them into (1) or read back from LDS (0)
+// The child setup's flag tests kept in the move loop (an opaque copy of each
+// slot's flags; S2LC_SOLO_NOHOIST=0 lets the compiler hoist them out of it:
+// profiles/r06/solo_nohoist_ab.txt)
 #ifndef S2LC_SOLO_NOHOIST
 #define S2LC_SOLO_NOHOIST 1
 #endif
-#ifndef S2LC_SOLO_REGHEAD
-#define S2LC_SOLO_REGHEAD 1
-#endif
+// After a carry, touch the records the advanced chains' next advance will
+// load (S2LC_SOLO_TOUCH=0 turns it off; profiles/r06/solo_touch_ab.txt)
 #ifndef S2LC_SOLO_TOUCH
 #define S2LC_SOLO_TOUCH 1
 #endif
@@ -228,8 +226,7 @@ __device__ __forceinline__ void lv_touch(const void* g, uint32_t* sink) {
 template <int NQ>
 __device__ __forceinline__ void lv_solo_head(const uint64_t* pool, const OpRec* h, const OpRec* end, uint32_t j,
                                              bool known, LvSoloHeads<NQ>& PL, LvSoloHeads<NQ>& NX,
-                                             LvSoloExt<NQ>& FR, LvSolo<NQ>& S, bool touch = false,
-                                             uint32_t* head4 = nullptr) {
+                                             LvSoloExt<NQ>& FR, LvSolo<NQ>& S, bool touch = false) {
   const uint4* a = reinterpret_cast<const uint4*>(h);
   const uint4* b = reinterpret_cast<const uint4*>(h + 1 < end ? h + 1 : h);  // (the sentinel has no next record)
   const uint4 x0 = lv_gld16(a), x1 = lv_gld16(a + 1), x2 = lv_gld16(a + 2), x3 = lv_gld16(a + 3);
@@ -238,12 +235,6 @@ __device__ __forceinline__ void lv_solo_head(const uint64_t* pool, const OpRec* 
   if (known) lv_solo_hashes(pool, S.nx_hoff[j], S.nx_hcnt[j], hv);
   else lv_solo_hashes(pool, x3.x, x3.y, hv);
   lv_solo_head_put<NQ>(x0, x1, x2, x3, y1, y2, y3, hv, j, PL, NX, FR, S);
-  if (head4) {  // the head's closure fields (call, ret, flags, P1 bound), as put
-    head4[0] = x2.z;
-    head4[1] = x2.w;
-    head4[2] = x3.w;
-    head4[3] = suf32((uint64_t)x2.x | ((uint64_t)x2.y << 32));
-  }
 #if S2LC_SOLO_TOUCH
   if (touch) {
     // what this chain's next advance loads (the record after the next one,
@@ -403,15 +394,6 @@ __device__ __attribute__((noinline)) uint32_t lv_solo_wave(const SoloArgs pa, Lv
   uint32_t ptail = tail32(uni64(S.tail)), ptok = uni32(S.tok), pmin = uni32(S.pmin), ptrace = uni32(S.ptrace);
   uint64_t phash = uni64(S.hash);
   bool chx_ok = true;  // S.chx is the configuration's (false after a carry: recomputed on demand)
-  uint32_t hcall[NQ], hret[NQ], hfl[NQ], hsuf[NQ];
-#pragma unroll
-  for (int q = 0; q < NQ; ++q) {
-    const uint32_t j = (uint32_t)(64 * q + lane);
-    hcall[q] = PL.call[j];
-    hret[q] = PL.ret[j];
-    hfl[q] = PL.fl[j];
-    hsuf[q] = PL.suf[j];
-  }
   uint32_t ex = SX_END;
 #ifdef S2LC_PROF
   unsigned long long pf_closures = 0, pf_dead = 0;
@@ -457,6 +439,23 @@ __device__ __attribute__((noinline)) uint32_t lv_solo_wave(const SoloArgs pa, Lv
       ex = SX_END;
       break;
     }
+    // the heads' closure fields and the precheck's values, read from LDS at
+    // the round's start with one wait (held in registers across rounds, they
+    // cost the loop ~30 back-edge copies and a register update per carry:
+    // profiles/r06/solo_ldsheads_ab.txt)
+    uint32_t hcall[NQ], hret[NQ], hfl[NQ], hsuf[NQ];
+    uint32_t a_nr[NQ], a_msn[NQ], a_toks[NQ], a_ot[NQ], a_nxs[NQ];
+#pragma unroll
+    for (int q = 0; q < NQ; ++q) {
+      const uint32_t j = (uint32_t)(64 * q + lane);
+      hcall[q] = PL.call[j]; hret[q] = PL.ret[j]; hfl[q] = PL.fl[j]; hsuf[q] = PL.suf[j];
+      a_nr[q] = FR.nr[j]; a_msn[q] = FR.msn[j]; a_toks[q] = FR.toks[j]; a_ot[q] = PL.ot[j]; a_nxs[q] = NX.suf[j];
+    }
+#pragma unroll
+    for (int q = 0; q < NQ; ++q) {
+      asm volatile("" : "+v"(hcall[q]), "+v"(hret[q]), "+v"(hfl[q]), "+v"(hsuf[q]));
+      asm volatile("" : "+v"(a_nr[q]), "+v"(a_msn[q]), "+v"(a_toks[q]), "+v"(a_ot[q]), "+v"(a_nxs[q]));
+    }
     LV_SOLO_T(0);
     // P1: a child's bound is the parent's with the moved chain's head
     // replaced by its next record, so (smallest, second smallest) over all
@@ -473,14 +472,6 @@ __device__ __attribute__((noinline)) uint32_t lv_solo_wave(const SoloArgs pa, Lv
     // every slot's values read first, with one wait for all of them: a value
     // only some lanes need (msn) would otherwise be loaded under a branch,
     // one LDS round trip after another
-    uint32_t a_nr[NQ], a_msn[NQ], a_toks[NQ], a_ot[NQ], a_nxs[NQ];
-#pragma unroll
-    for (int q = 0; q < NQ; ++q) {
-      const uint32_t j = (uint32_t)(64 * q + lane);
-      a_nr[q] = FR.nr[j]; a_msn[q] = FR.msn[j]; a_toks[q] = FR.toks[j]; a_ot[q] = PL.ot[j]; a_nxs[q] = NX.suf[j];
-    }
-#pragma unroll
-    for (int q = 0; q < NQ; ++q) asm volatile("" : "+v"(a_nr[q]), "+v"(a_msn[q]), "+v"(a_toks[q]), "+v"(a_ot[q]), "+v"(a_nxs[q]));
 #pragma unroll
     for (int q = 0; q < NQ; ++q) {
       const uint32_t nr = a_nr[q], msn = a_msn[q], toks = a_toks[q], otl = a_ot[q], nxs = a_nxs[q];
@@ -762,55 +753,18 @@ __device__ __attribute__((noinline)) uint32_t lv_solo_wave(const SoloArgs pa, Lv
 #pragma unroll
       for (int q = 0; q < NQ; ++q)
         if (kd[q]) { ++nmine; qm = (uint32_t)q; }
-      uint32_t h4[4] = {0u, 0u, 0u, 0u};
       if (nmine == 1) {
         const uint32_t jj = (uint32_t)lane + 64u * qm, dd = sel_u32<NQ>(kd, qm);
         const uint32_t c = (uint32_t)S.cnt[jj] + dd;
         S.cnt[jj] = (uint16_t)c;
         lv_solo_head<NQ>(p.pool, p.recs + s_cs[jj] + c, p.recs + (jj + 1 < K ? s_cs[jj + 1] : S.cs_end), jj, dd == 1,
-                         PL, NX, FR, S, true, S2LC_SOLO_REGHEAD ? h4 : nullptr);
+                         PL, NX, FR, S, true);
       } else if (nmine > 1) {
 #pragma unroll
         for (int q = 0; q < NQ; ++q) S.keep[lane + 64 * q] = (uint16_t)kd[q];
         lv_solo_reload_lane<NQ>(p.recs, p.pool, s_cs, K, PL, NX, FR, S);
       }
       asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-#if S2LC_SOLO_REGHEAD
-      // a lane's one advanced slot: its closure fields from the record
-      // registers (selects); two or more: read back from LDS (rare)
-#pragma unroll
-      for (int q = 0; q < NQ; ++q) {
-        const bool one = (nmine == 1) & (qm == (uint32_t)q);
-        hcall[q] = one ? h4[0] : hcall[q];
-        hret[q] = one ? h4[1] : hret[q];
-        hfl[q] = one ? h4[2] : hfl[q];
-        hsuf[q] = one ? h4[3] : hsuf[q];
-      }
-      if (wballot(nmine > 1)) {
-#pragma unroll
-        for (int q = 0; q < NQ; ++q) {
-          if ((nmine > 1) & (kd[q] != 0)) {
-            const uint32_t jq = (uint32_t)(64 * q + lane);
-            hcall[q] = PL.call[jq];
-            hret[q] = PL.ret[jq];
-            hfl[q] = PL.fl[jq];
-            hsuf[q] = PL.suf[jq];
-          }
-        }
-      }
-#else
-#pragma unroll
-      for (int q = 0; q < NQ; ++q) {
-        if (!wballot(kd[q] != 0)) continue;
-        if (kd[q]) {
-          const uint32_t jq = (uint32_t)(64 * q + lane);
-          hcall[q] = PL.call[jq];
-          hret[q] = PL.ret[jq];
-          hfl[q] = PL.fl[jq];
-          hsuf[q] = PL.suf[jq];
-        }
-      }
-#endif
       ptail = ktail; phash = khash; ptok = ktok; pmin = kmr;
       ptrace = wit ? p.tgid + tbase : TRACE_NONE;
       chx_ok = false;
