@@ -550,6 +550,10 @@ __device__ __attribute__((noinline)) uint32_t lv_solo_wave(const SoloArgs pa, Lv
       for (int k = 0; k < LV_SOLO_HP2; ++k) hv[LV_SOLO_HP + k] = FR.hp2[k][j];
       const uint32_t nx_call = NX.call[j], nx_ret = NX.ret[j], nx_fl = NX.fl[j], nx_suf = NX.suf[j], nx_ot = NX.ot[j];
       const uint64_t nx_oh = NX.oh[j];
+      // (all 8 hash loads issued here, with the move's other reads: the
+      // compiler sank the first one into the fold, a wait of its own)
+#pragma unroll
+      for (int k = 0; k < LV_SOLO_HPT; ++k) asm volatile("" : "+v"(hv[k]));
       const uint32_t otail = ptail + nr, otok = (toks >> 16) ? (toks >> 16) : ptok;
       uint64_t ohash = phash;
       if (m_opt || m_eqn) {
@@ -591,7 +595,7 @@ __device__ __attribute__((noinline)) uint32_t lv_solo_wave(const SoloArgs pa, Lv
           // round, and hold ~20 VGPRs and 10 SGPR masks across it)
           uint32_t flq = hfl[q];
           asm volatile("" : "+v"(flq));
-          const SoloKeys k0 = solo_keys(flq, hcall[q], PL.ot[jq], PL.oh[jq], ct, ch, p2);
+          const SoloKeys k0 = solo_keys(flq, hcall[q], a_ot[q], PL.oh[jq], ct, ch, p2);  // (a_ot: PL.ot, read at the round's start)
 #else
           const SoloKeys k0 = solo_keys(hfl[q], hcall[q], PL.ot[jq], PL.oh[jq], ct, ch, p2);
 #endif
