@@ -5,7 +5,7 @@ set -uo pipefail
 OUT=gpurun_out/${1:-mls}
 mkdir -p "$OUT"
 for rep in 1 2; do
-  for m in 8 16 32 64 100000; do
+  for m in ${MLS:-8 16 32 64 100000}; do
     S2LC_SOLO_MAXLIVE=$m timeout -k 10 120 python3 tools/c5run.py C5 C5wide H174 > "$OUT/m$m.$rep.jsonl" 2> "$OUT/m$m.$rep.err" || exit $?
     echo "$rep maxlive=$m $(python3 -c "import json; print([(d['name'], d['warm_s'], round(d['level_solo_ms'],1), d['level_solo_rounds']) for d in map(json.loads, open('$OUT/m$m.$rep.jsonl'))])")"
   done
