@@ -567,3 +567,28 @@ def test_concurrent_contexts_persistent_rounds():
     res = s2.Checker(devices=[0, 0]).check_many([hs["H174"], hs["H212"]])
     assert [r.verdict for r in res] == [rc[n]["0"]["verdict"] for n in names]
     assert [r.rounds for r in res] == [rc[n]["0"]["rounds"] for n in names]
+
+
+@pytest.mark.parametrize("mode", ["default", "no_solo", "no_persist"])
+def test_budget_inside_a_one_configuration_stretch(mode, monkeypatch):
+    """The configuration budget trips inside a stretch of one-configuration
+    rounds (H174 round 5,000 of 10,285; the solo rounds close such rounds on
+    registers and hold the budget as a count of rounds left): Unknown (budget)
+    at the same round in every mapping, one round later per configuration of
+    budget, with the committed counts before it."""
+    from s2_verification_amd import workloads as W
+    _set_mode(monkeypatch, mode)
+    ref = golden("hard_round_counts.json")["H174"]
+    assert config_digest("H174") == ref["digest"], "simulator output changed: regenerate the fixture"
+    want = ref["0"]["counts"]
+    r = next(i for i in range(5000, len(want) - 20) if all(c == 1 for c in want[i - 20:i + 20]))
+    cum = sum(want[:r + 1])
+    h = W.config_history("H174")
+    for extra in (0, 1, 2):
+        c = s2.Checker(round_counts=True, max_configs=cum - 1 + extra, engine=s2.ENGINE_LEVEL)
+        b = c.batch([h])
+        res = b.check(with_witness=False)[0]
+        assert res.verdict == s2.Unknown and res.reason == "budget", (extra, res)
+        got = b.round_counts(0)
+        assert res.rounds == r + extra and len(got) == r + extra, (extra, res.rounds, len(got), r)
+        assert got == want[:len(got)], extra
