@@ -241,6 +241,14 @@ struct DevBatch {
   size_t lit_bytes = 0, lit_mem_bytes = 0;
   bool lit_dev_ready = false;
   bool force_reset = false;  // the next run must zero its counters with the reset dispatch
+  // batch_run's engine routing of this load (the same for every run until
+  // the key changes: the engine after the environment's override and
+  // S2LC_MIDK_LEVEL_MAX), and the device's CU count: a C4 run's host
+  // preparation was ~26 us of routing loops and attribute queries per run
+  bool route_valid = false;
+  uint32_t route_engine = 0, route_midk_max = 0, route_n_forced = 0;
+  std::vector<uint32_t> route_todo, route_level;
+  int route_dev = -1, route_n_cu = 0;
   uint32_t lit_chunk = 1;  // literal histories per launch (their slices share one buffer)
   unsigned long long* agg = nullptr;   // device: per packed launch, 8 totals (pack_kernel PackAgg)
   unsigned long long* h_agg = nullptr; // pinned copy

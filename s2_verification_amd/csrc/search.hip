@@ -190,6 +190,7 @@ int batch_upload(DevBatch& b, const std::vector<const History*>& hs, uint32_t re
   b.lit_ev.clear();
   b.lit_dev_ready = false;
   b.rc_valid = false;
+  b.route_valid = false;
   uint32_t kmax_needed = 1;
   size_t n_recs = 0, n_pool = 0, n_cs = 0;
   uint64_t moves_total = 0;
@@ -483,8 +484,12 @@ int batch_run(DevBatch& b, hipStream_t stream, const RunOpts& ro, RunStats& st, 
   const bool witness = ro.witness;
   int dev = 0;
   HIPCHK(hipGetDevice(&dev));
-  int n_cu = 256;
-  (void)hipDeviceGetAttribute(&n_cu, hipDeviceAttributeMultiprocessorCount, dev);
+  if (b.route_dev != dev) {
+    b.route_n_cu = 256;
+    (void)hipDeviceGetAttribute(&b.route_n_cu, hipDeviceAttributeMultiprocessorCount, dev);
+    b.route_dev = dev;
+  }
+  const int n_cu = b.route_n_cu;
   b.rc_valid = false;
 
   // Counters, by run parity: [0..15] work counters, [16..17] deadline,
@@ -542,8 +547,35 @@ int batch_run(DevBatch& b, hipStream_t stream, const RunOpts& ro, RunStats& st, 
   // results) or fixed on the host: no reset dispatch; the first packed launch
   // zeroes the next run's counters. Otherwise one dispatch resets the
   // results and zeroes both counter sets.
-  uint32_t n_forced = 0;
-  for (uint32_t i = 0; i < b.n_hist; ++i) n_forced += b.forced[i] ? 1u : 0u;
+  uint32_t midk_level_max = 8;
+  if (const char* e = getenv("S2LC_MIDK_LEVEL_MAX")) midk_level_max = (uint32_t)strtoul(e, nullptr, 10);
+  if (!b.route_valid || b.route_engine != engine || b.route_midk_max != midk_level_max) {
+    // the histories of each engine, LPT order
+    b.route_todo.clear();   // workgroup passes
+    b.route_level.clear();  // device-wide level search
+    b.route_n_forced = 0;
+    for (uint32_t i = 0; i < b.n_hist; ++i) b.route_n_forced += b.forced[i] ? 1u : 0u;
+    const bool use_pack_r = engine == S2LC_ENGINE_AUTO;
+    // A few histories with 32 < K <= 128 go to the level search too: one
+    // workgroup per history (search_kernel) pays every round's latency in one
+    // workgroup, while the level search runs each round on the whole device
+    // (H96: 182 ms against 14 ms); a batch of many of them keeps the workgroup
+    // engine, which checks them side by side. S2LC_MIDK_LEVEL_MAX overrides
+    // the count (default 8).
+    uint32_t n_midk = 0;
+    for (uint32_t i : b.lpt)
+      if (b.h_hist[i].K > 32 && b.h_hist[i].K <= 128) ++n_midk;
+    const bool midk_level = engine == S2LC_ENGINE_AUTO && n_midk <= midk_level_max;
+    for (uint32_t i : b.lpt) {
+      const uint32_t K = b.h_hist[i].K;
+      if (engine == S2LC_ENGINE_LEVEL || K > 128 || (midk_level && K > 32)) b.route_level.push_back(i);
+      else if (!use_pack_r || K > 32 || !(b.h_hist[i].flags & H_TAIL32)) b.route_todo.push_back(i);
+    }
+    b.route_engine = engine;
+    b.route_midk_max = midk_level_max;
+    b.route_valid = true;
+  }
+  const uint32_t n_forced = b.route_n_forced;
   const uint32_t n_packed_all = b.n_pack8 + b.n_pack16 + b.n_pack32;
   // (force_reset: a run that flipped the parity but returned before it had
   // enqueued the zeroing of the other set leaves that set unzeroed)
@@ -577,27 +609,10 @@ int batch_run(DevBatch& b, hipStream_t stream, const RunOpts& ro, RunStats& st, 
     if (rc) return rc;
   }
 
-  // the histories of each engine, LPT order
-  std::vector<uint32_t> todo;   // workgroup passes
-  std::vector<uint32_t> level;  // device-wide level search
+  // the histories of each engine, LPT order (the cached routing)
+  std::vector<uint32_t> todo = b.route_todo;    // workgroup passes
+  const std::vector<uint32_t>& level = b.route_level;  // device-wide level search
   const bool use_pack = engine == S2LC_ENGINE_AUTO;
-  // A few histories with 32 < K <= 128 go to the level search too: one
-  // workgroup per history (search_kernel) pays every round's latency in one
-  // workgroup, while the level search runs each round on the whole device
-  // (H96: 182 ms against 14 ms); a batch of many of them keeps the workgroup
-  // engine, which checks them side by side. S2LC_MIDK_LEVEL_MAX overrides
-  // the count (default 8).
-  uint32_t midk_level_max = 8;
-  if (const char* e = getenv("S2LC_MIDK_LEVEL_MAX")) midk_level_max = (uint32_t)strtoul(e, nullptr, 10);
-  uint32_t n_midk = 0;
-  for (uint32_t i : b.lpt)
-    if (b.h_hist[i].K > 32 && b.h_hist[i].K <= 128) ++n_midk;
-  const bool midk_level = engine == S2LC_ENGINE_AUTO && n_midk <= midk_level_max;
-  for (uint32_t i : b.lpt) {
-    const uint32_t K = b.h_hist[i].K;
-    if (engine == S2LC_ENGINE_LEVEL || K > 128 || (midk_level && K > 32)) level.push_back(i);
-    else if (!use_pack || K > 32 || !(b.h_hist[i].flags & H_TAIL32)) todo.push_back(i);
-  }
   // histories settled by pack_kernel<8> / <16> (roofline accounting of those kernels)
   std::vector<uint8_t> pack_done(b.n_hist, 0);  // 8 or 16: the kernel that settled it
   const uint32_t n_packed = b.n_pack8 + b.n_pack16 + b.n_pack32;
