@@ -361,6 +361,12 @@ typedef struct s2lc_batch_stats {
   uint32_t _pad5;
 } s2lc_batch_stats;
 int s2lc_batch_stats_get(const s2lc_batch* b, s2lc_batch_stats* out);
+/* Totals over every successful s2lc_batch_run of b since it was created:
+ * runs, and the sums of their kernel_ms / pack16_ms / pack8_ms (a caller that
+ * times many runs reads these once before and once after, instead of the
+ * stats after every run). Any pointer may be NULL. */
+int s2lc_batch_run_totals(const s2lc_batch* b, uint64_t* runs, double* kernel_ms_sum, double* pack16_ms_sum,
+                          double* pack8_ms_sum);
 /* With S2LC_F_ROUND_COUNTS: the unique-configuration count of each completed
  * round of history i's last search, rounds 0 .. *n-1 (round 0 = the closed
  * initial configuration). With out == NULL only *n is set. */

@@ -188,6 +188,8 @@ SIGNATURES = [
     ("s2lc_batch_results_flat", ctypes.c_int, [_P, _P, _P, _P, _P, _P, _P, ctypes.c_size_t, _P]),
     ("s2lc_batch_free", None, [_P]),
     ("s2lc_batch_stats_get", ctypes.c_int, [_P, ctypes.POINTER(c_batch_stats)]),
+    ("s2lc_batch_run_totals", ctypes.c_int, [_P, ctypes.POINTER(ctypes.c_uint64), ctypes.POINTER(ctypes.c_double),
+                                             ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ctypes.c_double)]),
     ("s2lc_batch_round_counts", ctypes.c_int, [_P, ctypes.c_size_t, ctypes.POINTER(ctypes.c_uint32), ctypes.c_size_t,
                                                ctypes.POINTER(ctypes.c_size_t)]),
     ("s2lc_device_fold", ctypes.c_int, [_P, ctypes.POINTER(ctypes.c_uint64), ctypes.POINTER(ctypes.c_uint64),
@@ -641,6 +643,14 @@ class Batch:
         s = c_batch_stats()
         lib().s2lc_batch_stats_get(self._b, ctypes.byref(s))
         return {k: getattr(s, k) for k, _ in c_batch_stats._fields_}
+
+    def run_totals(self) -> dict:
+        """s2lc_batch_run_totals: runs so far and the sums of their kernel /
+        pack_kernel<16> / pack_kernel<8> milliseconds."""
+        n = ctypes.c_uint64()
+        k, p16, p8 = ctypes.c_double(), ctypes.c_double(), ctypes.c_double()
+        lib().s2lc_batch_run_totals(self._b, ctypes.byref(n), ctypes.byref(k), ctypes.byref(p16), ctypes.byref(p8))
+        return {"runs": n.value, "kernel_ms": k.value, "pack16_ms": p16.value, "pack8_ms": p8.value}
 
 
 class Checker:

@@ -69,6 +69,9 @@ struct s2lc_batch {
   RunStats stats;
   bool ran = false;
   bool witness = false;
+  // s2lc_batch_run_totals
+  uint64_t runs = 0;
+  double kernel_ms_sum = 0, pack16_ms_sum = 0, pack8_ms_sum = 0;
 };
 
 static void set_err(char* err, size_t errlen, const std::string& msg) {
@@ -592,6 +595,10 @@ int s2lc_batch_run(s2lc_ctx* c, s2lc_batch* b) {
     if (rc) { c->err = e; return rc; }
     b->ran = true;
     b->witness = ro.witness;
+    b->runs++;
+    b->kernel_ms_sum += b->stats.kernel_ms;
+    b->pack16_ms_sum += b->stats.pack16_ms;
+    b->pack8_ms_sum += b->stats.pack8_ms;
     return 0;
   } catch (...) {
     c->err = "internal error";
@@ -673,6 +680,16 @@ int s2lc_batch_check(s2lc_ctx* c, s2lc_batch* b, s2lc_result* out) {
   int rc = s2lc_batch_run(c, b);
   if (rc) return rc;
   return s2lc_batch_results(c, b, out, 1);
+}
+
+int s2lc_batch_run_totals(const s2lc_batch* b, uint64_t* runs, double* kernel_ms_sum, double* pack16_ms_sum,
+                          double* pack8_ms_sum) {
+  if (!b) return S2LC_EINVAL;
+  if (runs) *runs = b->runs;
+  if (kernel_ms_sum) *kernel_ms_sum = b->kernel_ms_sum;
+  if (pack16_ms_sum) *pack16_ms_sum = b->pack16_ms_sum;
+  if (pack8_ms_sum) *pack8_ms_sum = b->pack8_ms_sum;
+  return 0;
 }
 
 int s2lc_batch_stats_get(const s2lc_batch* b, s2lc_batch_stats* out) {
