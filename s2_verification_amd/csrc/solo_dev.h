@@ -117,6 +117,33 @@ __device__ __forceinline__ uint64_t uni64(uint64_t v) {
   return ((uint64_t)uni32((uint32_t)(v >> 32)) << 32) | uni32((uint32_t)v);
 }
 
+// Wave reductions that finish with row broadcasts (row_bcast:15 into rows 1
+// and 3, row_bcast:31 into rows 2 and 3: lane 63 holds the result, one
+// readlane) instead of four readlanes and scalar combines
+// (profiles/r06/solo_rbcast_ab.txt)
+template <int CTRL, int ROWS>
+__device__ __forceinline__ uint32_t solo_bcast(uint32_t v, uint32_t old) {
+  return (uint32_t)__builtin_amdgcn_update_dpp((int)old, (int)v, CTRL, ROWS, 0xF, false);
+}
+__device__ __forceinline__ uint32_t solo_wave_min(uint32_t v) {
+  v = min(v, lv_dpp<0xB1>(v));
+  v = min(v, lv_dpp<0x4E>(v));
+  v = min(v, lv_dpp<0x124>(v));
+  v = min(v, lv_dpp<0x128>(v));
+  v = min(v, solo_bcast<0x142, 0xA>(v, v));
+  v = min(v, solo_bcast<0x143, 0xC>(v, v));
+  return rl(v, 63);
+}
+__device__ __forceinline__ uint32_t solo_wave_sum(uint32_t c) {
+  c += lv_dpp<0xB1>(c);
+  c += lv_dpp<0x4E>(c);
+  c += lv_dpp<0x124>(c);
+  c += lv_dpp<0x128>(c);
+  c += solo_bcast<0x142, 0xA>(c, 0u);
+  c += solo_bcast<0x143, 0xC>(c, 0u);
+  return rl(c, 63);
+}
+
 // (smallest, second smallest) of v over the wave's chain slots (a value held
 // by two chains is both), wave-uniform
 template <int CTRL>
@@ -137,15 +164,18 @@ __device__ __forceinline__ void wave_min2_32(const uint32_t (&v)[NQ], uint32_t& 
   min2_step32<0x4E>(a, b);
   min2_step32<0x124>(a, b);
   min2_step32<0x128>(a, b);
-  uint32_t x1 = 0xFFFFFFFFu, x2 = 0xFFFFFFFFu;
-#pragma unroll
-  for (int row = 0; row < 4; ++row) {
-    const uint32_t ra = rl(a, 16 * row), rb = rl(b, 16 * row);
-    x2 = min(max(x1, ra), min(x2, rb));
-    x1 = min(x1, ra);
+  {  // (rows a bcast does not write combine with (INF, INF): unchanged)
+    const uint32_t oa = solo_bcast<0x142, 0xA>(a, 0xFFFFFFFFu), ob = solo_bcast<0x142, 0xA>(b, 0xFFFFFFFFu);
+    b = min(max(a, oa), min(b, ob));
+    a = min(a, oa);
   }
-  m1 = x1;
-  m2 = x2;
+  {
+    const uint32_t oa = solo_bcast<0x143, 0xC>(a, 0xFFFFFFFFu), ob = solo_bcast<0x143, 0xC>(b, 0xFFFFFFFFu);
+    b = min(max(a, oa), min(b, ob));
+    a = min(a, oa);
+  }
+  m1 = rl(a, 63);
+  m2 = rl(b, 63);
 }
 
 // Closure keys of a head at the child's state (tail t, hash h): its call
@@ -499,12 +529,7 @@ __device__ __attribute__((noinline)) uint32_t lv_solo_wave(const SoloArgs pa, Lv
     {
       // live moves of the round and P1-dead opt children (wave-wide sums of
       // the per-lane counts, one reduction: 16 bits each, at most 320)
-      uint32_t c = (uint32_t)__popc(b_live) | ((uint32_t)__popc(b_dead) << 16);
-      c += lv_dpp<0xB1>(c);
-      c += lv_dpp<0x4E>(c);
-      c += lv_dpp<0x124>(c);
-      c += lv_dpp<0x128>(c);
-      const uint32_t sum = rl(c, 0) + rl(c, 16) + rl(c, 32) + rl(c, 48);
+      const uint32_t sum = solo_wave_sum((uint32_t)__popc(b_live) | ((uint32_t)__popc(b_dead) << 16));
       tot = sum & 0xFFFFu;
       n_dead = sum >> 16;
       if (tot > p.max_live) {
@@ -625,7 +650,7 @@ __device__ __attribute__((noinline)) uint32_t lv_solo_wave(const SoloArgs pa, Lv
             advb |= ek[q] < mprev ? 1u << q : 0u;
             bad |= (uint32_t)((dk[q] < mprev) | (p1 & (csuf[q] < ct)));
           }
-          minret = wave_min_u32(mr);
+          minret = solo_wave_min(mr);
 #ifdef S2LC_PROF
           if (lane == 0) S.pc[4] += 1;
 #endif
