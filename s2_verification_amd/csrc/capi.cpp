@@ -19,6 +19,7 @@
 #include "history.h"
 #include "s2lincheck.h"
 #include "search.h"
+#include "cert_prof.h"
 #include "host_par.h"
 
 namespace s2lc {
@@ -383,6 +384,7 @@ namespace {
 int collect_results(DevBatch& B, const RunStats& stats, bool witness_recorded, s2lc_result* out, int with_witness,
                     std::string& err, int64_t* flat_ids = nullptr, const uint64_t* flat_offs = nullptr) {
   const bool want_w = with_witness && witness_recorded;
+  CP_DECL(tc0);
   {
     const int rc = batch_host_results(B, err);
     if (rc) return rc;
@@ -393,6 +395,7 @@ int collect_results(DevBatch& B, const RunStats& stats, bool witness_recorded, s
   }
   // test hook: corrupt every Ok witness before certification (the failure path
   // of the certificate must be loud; tests/test_gpu.py)
+  CP_LAP(5, tc0);
   const char* fault = getenv("S2LC_FAULT_WITNESS");
   const bool corrupt = fault && fault[0] == '1';
   std::atomic<uint32_t> next{0};
@@ -452,7 +455,9 @@ int collect_results(DevBatch& B, const RunStats& stats, bool witness_recorded, s
           continue;
         }
         if (r.verdict == V_OK) {
+          CP_DECL(th0);
           const bool ok = rebuild_and_replay(H, moves, n_moves, r.p4 != 0, order, ident);
+          CP_LAP(3, th0);
           if (!ok) {
             o.verdict = S2LC_UNKNOWN;
             o.reason = S2LC_R_WITNESS_INVALID;
@@ -463,6 +468,10 @@ int collect_results(DevBatch& B, const RunStats& stats, bool witness_recorded, s
             int64_t* w = flat_ids + flat_offs[i];
             for (size_t k = 0; k < order.size(); ++k) w[k] = H.op_ids[order[k]];
             o.witness_len = (uint32_t)order.size();
+            CP_LAP(4, th0);
+#ifdef S2LC_CERT_PROF
+            g_cert_prof[7].fetch_add(1);
+#endif
             continue;
           }
           o.witness = (int64_t*)malloc(sizeof(int64_t) * (order.size() ? order.size() : 1));
@@ -495,6 +504,12 @@ int collect_results(DevBatch& B, const RunStats& stats, bool witness_recorded, s
   for (int t = 1; t < n_threads; ++t) ts.emplace_back(work);
   work();
   for (auto& t : ts) t.join();
+#ifdef S2LC_CERT_PROF
+  CP_LAP(6, tc0);
+  fprintf(stderr, "{\"cert_prof\": [");
+  for (int k = 0; k < 16; ++k) fprintf(stderr, "%s%llu", k ? ", " : "", (unsigned long long)g_cert_prof[k].exchange(0));
+  fprintf(stderr, "], \"threads\": %d}\n", n_threads);
+#endif
   if (oom) { err = "out of memory"; return S2LC_ENOMEM; }
   if (invalid) { err = "an Ok witness failed CPU-model certification (checker bug)"; return S2LC_EWITNESS; }
   return 0;

@@ -10,8 +10,16 @@
 #include <vector>
 
 #include "search.h"
+#include "cert_prof.h"
+
+static_assert(s2lc::OPF_CLS_E == 0x100u && s2lc::OPF_FAIL == 0x4u && s2lc::OPF_HAS_HASH == 0x20u,
+              "witness.cpp's head bits");
 
 namespace s2lc {
+
+#ifdef S2LC_CERT_PROF
+std::atomic<uint64_t> g_cert_prof[16];
+#endif
 
 namespace {
 
@@ -46,6 +54,15 @@ bool claim_ok(const OpRec& r, const State& s, const uint64_t* pool, bool applied
 // outcome the linearization claims, from the replay's own state.
 inline bool replay_step(const History& h, uint32_t op, uint8_t ident, State& s) {
   const OpRec& r = h.recs[h.op_rec[op]];
+  const uint32_t f = r.flags;
+  if (f & OPF_CLS_E) {
+    // Step(s) is {s} or {} (main.go:283-285, 320-331): ident_legal, without a
+    // branch per field (the closure takes these ops in data-dependent kinds)
+    const int any = (f & OPF_KIND_MASK) == 0;  // definite append failure
+    const int hash_ok = !(f & OPF_HAS_HASH) | (s.hash == r.out_hash);
+    const int tail_ok = ((f & OPF_FAIL) != 0) | (s.tail == r.out_tail);
+    return any | (hash_ok & tail_ok);
+  }
   // the outcome this linearization claims: the optimistic successor for an
   // append taken as applied, the unchanged state otherwise
   const bool applied = !ident && !(r.flags & OPF_CLS_E) && (r.flags & OPF_KIND_MASK) == 0;
@@ -61,28 +78,41 @@ void prefetch_range(const void* p, size_t bytes) {
 }
 
 // Per-thread scratch of the rebuild (no allocation per history once warm).
-struct Head {  // a chain's head, as the closure tests it
-  uint32_t call, ret;
-  uint32_t need;  // bit 0: identity class; bit 1: tail must match; bit 2: hash must match
-  uint32_t _pad;
-  uint64_t tail, hash;
-  const OpRec* rec;
+// The chains' heads as the closure tests them, one array per field: a pass's
+// min-return and its "called before mr" test are straight loops over K
+// entries, and only the heads that pass the second get the observation test.
+struct Heads {
+  std::vector<uint32_t> ccall;  // call event of an identity-class head, EV_INF otherwise (never closure-taken)
+  std::vector<uint32_t> ret;
+  std::vector<uint32_t> need;   // bit 1: tail must match; bit 2: hash must match
+  std::vector<uint64_t> tail, hash;
+  std::vector<const OpRec*> rec;
+  void resize(uint32_t K) {
+    ccall.resize(K);
+    ret.resize(K);
+    need.resize(K);
+    tail.resize(K);
+    hash.resize(K);
+    rec.resize(K);
+  }
 };
 struct Scratch {
-  std::vector<Head> head;
+  Heads head;
   std::vector<uint8_t> seen;
 };
 thread_local Scratch t_scr;
 
 // The device's closure and moves over one history, host side. The heads are
-// kept as a small array of what the closure tests (call, return, and the
-// observation an identity op must match), so a closure pass is a short loop
-// with no record loads; a chain's next head is its next record. The
-// linearization is written by index into buffers sized n_ops.
+// kept as what the closure tests (call, return, and the observation an
+// identity op must match), so a closure pass is a few loops with no record
+// loads; a chain's next head is its next record. The linearization is written
+// by index into buffers sized n_ops.
 struct Rebuild {
   const History& h;
   const OpRec* recs;
-  Head* hd;
+  Heads& hd;
+  uint32_t* const ccall;
+  uint32_t* const ret;
   const uint32_t K;
   uint32_t* order;
   uint8_t* ident;
@@ -94,56 +124,85 @@ struct Rebuild {
   // chains in flight together instead of two passes
   bool rep = false, rep_ok = true;
   State rs{0, 0, 0};
-  Rebuild(const History& h_, Head* hd_, uint32_t* ord, uint8_t* id)
-      : h(h_), recs(h_.recs.data()), hd(hd_), K(h_.K), order(ord), ident(id) {
+  Rebuild(const History& h_, Heads& hd_, uint32_t* ord, uint8_t* id)
+      : h(h_), recs(h_.recs.data()), hd(hd_), ccall(hd_.ccall.data()), ret(hd_.ret.data()), K(h_.K), order(ord),
+        ident(id) {
     for (uint32_t q = 0; q < K; ++q) load(q, recs + h.chain_start[q]);
   }
   void load(uint32_t q, const OpRec* r) {
-    Head& x = hd[q];
-    x.rec = r;
-    x.call = r->call_ev;
-    x.ret = r->ret_ev;
+    hd.rec[q] = r;
+    ret[q] = r->ret_ev;
     const uint32_t f = r->flags;
-    uint32_t need = 0;
-    if (f & OPF_CLS_E) {
-      need = 1;
-      if ((f & OPF_KIND_MASK) != 0) {  // read / check-tail (ident_legal)
-        if (!(f & OPF_FAIL)) need |= 2;
-        if (f & OPF_HAS_HASH) need |= 4;
-      }
-    }
-    x.need = need;
-    x.tail = r->out_tail;
-    x.hash = r->out_hash;
+    // read / check-tail (ident_legal): bit 1 unless failed, bit 2 if it carries
+    // a hash; none for an append (bit arithmetic: the kinds come in data order)
+    const uint32_t ce = (f >> 8) & 1u;                          // OPF_CLS_E
+    const uint32_t rd = ce & (uint32_t)((f & OPF_KIND_MASK) != 0);
+    const uint32_t need = rd * ((((f >> 2) & 1u) ^ 1u) << 1 | ((f >> 5) & 1u) << 2);  // OPF_FAIL, OPF_HAS_HASH
+    ccall[q] = ce ? r->call_ev : EV_INF;
+    hd.need[q] = need;
+    hd.tail[q] = r->out_tail;
+    hd.hash[q] = r->out_hash;
   }
   uint32_t min_ret() const {
     uint32_t m = EV_INF;
-    for (uint32_t q = 0; q < K; ++q) m = std::min(m, hd[q].ret);
+    for (uint32_t q = 0; q < K; ++q) m = ret[q] < m ? ret[q] : m;
     return m;
   }
-  bool eligible(const Head& x, uint32_t mr) const {
-    return (x.need & 1) && x.call < mr && (!(x.need & 2) || x.tail == s.tail) && (!(x.need & 4) || x.hash == s.hash);
+  // head q (called before mr) observes the current state
+  bool obs_ok(uint32_t q) const {
+    const uint32_t nd = hd.need[q];
+    const int tail_ok = !(nd & 2) | (hd.tail[q] == s.tail), hash_ok = !(nd & 4) | (hd.hash[q] == s.hash);
+    return tail_ok & hash_ok;
   }
   void take(uint32_t q, uint8_t id) {
-    const OpRec* r = hd[q].rec;
+    const OpRec* r = hd.rec[q];
     order[n] = h.rec_op[(size_t)(r - recs)];
     ident[n] = id;
     if (rep && rep_ok) rep_ok = replay_step(h, order[n], id, rs);
     ++n;
     load(q, r + 1);
   }
-  // legal minimal identity ops, to the fixpoint (search.hip's closure)
+  // legal minimal identity ops, to the fixpoint (search.hip's closure). A pass
+  // holds mr fixed and takes, chain by chain in order, every head that was
+  // called before it and observes the state; a take changes only its own
+  // chain's head, so the heads that pass the call test at the pass's start are
+  // exactly the ones the pass can take. The state is fixed too (identity ops),
+  // so a pass after one that left mr where it was would take nothing: the
+  // fixpoint is reached when a pass takes nothing or mr does not move.
   void close() {
+#ifdef S2LC_CERT_PROF
+    CP_DECL(tq);
+    const uint32_t n0 = n;
+    uint32_t passes = 0;
+    struct Done {
+      uint64_t& t; const uint32_t& n; uint32_t n0; uint32_t& passes;
+      ~Done() { CP_LAP(11, t); CP_CNT(10, n - n0); CP_CNT(9, passes); CP_CNT(8, 1); }
+    } done{tq, n, n0, passes};
+#endif
+    uint32_t mr = min_ret();
     for (;;) {
-      const uint32_t mr = min_ret();
+#ifdef S2LC_CERT_PROF
+      ++passes;
+#endif
       if (mr == EV_INF) return;
       bool changed = false;
-      for (uint32_t q = 0; q < K; ++q)
-        while (eligible(hd[q], mr)) {
-          take(q, 1);
-          changed = true;
+      for (uint32_t q0 = 0; q0 < K; q0 += 64) {
+        const uint32_t nq = K - q0 < 64 ? K - q0 : 64;
+        uint64_t m = 0;
+        for (uint32_t j = 0; j < nq; ++j) m |= (uint64_t)(ccall[q0 + j] < mr) << j;
+        while (m) {
+          const uint32_t q = q0 + (uint32_t)__builtin_ctzll(m);
+          m &= m - 1;
+          while ((ccall[q] < mr) & obs_ok(q)) {
+            take(q, 1);
+            changed = true;
+          }
         }
+      }
       if (!changed) return;
+      const uint32_t mr2 = min_ret();
+      if (mr2 == mr) return;
+      mr = mr2;
     }
   }
 };
@@ -159,20 +218,22 @@ static bool rebuild(const History& h, const uint32_t* moves, uint32_t n_moves, b
   // and in a batch they are cold (last touched by the upload): stream them
   // (and the record-hash pool and record -> op map) into the cache first, with
   // all misses in flight at once, instead of one miss per closure step.
+  CP_DECL(t0);
   prefetch_range(h.recs.data(), h.recs.size() * sizeof(OpRec));
   prefetch_range(h.rec_op.data(), h.rec_op.size() * sizeof(uint32_t));
   prefetch_range(h.pool.data(), h.pool.size() * sizeof(uint64_t));
+  CP_LAP(0, t0);
   order.resize(h.n_ops);
   ident.resize(h.n_ops);
   t_scr.head.resize(h.K);
-  Rebuild c(h, t_scr.head.data(), order.data(), ident.data());
+  Rebuild c(h, t_scr.head, order.data(), ident.data());
   c.rep = replay;
   c.close();
   for (uint32_t m = 0; m < n_moves; ++m) {
     const uint32_t j = moves[m] & 0xFFFFu;
     const bool is_id = moves[m] & MOVE_IDENT;
     if (j >= h.K || c.n >= h.n_ops) { order.resize(c.n); ident.resize(c.n); return false; }
-    const OpRec& r = *c.hd[j].rec;
+    const OpRec& r = *c.hd.rec[j];
     State next;
     if ((r.flags & (OPF_SENTINEL | OPF_CLS_E)) || r.call_ev >= c.min_ret() ||  // a minimal non-identity op
         !claim_ok(r, c.s, h.pool.data(), !is_id, next)) {
@@ -186,13 +247,14 @@ static bool rebuild(const History& h, const uint32_t* moves, uint32_t n_moves, b
   }
   order.resize(c.n);
   ident.resize(c.n);
+  CP_LAP(1, t0);
   if (partial) return true;
   if (order.size() != h.n_ops) {
     if (!p4) return false;
     // P4 completion: nothing left constrains the state; finish in return order.
     std::vector<uint32_t> rest;
     for (uint32_t q = 0; q < h.K; ++q)
-      for (const OpRec* x = c.hd[q].rec; !(x->flags & OPF_SENTINEL); ++x) rest.push_back(h.rec_op[(size_t)(x - c.recs)]);
+      for (const OpRec* x = c.hd.rec[q]; !(x->flags & OPF_SENTINEL); ++x) rest.push_back(h.rec_op[(size_t)(x - c.recs)]);
     std::sort(rest.begin(), rest.end(), [&](uint32_t a, uint32_t b) { return h.op_ret[a] < h.op_ret[b]; });
     order.insert(order.end(), rest.begin(), rest.end());
     ident.resize(order.size(), 1);
@@ -210,8 +272,17 @@ bool rebuild_linearization(const History& h, const uint32_t* moves, uint32_t n_m
 
 bool rebuild_and_replay(const History& h, const uint32_t* moves, uint32_t n_moves, bool p4,
                         std::vector<uint32_t>& order, std::vector<uint8_t>& ident) {
+#ifdef S2LC_CERT_PROF
+  static const bool norep = getenv("S2LC_CERT_NOREPLAY") != nullptr;
+  if (!rebuild(h, moves, n_moves, p4, order, ident, false, !norep)) return false;
+  CP_DECL(t0);
+  const bool ok = real_time_ok(h, order.data(), order.size());
+  CP_LAP(2, t0);
+  return ok;
+#else
   return rebuild(h, moves, n_moves, p4, order, ident, false, true) &&
          real_time_ok(h, order.data(), order.size());
+#endif
 }
 
 // (The op's record is recs[op_rec[d]]: History::finalize builds it with
