@@ -162,6 +162,34 @@ struct Rebuild {
     ++n;
     load(q, r + 1);
   }
+  // record x (a chain's next head) is an identity op called before mr that
+  // observes the state: the test obs_ok makes on a loaded head
+  bool ident_ok(const OpRec& x, uint32_t mr) const {
+    const uint32_t f = x.flags;
+    const int ce = (f & OPF_CLS_E) != 0, before = x.call_ev < mr, rd = (f & OPF_KIND_MASK) != 0;
+    const int tail_ok = !rd | ((f & OPF_FAIL) != 0) | (x.out_tail == s.tail);
+    const int hash_ok = !rd | ((f & OPF_HAS_HASH) == 0) | (x.out_hash == s.hash);
+    return ce & before & tail_ok & hash_ok;
+  }
+  // the run of chain q's identity ops a pass takes, read straight from the
+  // chain's consecutive records, then the head loaded once (a sentinel ends
+  // every run: it is not identity-class)
+  bool take_run(uint32_t q, uint32_t mr) {
+    if (!((ccall[q] < mr) & obs_ok(q))) return false;
+    const OpRec* r = hd.rec[q];
+    const uint32_t* ro = h.rec_op.data() + (size_t)(r - recs);
+    size_t k = 0;
+    do {
+      const uint32_t op = ro[k];
+      order[n] = op;
+      ident[n] = 1;
+      if (rep) rep_ok &= replay_step(h, op, 1, rs);
+      ++n;
+      ++k;
+    } while (ident_ok(r[k], mr));
+    load(q, r + k);
+    return true;
+  }
   // legal minimal identity ops, to the fixpoint (search.hip's closure). A pass
   // holds mr fixed and takes, chain by chain in order, every head that was
   // called before it and observes the state; a take changes only its own
@@ -193,10 +221,7 @@ struct Rebuild {
         while (m) {
           const uint32_t q = q0 + (uint32_t)__builtin_ctzll(m);
           m &= m - 1;
-          while ((ccall[q] < mr) & obs_ok(q)) {
-            take(q, 1);
-            changed = true;
-          }
+          if (take_run(q, mr)) changed = true;
         }
       }
       if (!changed) return;
