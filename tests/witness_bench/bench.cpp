@@ -4,6 +4,8 @@
 // search written here (the GPU search's rounds, no reductions but the
 // E-closure), so the timing needs no GPU:
 //   make -C tests/witness_bench && tests/witness_bench/bench [n]
+// Exit status 0 when every witness certifies and every broken move list is
+// rejected (tests/test_witness_cpu.py runs it at a small n).
 #include <chrono>
 #include <map>
 #include <stdio.h>
@@ -143,6 +145,30 @@ int main(int argc, char** argv) {
       bad += s2lc_witness_from_moves(hs[i], mv[i].data(), mv[i].size(), 0, ids.data(), ids.size()) != 0;
     const double s = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
     printf("{\"histories\": %zu, \"us_per_history\": %.2f, \"failed\": %d}\n", hs.size(), 1e6 * s / hs.size(), bad);
+  }
+  {  // a digest of every certified witness (op ids in order), to compare builds
+    uint64_t fnv = 0xcbf29ce484222325ull;
+    for (size_t i = 0; i < hs.size(); ++i) {
+      if (s2lc_witness_from_moves(hs[i], mv[i].data(), mv[i].size(), 0, ids.data(), ids.size()) != 0) { ++bad; continue; }
+      for (uint32_t k = 0; k < hs[i]->h.n_ops; ++k) fnv = (fnv ^ (uint64_t)ids[k]) * 0x100000001b3ull;
+    }
+    printf("{\"witness_digest\": \"%016llx\"}\n", (unsigned long long)fnv);
+  }
+  {  // broken move lists must fail certification: an unknown chain first, or the last move dropped
+    int negatives = 0, rejected = 0;
+    for (size_t i = 0; i < hs.size() && i < 100; ++i) {
+      if (mv[i].empty()) continue;
+      std::vector<uint32_t> m = mv[i];
+      m[0] = 0xFFFFu;
+      ++negatives;
+      rejected += s2lc_witness_from_moves(hs[i], m.data(), m.size(), 0, ids.data(), ids.size()) != 0;
+      m = mv[i];
+      m.pop_back();
+      ++negatives;
+      rejected += s2lc_witness_from_moves(hs[i], m.data(), m.size(), 0, ids.data(), ids.size()) != 0;
+    }
+    printf("{\"negatives\": %d, \"rejected\": %d}\n", negatives, rejected);
+    bad += negatives - rejected;
   }
   for (auto* h : hs) s2lc_history_free(h);
   return bad != 0;
